@@ -1,0 +1,232 @@
+"""Generate the golden vectors that pin the oracle to the reference.
+
+Runs ONLY in the build container, where ``/root/reference`` exists: it loads the reference's
+arch files by file path (importlib, no package import, nothing copied into this repo), fills them
+with the deterministic synthetic weights of ``turtlevsr_amd.synthetic`` and writes input/output
+tensors (data only) as ``.npz`` files next to this script.
+
+    python tests/golden/gen_golden.py
+
+Outputs (all float32, loadable with ``numpy.load(allow_pickle=False)``):
+
+* ``state_dict_keys.json``   - name -> shape for the GoPro Turtle_t1 and TurtleSuper_t1 models;
+* ``clip_*.npz``             - whole-model causal clips (tiny widths, and GoPro widths at 64x64):
+                               every frame's output, the last frame's caches in full (tiny) or as
+                               checksums + fixed samples (GoPro);
+* ``block_*.npz``            - per-block vectors (LayerNorm, ReducedAttn, FFW, GFFW, Channel,
+                               FHR with cache, SAB with cache, CHM with cache) at GoPro widths.
+"""
+from __future__ import annotations
+
+import importlib.util
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import yaml
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from turtlevsr_amd.synthetic import synthetic_frames, synthetic_state_dict  # noqa: E402
+
+REF = "/root/reference"
+OPT_GOPRO = os.path.join(REF, "options", "Turtle_Deblur_Gopro.yml")
+
+
+def load_by_path(rel: str, name: str):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, rel))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def gopro_opt() -> dict:
+    with open(OPT_GOPRO) as f:
+        return yaml.safe_load(f)
+
+
+def tiny_opt(**over) -> dict:
+    o = gopro_opt()
+    o.update(dim=16, Enc_blocks=[1, 1, 2], Middle_blocks=2, Dec_blocks=[2, 1, 2], num_refinement_blocks=1)
+    o.update(over)
+    return o
+
+
+ARCH_KEYS = [
+    "n_colors", "dim", "Enc_blocks", "Middle_blocks", "Dec_blocks", "num_refinement_blocks",
+    "ffn_expansion_factor", "bias", "LayerNorm_type", "num_heads_blks", "use_both_input",
+    "num_frames_tocache", "num_heads",
+] + [f"{p}{i}_attn_type{j}" for p in ("encoder", "decoder") for i in (1, 2, 3) for j in (1, 2)] + [
+    f"{p}{i}_ffw_type" for p in ("encoder", "decoder") for i in (1, 2, 3)] + [
+    "latent_attn_type1", "latent_attn_type2", "latent_attn_type3", "latent_ffw_type",
+    "refinement_attn_type1", "refinement_attn_type2", "refinement_ffw_type"]
+
+
+def arch_opt(o: dict) -> dict:
+    return {k: o[k] for k in ARCH_KEYS if k in o}
+
+
+def fill(model: torch.nn.Module, seed: int = 0):
+    shapes = {k: tuple(v.shape) for k, v in model.state_dict().items()}
+    sd = synthetic_state_dict(shapes, seed)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+    return shapes
+
+
+def summary(t: torch.Tensor, nsamp: int = 256) -> dict:
+    a = t.detach().double().reshape(-1).numpy()
+    idx = np.random.default_rng(123).integers(0, a.size, nsamp)
+    return dict(shape=np.array(t.shape, np.int64), sum=np.float64(a.sum()),
+                abssum=np.float64(np.abs(a).sum()), sqsum=np.float64((a * a).sum()),
+                idx=idx.astype(np.int64), samp=a[idx].astype(np.float32))
+
+
+def run_clip(model, clip: np.ndarray, full_caches: bool):
+    """Causal loop of video_restoration_model.py:85-92 on the reference model."""
+    x = torch.from_numpy(clip)
+    kc = vc = None
+    rec = {}
+    with torch.no_grad():
+        for j in range(x.shape[1]):
+            inp = torch.stack([x[:, max(j - 1, 0)], x[:, j]], dim=1)
+            out, kc, vc = model(inp, kc, vc)
+            rec[f"out{j}"] = out.numpy().astype(np.float32)
+            for which, lst in (("k", kc), ("v", vc)):
+                for i, t in enumerate(lst):
+                    if t is None:
+                        continue
+                    key = f"f{j}_{which}{i}"
+                    if full_caches and j == x.shape[1] - 1:
+                        rec[key] = t.numpy().astype(np.float32)
+                    for sk, sv in summary(t).items():
+                        rec[f"{key}__{sk}"] = sv
+    return rec
+
+
+def save(name: str, arrays: dict, meta: dict):
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
+    with open(os.path.join(HERE, name + ".json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    print("wrote", name, sum(v.nbytes for v in arrays.values() if hasattr(v, "nbytes")) / 1e6, "MB raw")
+
+
+def gen_clips(t1, sr):
+    torch.set_num_threads(8)
+    jobs = [
+        # name, module, opt, clip shape, full caches, seed
+        ("clip_tiny_64", t1, tiny_opt(), (1, 5, 3, 64, 64), True, 1),
+        ("clip_tiny_ragged", t1, tiny_opt(), (2, 3, 3, 40, 72), False, 2),
+        ("clip_tiny_both", t1, tiny_opt(use_both_input=True), (1, 2, 3, 64, 64), False, 3),
+        ("clip_tiny_biasfree", t1, tiny_opt(LayerNorm_type="BiasFree"), (1, 2, 3, 64, 64), False, 4),
+        ("clip_tiny_sr", sr, tiny_opt(), (1, 3, 3, 16, 24), False, 5),
+        ("clip_gopro_64", t1, gopro_opt(), (1, 4, 3, 64, 64), False, 6),
+    ]
+    for name, mod, opt, shape, full, seed in jobs:
+        torch.manual_seed(0)
+        model = mod.make_model(opt).eval()
+        fill(model, seed)
+        clip = synthetic_frames(shape, seed, name="frames")
+        rec = run_clip(model, clip, full)
+        rec["clip"] = clip
+        save(name, rec, dict(opt=arch_opt(opt), seed=seed, sr=mod is sr, shape=list(shape)))
+
+
+def gen_blocks(t1):
+    torch.set_num_threads(8)
+    rng_seed = 100
+
+    def mk(cls, *args, **kw):
+        m = cls(*args, **kw).eval()
+        shapes = {"blk." + k: tuple(v.shape) for k, v in m.state_dict().items()}
+        sd = synthetic_state_dict(shapes, rng_seed)
+        m.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in sd.items()}, strict=True)
+        return m
+
+    def frames(shape, name):
+        return torch.from_numpy(synthetic_frames(shape, rng_seed, name=name) * 2.0 - 1.0)
+
+    with torch.no_grad():
+        out = {}
+        x = frames((1, 64, 16, 24), "ln_x")
+        m = mk(t1.LayerNorm, 64, "WithBias")
+        out["ln_x"], out["ln_y"] = x.numpy(), m(x).numpy()
+        m = mk(t1.LayerNorm, 64, "BiasFree")
+        out["lnbf_y"] = m(x).numpy()
+        save("block_layernorm", out, dict(dim=64))
+
+        x = frames((1, 64, 16, 24), "ra_x")
+        out = {"x": x.numpy(), "y": mk(t1.ReducedAttn, 64)(x)[0].numpy()}
+        save("block_reducedattn", out, dict(dim=64))
+
+        x = frames((1, 128, 16, 16), "ffw_x")
+        out = {"x": x.numpy(), "y": mk(t1.FeedForward, 128)(x).numpy()}
+        save("block_ffw", out, dict(dim=128))
+
+        x = frames((1, 256, 8, 12), "gffw_x")
+        out = {"x": x.numpy(), "y": mk(t1.GatedFeedForward, 256, 2.5, False)(x).numpy()}
+        save("block_gffw", out, dict(dim=256, ffe=2.5))
+
+        x = frames((1, 256, 8, 12), "ca_x")
+        out = {"x": x.numpy(), "y": mk(t1.ChannelAttention, 256, 4, False)(x)[0].numpy()}
+        save("block_channel", out, dict(dim=256, heads=4))
+
+        # FHR at latent width with a 2-frame cache (rows = 2 * c / heads)
+        m = mk(t1.FrameHistoryRouter, 512, 8, False, 3)
+        x = frames((1, 512, 4, 6), "fhr_x")
+        kc = torch.nn.functional.normalize(frames((1, 8, 128, 24), "fhr_kc"), dim=-1)
+        vc = frames((1, 8, 128, 24), "fhr_vc")
+        y, k, v = m(x, kc, vc)
+        y0, k0, v0 = m(x)
+        save("block_fhr", {"x": x.numpy(), "kc": kc.numpy(), "vc": vc.numpy(), "y": y.numpy(),
+                           "k": k.numpy(), "v": v.numpy(), "y0": y0.numpy(), "k0": k0.numpy(),
+                           "v0": v0.numpy()}, dict(dim=512, heads=8, ntc=3))
+
+        # SAB (c=32, ws=8) on a 32x24 map -> 4x3 = 12 tokens; 2-frame cache
+        m = mk(t1.StateAlignBlock, 32, 1, False, 2, Scale_patchsize=4)
+        x = frames((1, 32, 32, 24), "sab_x")
+        kc = torch.nn.functional.normalize(frames((1, 2, 1, 12, 64), "sab_kc"), dim=-1)
+        vc = frames((1, 2, 1, 12, 8 * 8 * 32), "sab_vc")
+        y, k, v = m(x, kc, vc)
+        y0, k0, v0 = m(x)
+        save("block_sab", {"x": x.numpy(), "kc": kc.numpy(), "vc": vc.numpy(), "y": y.numpy(),
+                           "k": k.numpy(), "v": v.numpy(), "y0": y0.numpy(), "k0": k0.numpy(),
+                           "v0": v0.numpy()}, dict(dim=32, ws=8, ntc=2))
+
+        # CHM (c=32, 2 heads, ws=4) on a 16x20 map -> 4x5 = 20 tokens; 3-frame cache
+        m = mk(t1.CausalHistoryModel, 32, 2, False, 2, 3)
+        x = frames((1, 32, 16, 20), "chm_x")
+        kc = torch.nn.functional.normalize(frames((1, 3, 1, 20, 64), "chm_kc"), dim=-1)
+        vc = frames((1, 3, 1, 20, 4 * 4 * 32), "chm_vc")
+        y, k, v = m(x, kc, vc)
+        y0, k0, v0 = m(x)
+        save("block_chm", {"x": x.numpy(), "kc": kc.numpy(), "vc": vc.numpy(), "y": y.numpy(),
+                           "k": k.numpy(), "v": v.numpy(), "y0": y0.numpy(), "k0": k0.numpy(),
+                           "v0": v0.numpy()}, dict(dim=32, heads=2, ws=4, ntc=3))
+
+
+def gen_keys(t1, sr):
+    res = {}
+    for name, mod in (("Turtle_t1", t1), ("TurtleSuper_t1", sr)):
+        m = mod.make_model(gopro_opt())
+        res[name] = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    m = t1.make_model(tiny_opt())
+    res["Turtle_t1_tiny"] = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    with open(os.path.join(HERE, "state_dict_keys.json"), "w") as f:
+        json.dump(res, f)
+    print("keys:", {k: len(v) for k, v in res.items()})
+
+
+if __name__ == "__main__":
+    t1 = load_by_path("basicsr/models/archs/turtle_t1_arch.py", "ref_turtle_t1")
+    sr = load_by_path("basicsr/models/archs/turtlesuper_t1_arch.py", "ref_turtlesuper_t1")
+    which = sys.argv[1:] or ["keys", "blocks", "clips"]
+    if "keys" in which:
+        gen_keys(t1, sr)
+    if "blocks" in which:
+        gen_blocks(t1)
+    if "clips" in which:
+        gen_clips(t1, sr)
