@@ -1,0 +1,106 @@
+/* turtle_hip.h - C ABI of libturtle_hip.so, the MI355X (gfx950) Turtle per-frame restoration path.
+ *
+ * This is the drop-in boundary for the reference's arch plug-in
+ *   basicsr/models/archs/turtle_t1_arch.py  (make_model 10-53, Turtle_t1.forward 1045-1132)
+ *   basicsr/models/archs/turtlesuper_t1_arch.py (TurtleSuper_t1.forward 1049-1147)
+ * The reference has no native FFI; these entry points are what its Python module binds (via
+ * ctypes): plain pointers and sizes, device pointers are hipMalloc'd memory
+ * (e.g. torch.Tensor.data_ptr() on a ROCm device), all work is stream-ordered on `stream`.
+ *
+ * Every function returns 0 on success, a negative TURTLE_E* code on failure; the message is
+ * available from turtle_last_error() (thread-local), mirroring the reference's Python exceptions.
+ */
+#ifndef TURTLE_HIP_H
+#define TURTLE_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TURTLE_OK 0
+#define TURTLE_EINVAL -1   /* bad argument / shape (the reference raises RuntimeError / einops errors) */
+#define TURTLE_ENOWEIGHT -2 /* missing or mis-shaped weight (load_state_dict strict=True)        */
+#define TURTLE_EHIP -3     /* HIP runtime error                                                   */
+#define TURTLE_ESTATE -4   /* call order (e.g. forward before turtle_load_weights)                */
+
+#define TURTLE_DTYPE_F32 0
+#define TURTLE_DTYPE_BF16 1
+
+/* attention / FFN type codes (TurtleAttnBlock, turtle_t1_arch.py:780-802) */
+#define TURTLE_ATTN_REDUCED 0
+#define TURTLE_ATTN_CHANNEL 1
+#define TURTLE_ATTN_FHR 2
+#define TURTLE_ATTN_CHM 3
+#define TURTLE_ATTN_NONE 4
+#define TURTLE_FFN_FFW 0
+#define TURTLE_FFN_GFFW 1
+
+/* Arch keys read by make_model (turtle_t1_arch.py:12-52), already defaulted by the caller. */
+typedef struct TurtleConfig {
+  int n_colors;
+  int dim;
+  int enc_blocks[3];
+  int middle_blocks;
+  int dec_blocks[3];
+  int num_refinement_blocks;
+  float ffn_expansion_factor;
+  int bias;
+  int layernorm_biasfree;   /* LayerNorm_type == 'BiasFree' */
+  int use_both_input;
+  int num_frames_tocache;
+  int num_heads[4];
+  /* [encoder1..3, decoder1..3, refinement][type1, type2] */
+  int level_attn[7][2];
+  int level_ffn[7];         /* encoder1..3, decoder1..3, refinement */
+  int latent_attn[3];
+  int latent_ffn;
+  int super_resolution;     /* 1: TurtleSuper_t1 (4x bilinear front-end) */
+  int dtype;                /* TURTLE_DTYPE_* storage / MFMA type; accumulation is fp32 */
+} TurtleConfig;
+
+typedef struct TurtleHandle TurtleHandle;
+
+/* make_model(opt): validate the config and create a handle (no device memory yet). */
+int turtle_create(const TurtleConfig* cfg, TurtleHandle** out);
+void turtle_destroy(TurtleHandle* h);
+
+/* Number of state-dict entries and their names / shapes, in the reference's state_dict() order. */
+int turtle_num_weights(const TurtleHandle* h);
+int turtle_weight_info(const TurtleHandle* h, int idx, const char** name, int* ndim, int64_t shape[4]);
+
+/* Stage one state-dict tensor (host fp32, C-contiguous, `numel` elements). */
+int turtle_set_weight(TurtleHandle* h, const char* name, const float* host_data, int64_t numel);
+/* Validate that every entry is staged (strict load), pack and upload to the device. */
+int turtle_load_weights(TurtleHandle* h);
+
+/* History-state layout. For cache slot i (0..7, order of Turtle_t1.forward's k_to_cache list):
+ *   kind[i] = 0 none, 1 FHR rows, 2 SAB frames.
+ *   FHR:  shape [B, heads, rows, P]      with strides (P*heads*rows, rows, 1, heads*rows)
+ *   SAB:  k [B, frames, 1, N, 2c], v [B, frames, 1, N, ws*ws*c], contiguous.
+ * `t_in[i]` = rows (FHR) / frames (SAB) of the incoming cache (0 when the caller passes None).
+ * Writes kind[8], and for each slot the 5-d shapes (unused trailing dims = 1) of the k and v
+ * tensors forward() will return: k_shape[i*5 + d], v_shape[i*5 + d]. */
+int turtle_cache_layout(const TurtleHandle* h, int B, int H, int W, const int t_in[8],
+                        int kind[8], int64_t k_shape[40], int64_t v_shape[40]);
+
+/* Device workspace bytes needed by turtle_forward for frames of B x H x W. */
+int turtle_workspace_size(const TurtleHandle* h, int B, int H, int W, size_t* bytes);
+
+/* One causal step (Turtle_t1.forward): inp [B, 2, n_colors, H, W] fp32 contiguous (device),
+ * out [B, n_colors, Hout, Wout] fp32 (Hout = H, or 4H for super-resolution).
+ * k_in/v_in[i]: incoming caches (NULL when t_in[i] == 0), k_out/v_out[i]: caller-allocated
+ * tensors of the shapes given by turtle_cache_layout (NULL for kind 0). Storage dtype of caches
+ * = the handle's dtype. */
+int turtle_forward(TurtleHandle* h, const float* inp, int B, int H, int W, float* out,
+                   const void* const k_in[8], const void* const v_in[8], const int t_in[8],
+                   void* const k_out[8], void* const v_out[8],
+                   void* workspace, size_t workspace_bytes, void* stream);
+
+const char* turtle_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

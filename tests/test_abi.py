@@ -1,0 +1,78 @@
+"""CPU-side checks of the C ABI: the library loads, exports every symbol of include/turtle_hip.h,
+reproduces the reference state_dict surface, sizes workspaces and reports errors. No kernels run."""
+import ctypes as C
+import json
+import os
+import re
+
+import pytest
+import yaml
+
+from golden_io import key_shapes
+from turtlevsr_amd import _lib
+from turtlevsr_amd.arch import resolve
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOPRO = os.path.join(REPO, "options", "Turtle_Deblur_Gopro.yml")
+
+
+def gopro():
+    with open(GOPRO) as f:
+        return yaml.safe_load(f)
+
+
+def handle(opt, sr=False, dtype=0):
+    L = _lib.lib()
+    h = C.c_void_p()
+    _lib.check(L.turtle_create(C.byref(_lib.config_from_arch(resolve(opt), sr, dtype)), C.byref(h)))
+    return L, h
+
+
+def test_exports_match_header():
+    hdr = open(os.path.join(REPO, "include", "turtle_hip.h")).read()
+    declared = set(re.findall(r"\b(turtle_[a-z_]+)\s*\(", hdr))
+    assert declared == set(_lib.EXPORTED)
+    L = _lib.lib()
+    for s in declared:
+        assert hasattr(L, s)
+
+
+@pytest.mark.parametrize("model,sr", [("Turtle_t1", False), ("TurtleSuper_t1", True)])
+def test_state_dict_surface(model, sr):
+    L, h = handle(gopro(), sr)
+    n = L.turtle_num_weights(h)
+    got = []
+    for i in range(n):
+        nm, nd, sh = C.c_char_p(), C.c_int(), (C.c_int64 * 4)()
+        _lib.check(L.turtle_weight_info(h, i, C.byref(nm), C.byref(nd), sh))
+        got.append((nm.value.decode(), tuple(sh[:nd.value])))
+    assert got == list(key_shapes(model).items())
+    L.turtle_destroy(h)
+
+
+def test_workspace_and_cache_layout():
+    L, h = handle(gopro(), False, 1)
+    ws = C.c_size_t()
+    _lib.check(L.turtle_workspace_size(h, 1, 1080, 1920, C.byref(ws)))
+    assert 1e9 < ws.value < 64e9
+    kind, ks, vs = (C.c_int * 8)(), (C.c_int64 * 40)(), (C.c_int64 * 40)()
+    _lib.check(L.turtle_cache_layout(h, 1, 256, 256, (C.c_int * 8)(*([0] * 8)), kind, ks, vs))
+    assert list(kind) == [0, 0, 0, 1, 1, 2, 2, 2]
+    assert tuple(ks[15:19]) == (1, 8, 64, 1024)             # latent FHR after frame 0
+    assert tuple(ks[25:30]) == (1, 1, 1, 256, 512)          # dec3 SAB k, N = 256 tokens
+    assert tuple(vs[35:40]) == (1, 1, 1, 256, 16 * 16 * 64)  # dec1 SAB v
+    t_in = (C.c_int * 8)(0, 0, 0, 192, 192, 3, 3, 2)
+    _lib.check(L.turtle_cache_layout(h, 2, 256, 256, t_in, kind, ks, vs))
+    assert ks[17] == 192 and ks[26] == 3 and ks[36] == 2
+
+
+def test_errors_are_reported():
+    o = gopro()
+    o["decoder1_attn_type2"] = "MEST"   # Turtle_Denoise_Davis.yml: undefined in every arch
+    with pytest.raises(ValueError):
+        resolve(o)
+    L, h = handle(gopro())
+    rc = L.turtle_load_weights(h)
+    assert rc == -2 and b"missing key" in L.turtle_last_error()
+    rc = L.turtle_set_weight(h, b"nope.weight", C.c_void_p(1), 1)
+    assert rc == -2

@@ -1,0 +1,92 @@
+"""HIP path parity on a real MI355X: libturtle_hip.so vs the reference golden vectors and the oracle.
+
+All calls go through the C ABI (ctypes) of the in-tree library; there is no fallback.
+fp32 gate: max-abs <= 2e-4 on outputs (values O(1)) and PSNR(build, reference) >= 80 dB;
+bf16 gate: PSNR(build, reference fp32) >= 45 dB per frame (the reference's own fp32 vs
+bf16-autocast gap is 62 dB).
+"""
+import numpy as np
+import pytest
+import torch
+
+from golden_io import check_summary, load, synth_sd
+
+pytestmark = pytest.mark.gpu
+
+CLIPS = ["clip_tiny_64", "clip_tiny_ragged", "clip_tiny_both", "clip_tiny_biasfree", "clip_tiny_sr",
+         "clip_gopro_64"]
+
+
+def psnr(a, b):
+    mse = float(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2))
+    return 99.0 if mse == 0 else 10 * np.log10(1.0 / mse)
+
+
+def _model(meta, dtype="fp32"):
+    from turtlevsr_amd.model import TurtleHIP
+    m = TurtleHIP(meta["opt"], sr=meta["sr"], dtype=dtype)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    m.load_state_dict(synth_sd(shapes, meta["seed"]), strict=True)
+    return m.cuda().eval()
+
+
+def _run(m, clip):
+    x = torch.from_numpy(clip).cuda()
+    kc = vc = None
+    outs, caches = [], []
+    with torch.no_grad():
+        for j in range(x.shape[1]):
+            inp = torch.stack([x[:, max(j - 1, 0)], x[:, j]], dim=1)
+            o, kc, vc = m(inp, kc, vc)
+            outs.append(o.float().cpu())
+            caches.append(([None if t is None else t.float().cpu() for t in kc],
+                           [None if t is None else t.float().cpu() for t in vc]))
+    torch.cuda.synchronize()
+    return outs, caches
+
+
+@pytest.mark.parametrize("name", CLIPS)
+def test_clip_fp32_vs_reference(name):
+    g, meta = load(name)
+    m = _model(meta, "fp32")
+    outs, caches = _run(m, g["clip"])
+    for j, o in enumerate(outs):
+        ref = g[f"out{j}"]
+        err = float(np.abs(o.numpy() - ref).max())
+        assert err <= 2e-4, (name, j, err)
+        assert psnr(o.numpy(), ref) >= 80.0
+        kc, vc = caches[j]
+        for which, lst in (("k", kc), ("v", vc)):
+            for i, t in enumerate(lst):
+                key = f"f{j}_{which}{i}"
+                if t is None:
+                    assert key + "__shape" not in g, key
+                    continue
+                check_summary(g, key, t, rtol=2e-3, atol=2e-4)
+                if key in g:
+                    np.testing.assert_allclose(t.numpy(), g[key], atol=2e-4, rtol=2e-3, err_msg=key)
+
+
+@pytest.mark.parametrize("name", ["clip_tiny_64", "clip_gopro_64"])
+def test_clip_bf16_psnr(name):
+    g, meta = load(name)
+    m = _model(meta, "bf16")
+    outs, _ = _run(m, g["clip"])
+    for j, o in enumerate(outs):
+        p = psnr(o.numpy(), g[f"out{j}"])
+        assert p >= 45.0, (name, j, p)
+
+
+def test_fp32_vs_oracle_256():
+    """GoPro widths at 256x256 (the bench shape), 3 frames, HIP fp32 vs the CPU oracle."""
+    from oracle import turtle_ref as R
+    from turtlevsr_amd.synthetic import synthetic_frames
+    g, meta = load("clip_gopro_64")
+    m = _model(meta, "fp32")
+    clip = synthetic_frames((1, 3, 3, 256, 256), 7)
+    outs, _ = _run(m, clip)
+    sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    torch.set_num_threads(16)
+    ref, _ = R.run_clip(sd, meta["opt"], torch.from_numpy(clip))
+    for o, r in zip(outs, ref):
+        assert psnr(o.numpy(), r.numpy()) >= 80.0

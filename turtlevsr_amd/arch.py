@@ -1,7 +1,7 @@
 """Architecture resolution: option dict -> levels / blocks (make_model, turtle_t1_arch.py:10-53).
 
 Pure host logic shared by the parameter holder (``model.py``) and the HIP frame driver
-(``hip_forward.py``). It reads the same keys with the same defaults as the reference's
+(``model.py`` / ``csrc/turtle.cpp``). It reads the same keys with the same defaults as the reference's
 ``make_model`` and mirrors the level wiring of ``Turtle_t1.__init__`` (turtle_t1_arch.py:932-1043):
 
 * ``LevelBlock`` (813-865): ``num_blocks - 1`` blocks of ``attn_type1`` then one ``attn_type2``;
@@ -56,6 +56,9 @@ class TurtleArch:
     use_both: bool
     ntc: int
     levels: Dict[str, LevelSpec]
+    ffe: float = 1.0
+    heads: tuple = (1, 1, 1, 1)
+    type1: Dict[str, str] = field(default_factory=dict)   # raw attn_type1 per level (+ latent_mid)
 
     @property
     def order(self):
@@ -109,6 +112,10 @@ def resolve(opt: dict) -> TurtleArch:
     }
     use_both = bool(o["use_both_input"])
     n_col = int(o["n_colors"])
+    type1 = {"encoder_level1": o["encoder1_attn_type1"], "encoder_level2": o["encoder2_attn_type1"],
+             "encoder_level3": o["encoder3_attn_type1"], "decoder_level3": o["decoder1_attn_type1"],
+             "decoder_level2": o["decoder2_attn_type1"], "decoder_level1": o["decoder3_attn_type1"],
+             "refinement": o["refinement_attn_type1"], "latent_mid": o["latent_attn_type2"]}
     return TurtleArch(dim=dim, in_ch=n_col * (2 if use_both else 1), out_ch=n_col, bias=bias,
                       ln_type=o.get("LayerNorm_type", "WithBias"), use_both=use_both, ntc=ntc,
-                      levels=levels)
+                      levels=levels, ffe=ffe, heads=tuple(heads), type1=type1)

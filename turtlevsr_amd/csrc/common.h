@@ -1,0 +1,96 @@
+// Shared device helpers for the Turtle HIP kernels (gfx950 / CDNA4, wave64).
+//
+// Storage types: activations and GEMM weights are either float (fp32 parity mode) or __bf16
+// (throughput mode); every reduction / accumulation is fp32. Feature maps are pixel-major
+// ("NHWC"): [image][y][x][channel], channel contiguous, so a 16-byte vector holds VEC consecutive
+// channels of one pixel.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+#define TURTLE_DEV __device__ __forceinline__
+
+TURTLE_DEV float to_f(float x) { return x; }
+TURTLE_DEV float to_f(bf16 x) { return (float)x; }
+template <typename T> TURTLE_DEV T from_f(float x);
+template <> TURTLE_DEV float from_f<float>(float x) { return x; }
+template <> TURTLE_DEV bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+// 16-byte vector of storage elements, unpacked to fp32 registers.
+template <typename T> struct Vec;
+template <> struct Vec<float> {
+  static constexpr int N = 4;
+  float v[4];
+  TURTLE_DEV void load(const float* p) {
+    float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  }
+  TURTLE_DEV void store(float* p) const {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  TURTLE_DEV void zero() { v[0] = v[1] = v[2] = v[3] = 0.f; }
+};
+template <> struct Vec<bf16> {
+  static constexpr int N = 8;
+  float v[8];
+  TURTLE_DEV void load(const bf16* p) {
+    uint4 q = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  TURTLE_DEV void store(bf16* p) const {
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+    *reinterpret_cast<bf16x8*>(p) = o;
+  }
+  TURTLE_DEV void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = 0.f;
+  }
+};
+
+TURTLE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+
+TURTLE_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+TURTLE_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host/device descriptors
+// ------------------------------------------------------------------------------------------
+#define TURTLE_MAX_SRC 6
+
+// One operand source of a K-concatenated GEMM A matrix (pixel rows, channel columns).
+// Row of output pixel m = (img, p):   src_img = img * img_mul + img_add
+//   element (m, k) = base[(src_img * HW + p) * ld + off + k - kbeg]   for kbeg <= k < kbeg + K
+struct SrcDesc {
+  const void* base;
+  int64_t ld;
+  int off;
+  int K;
+  int img_mul;
+  int img_add;
+};
+
+struct SrcList {
+  SrcDesc s[TURTLE_MAX_SRC];
+  int n;
+  int Ktot;
+};

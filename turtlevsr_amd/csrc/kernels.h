@@ -1,0 +1,148 @@
+// Kernel argument blocks and launchers (host + device visible).
+#pragma once
+#include "common.h"
+
+namespace turtle {
+
+enum StoreMode { STORE_NHWC = 0, STORE_SHUFFLE = 1, STORE_UNSHUFFLE = 2 };
+
+struct GemmArgs {
+  SrcList a;                       // A sources, K-concatenated
+  int64_t M;                       // output pixels (all images)
+  int N;                           // output channels
+  int HW, Wimg;                    // pixels per image, image width (GEMM pixel grid)
+  const void* w;                   // [N][ldw] (storage type), per-image set if wstride != 0
+  int64_t ldw, wstride;
+  int wdiv;                        // weight set index = image / wdiv
+  int conv3, cin;                  // implicit 3x3 (K = 9 * cin, tap-major)
+  int ln;                          // LayerNorm prologue over a.s[0]
+  const float* ln_s;               // rowsum(W*g) (null: BiasFree)
+  const float* ln_t;               // W.b         (null: BiasFree)
+  const float* bias;
+  const float* scale;
+  int gelu;
+  const void* res;                 // residual (pixel-major, same pixel index as out)
+  int64_t ldr;
+  int offr;
+  void* out;
+  int64_t ldo;
+  int offo;
+  int store_mode;
+};
+template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
+
+enum DwMode { DW_PLAIN = 0, DW_GELU = 1, DW_GATE = 2 };
+struct DwArgs {
+  const void* in; int64_t ldi; int offi;
+  void* out; int64_t ldo; int offo;
+  const float* w;                  // [9][Cw] tap-major fp32 (Cw = C, or 2C for DW_GATE)
+  const float* bias;               // [Cw] or null
+  int nimg, H, W, C;               // C = output channels
+  int mode;
+  int tok_ws;                      // > 0: SAB dilated token-major output [img][n][(p1*ws+p2)*C + c]
+  int64_t tok_img_stride;          // element stride between images of the token-major output
+};
+template <typename T> void launch_dw(const DwArgs& a, hipStream_t st);
+
+struct WinArgs {                   // SAB q2/k2 window conv (ws x ws, stride ws, pad 1) + L2 norm
+  const void* in; int64_t ldi; int offi;
+  const float* w;                  // [ws*ws][C] fp32
+  const float* bias;               // [C] or null
+  void* out; int64_t out_img_stride;   // token rows of C elements; image stride in elements
+  int nimg, H, W, C, ws;
+};
+template <typename T> void launch_window(const WinArgs& a, hipStream_t st);
+
+#define TURTLE_MAX_T 8
+struct SabScoreArgs {
+  const void* q;                   // [B][N][d] normalised query tokens
+  int64_t q_bstride;
+  const void* k[TURTLE_MAX_T];     // frame t: [N][d] for batch 0
+  int64_t k_bstride[TURTLE_MAX_T];
+  int B, T, N, d;
+  const float* tau;                // temperature (device scalar)
+  float* topv;                     // [B][T][N][5]
+  int* topi;
+};
+template <typename T> void launch_sab_score(const SabScoreArgs& a, hipStream_t st);
+
+struct SabAvArgs {
+  const void* q; int64_t q_bstride;
+  const void* k[TURTLE_MAX_T]; int64_t k_bstride[TURTLE_MAX_T];
+  const void* v[TURTLE_MAX_T]; int64_t v_bstride[TURTLE_MAX_T];   // [N][ws*ws*C]
+  int B, T, N, d, th, tw, ws, C;
+  const float* tau;
+  const float* topv; const int* topi;
+  void* out;                       // [B*T][Hl][Wl][C] pixel-major
+};
+template <typename T> void launch_sab_av(const SabAvArgs& a, hipStream_t st);
+
+#define TURTLE_MAX_SEG 6
+struct GramSeg {                   // ch key columns per head from a pixel-major source
+  const void* base; int64_t ld; int off; int hstride; int img_mul, img_add; int norm;
+};
+struct GramArgs {
+  const void* q; int64_t ldq; int qoff;   // q channel h*ch+i at qoff
+  GramSeg seg[TURTLE_MAX_SEG]; int nseg;
+  int B, heads, ch, HW, nchunk, chunk;
+  float* part;                     // [B*heads][nchunk][ch*ncol + ch + ncol]
+};
+template <typename T> void launch_gram(const GramArgs& a, hipStream_t st);
+
+struct AttnFinArgs {
+  const float* part; int nchunk;
+  int B, heads, ch, nseg;
+  unsigned norm_mask;              // bit s: segment s is L2-normalised over HW
+  const float* tau;                // [heads]
+  float* red;                      // scratch [B*heads][ch*ncol + ch + ncol]
+  float* attn;                     // [B*heads][ch][ncol]
+  float* kinv;                     // [B][heads*ch] 1/max(|k_cur|,eps) of segment `cur_seg`, or null
+  int cur_seg;
+};
+void launch_attn_finalize(const AttnFinArgs& a, hipStream_t st);
+
+struct WeffArgs {                  // W_eff[b][o][col] = sum_i Wp[o][h*ch+i] * A[b][h][i][seg*ch+j]
+  const float* attn; const float* wp;   // wp fp32 [C][C]
+  int B, heads, ch, nseg, C;
+  int64_t seg_col[TURTLE_MAX_SEG]; // column of (seg, h=0, j=0) in W_eff
+  int seg_hstride[TURTLE_MAX_SEG]; // column step per head
+  int Keff;
+  void* weff;                      // [B][C][Keff] storage type
+};
+template <typename T> void launch_weff(const WeffArgs& a, hipStream_t st);
+
+struct FhrCacheArgs {              // latent FHR cache roll: keep last Rnew rows of [old R ; cur ch]
+  const void* old; int R;          // [B][P][heads][R] (R may be 0)
+  const void* cur; int64_t ldc; int coff;   // current k or v, pixel-major
+  const float* kinv;               // [B][heads*ch] scale for current rows (k) or null (v)
+  void* out; int Rnew;             // [B][P][heads][Rnew]
+  int B, P, heads, ch;
+};
+template <typename T> void launch_fhr_cache(const FhrCacheArgs& a, hipStream_t st);
+
+struct StemArgs {                  // input_projection 3x3 on the padded (or 4x bilinear) frame
+  const float* inp;                // [B][2][Cin][H][W] fp32 (caller layout)
+  int64_t in_bstride, in_fstride;  // element strides of batch / frame
+  int B, Cimg, Hin, Win;           // source frame size
+  int Hp, Wp;                      // padded working size
+  int use_both;                    // channels = [prev, cur]
+  int sr;                          // 4x bilinear upsample of the current frame before padding
+  const float* w;                  // [Cout][Cin_tot][3][3]
+  const float* bias;
+  int Cout;
+  void* out;                       // [B][Hp][Wp][Cout]
+};
+template <typename T> void launch_stem(const StemArgs& a, hipStream_t st);
+
+struct EndArgs {                   // ending 3x3 Cin->Cimg + bias + current frame, cropped, NCHW fp32
+  const void* x; int Cin;          // [B][Hp][Wp][Cin]
+  const float* w; const float* bias;
+  const float* inp; int64_t in_bstride, in_fstride;
+  int B, Cimg, Hin, Win, Hp, Wp, Hout, Wout, sr;
+  float* out;                      // [B][Cimg][Hout][Wout]
+};
+template <typename T> void launch_ending(const EndArgs& a, hipStream_t st);
+
+void launch_cast_f32(const float* src, void* dst, int64_t n, int to_bf16, hipStream_t st);
+
+}  // namespace turtle

@@ -1,0 +1,328 @@
+// Spatial (non-GEMM) kernels on pixel-major maps:
+//   * depthwise 3x3 (+bias, +GELU, or the GatedFeedForward gate gelu(x1)*x2) with an optional
+//     SAB dilated token-major output layout             turtle_t1_arch.py:159-178, 716-740, 555-574
+//   * SAB window conv ws x ws / stride ws / pad 1 on q2/k2 + L2 normalisation over d   559-578
+//   * input_projection 3x3 from the caller's NCHW frames (zero pad to 32, or SR 4x bilinear)
+//     1063, turtlesuper 976-977
+//   * ending 3x3 + bias + current frame, crop, NCHW fp32 output                          1128-1132
+//   * latent FrameHistoryRouter cache roll (keep the last Rnew rows of [cached ; current])   272-286
+#include "common.h"
+#include "kernels.h"
+
+namespace turtle {
+
+// ------------------------------------------------------------------------------------------
+// depthwise 3x3: one thread = one pixel x VEC channels
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
+  constexpr int VEC = Vec<T>::N;
+  const int CV = a.C / VEC;
+  const int64_t total = (int64_t)a.nimg * a.H * a.W * CV;
+  const int Cw = a.mode == DW_GATE ? 2 * a.C : a.C;
+  const T* in = reinterpret_cast<const T*>(a.in);
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int cv = (int)(idx % CV);
+    const int64_t pix = idx / CV;
+    const int x = (int)(pix % a.W);
+    const int64_t t = pix / a.W;
+    const int y = (int)(t % a.H);
+    const int64_t img = t / a.H;
+    const int c0 = cv * VEC;
+    float acc1[VEC], acc2[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      acc1[i] = a.bias ? a.bias[c0 + i] : 0.f;
+      acc2[i] = (a.mode == DW_GATE && a.bias) ? a.bias[a.C + c0 + i] : 0.f;
+    }
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int yy = y + dy;
+      if (yy < 0 || yy >= a.H) continue;
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int xx = x + dx;
+        if (xx < 0 || xx >= a.W) continue;
+        const int tap = (dy + 1) * 3 + (dx + 1);
+        const T* p = in + ((img * a.H + yy) * a.W + xx) * a.ldi + a.offi + c0;
+        const float* wt = a.w + tap * Cw + c0;
+        Vec<T> v; v.load(p);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc1[i] = fmaf(wt[i], v.v[i], acc1[i]);
+        if (a.mode == DW_GATE) {
+          Vec<T> v2; v2.load(p + a.C);
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) acc2[i] = fmaf(wt[a.C + i], v2.v[i], acc2[i]);
+        }
+      }
+    }
+    Vec<T> o;
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) {
+      float r = acc1[i];
+      if (a.mode == DW_GELU) r = gelu_erf(r);
+      else if (a.mode == DW_GATE) r = gelu_erf(r) * acc2[i];
+      o.v[i] = r;
+    }
+    int64_t dst;
+    if (a.tok_ws > 0) {
+      const int ws = a.tok_ws, h = a.H / ws, w = a.W / ws;
+      const int p1 = y / h, i = y - p1 * h, p2 = x / w, j = x - p2 * w;
+      dst = img * a.tok_img_stride + ((int64_t)i * w + j) * ((int64_t)ws * ws * a.C) + (int64_t)(p1 * ws + p2) * a.C + c0;
+    } else {
+      dst = pix * a.ldo + a.offo + c0;
+    }
+    o.store(reinterpret_cast<T*>(a.out) + dst);
+  }
+}
+
+template <typename T>
+void launch_dw(const DwArgs& a, hipStream_t st) {
+  const int64_t total = (int64_t)a.nimg * a.H * a.W * (a.C / Vec<T>::N);
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(dw_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// SAB window conv + L2 normalisation: one block per token
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void window_kernel(WinArgs a) {
+  // thread = (channel vector cv, tap subset `part`); C / VEC <= 256 for every Turtle level
+  constexpr int VEC = Vec<T>::N;
+  __shared__ float red[256 * VEC];
+  __shared__ float ss[4];
+  const int th = a.H / a.ws, tw = a.W / a.ws, N = th * tw;
+  const int n = blockIdx.x % N;
+  const int64_t img = blockIdx.x / N;
+  const int ti = n / tw, tj = n % tw;
+  const int CV = a.C / VEC, nparts = 256 / CV;
+  const int tid = threadIdx.x, cv = tid % CV, part = tid / CV;
+  const T* in = reinterpret_cast<const T*>(a.in);
+  const int taps = a.ws * a.ws;
+  float acc[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+  if (part < nparts) {
+    for (int tp = part; tp < taps; tp += nparts) {
+      const int dy = tp / a.ws, dx = tp % a.ws;
+      const int y = ti * a.ws - 1 + dy, x = tj * a.ws - 1 + dx;   // padding = 1
+      if (y < 0 || y >= a.H || x < 0 || x >= a.W) continue;
+      Vec<T> v; v.load(in + ((img * a.H + y) * a.W + x) * a.ldi + a.offi + cv * VEC);
+      const float* wt = a.w + (int64_t)tp * a.C + cv * VEC;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] = fmaf(wt[i], v.v[i], acc[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) red[tid * VEC + i] = acc[i];
+  __syncthreads();
+  if (tid < CV) {
+    for (int pp = 1; pp < nparts; ++pp)
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[i] += red[(pp * CV + tid) * VEC + i];
+  }
+  __syncthreads();
+  if (tid < CV) {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) red[tid * VEC + i] = acc[i];
+  }
+  __syncthreads();
+  // L2 normalisation over the C = 2c token features (F.normalize, eps 1e-12)
+  float s = 0.f;
+  for (int c = tid; c < a.C; c += 256) {
+    float v = red[c] + (a.bias ? a.bias[c] : 0.f);
+    red[c] = v;
+    s += v * v;
+  }
+  s = wave_sum(s);
+  if ((tid & 63) == 0) ss[tid >> 6] = s;
+  __syncthreads();
+  const float tot = ss[0] + ss[1] + ss[2] + ss[3];
+  const float inv = 1.f / fmaxf(sqrtf(tot), 1e-12f);
+  T* out = reinterpret_cast<T*>(a.out) + img * a.out_img_stride + (int64_t)n * a.C;
+  for (int c = tid; c < a.C; c += 256) out[c] = from_f<T>(red[c] * inv);
+}
+
+template <typename T>
+void launch_window(const WinArgs& a, hipStream_t st) {
+  const int N = (a.H / a.ws) * (a.W / a.ws);
+  hipLaunchKernelGGL(window_kernel<T>, dim3((unsigned)(a.nimg * N)), dim3(256), 0, st, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// input_projection: zero-padded (or SR bilinear x4 then padded) frame -> 3x3 conv -> pixel-major
+// ------------------------------------------------------------------------------------------
+TURTLE_DEV float frame_px(const StemArgs& a, int b, int f, int c, int y, int x) {
+  // value of channel c of frame f at padded working coordinate (y, x); 0 outside the image
+  const float* base = a.inp + (int64_t)b * a.in_bstride + (int64_t)f * a.in_fstride + (int64_t)c * a.Hin * a.Win;
+  if (!a.sr) {
+    if (y < 0 || y >= a.Hin || x < 0 || x >= a.Win) return 0.f;
+    return base[(int64_t)y * a.Win + x];
+  }
+  // TurtleSuper_t1: nn.Upsample(scale_factor=4, bilinear, align_corners=False), then zero pad
+  if (y < 0 || y >= 4 * a.Hin || x < 0 || x >= 4 * a.Win) return 0.f;
+  float sy = fmaxf(0.25f * (y + 0.5f) - 0.5f, 0.f), sx = fmaxf(0.25f * (x + 0.5f) - 0.5f, 0.f);
+  int y0 = (int)sy, x0 = (int)sx;
+  int y1 = y0 < a.Hin - 1 ? y0 + 1 : y0, x1 = x0 < a.Win - 1 ? x0 + 1 : x0;
+  float ly = sy - y0, lx = sx - x0;
+  float v00 = base[(int64_t)y0 * a.Win + x0], v01 = base[(int64_t)y0 * a.Win + x1];
+  float v10 = base[(int64_t)y1 * a.Win + x0], v11 = base[(int64_t)y1 * a.Win + x1];
+  return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
+  // one thread per (pixel, 8 output channels)
+  const int CG = (a.Cout + 7) / 8;
+  const int64_t total = (int64_t)a.B * a.Hp * a.Wp * CG;
+  const int cin = a.use_both ? 2 * a.Cimg : a.Cimg;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int cg = (int)(idx % CG);
+    const int64_t pix = idx / CG;
+    const int x = (int)(pix % a.Wp);
+    const int y = (int)((pix / a.Wp) % a.Hp);
+    const int b = (int)(pix / ((int64_t)a.Wp * a.Hp));
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = (a.bias && cg * 8 + i < a.Cout) ? a.bias[cg * 8 + i] : 0.f;
+    for (int ci = 0; ci < cin; ++ci) {
+      const int f = a.use_both ? (ci < a.Cimg ? 0 : 1) : 1;
+      const int c = a.use_both ? ci % a.Cimg : ci;
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int yy = y + dy, xx = x + dx;
+          // the conv's own zero padding is at the padded-frame border
+          float v = (yy < 0 || yy >= a.Hp || xx < 0 || xx >= a.Wp) ? 0.f : frame_px(a, b, f, c, yy, xx);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int co = cg * 8 + i;
+            if (co < a.Cout) acc[i] = fmaf(a.w[((co * cin + ci) * 3 + dy + 1) * 3 + dx + 1], v, acc[i]);
+          }
+        }
+    }
+    T* o = reinterpret_cast<T*>(a.out) + pix * a.Cout + cg * 8;
+    for (int i = 0; i < 8 && cg * 8 + i < a.Cout; ++i) o[i] = from_f<T>(acc[i]);
+  }
+}
+
+template <typename T>
+void launch_stem(const StemArgs& a, hipStream_t st) {
+  const int64_t total = (int64_t)a.B * a.Hp * a.Wp * ((a.Cout + 7) / 8);
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(stem_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// ending: 3x3 Cin->Cimg (+bias) + current padded frame, cropped to the output size
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void ending_kernel(EndArgs a) {
+  constexpr int VEC = Vec<T>::N;
+  const int64_t total = (int64_t)a.B * a.Hout * a.Wout;
+  const T* xin = reinterpret_cast<const T*>(a.x);
+  StemArgs s{};
+  s.inp = a.inp; s.in_bstride = a.in_bstride; s.in_fstride = a.in_fstride;
+  s.Cimg = a.Cimg; s.Hin = a.Hin; s.Win = a.Win; s.sr = a.sr;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int x = (int)(idx % a.Wout);
+    const int y = (int)((idx / a.Wout) % a.Hout);
+    const int b = (int)(idx / ((int64_t)a.Wout * a.Hout));
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int yy = y + dy;
+      if (yy < 0 || yy >= a.Hp) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int xx = x + dx;
+        if (xx < 0 || xx >= a.Wp) continue;
+        const int tap = (dy + 1) * 3 + dx + 1;
+        const T* p = xin + (((int64_t)b * a.Hp + yy) * a.Wp + xx) * a.Cin;
+        for (int c0 = 0; c0 < a.Cin; c0 += VEC) {
+          Vec<T> v; v.load(p + c0);
+#pragma unroll
+          for (int i = 0; i < VEC; ++i)
+            for (int co = 0; co < a.Cimg && co < 4; ++co)
+              acc[co] = fmaf(a.w[((co * a.Cin + c0 + i) * 3 + dy + 1) * 3 + dx + 1], v.v[i], acc[co]);
+        }
+      }
+    }
+    for (int co = 0; co < a.Cimg && co < 4; ++co) {
+      float r = acc[co] + a.bias[co] + frame_px(s, b, 1, co, y, x);
+      a.out[(((int64_t)b * a.Cimg + co) * a.Hout + y) * a.Wout + x] = r;
+    }
+  }
+}
+
+template <typename T>
+void launch_ending(const EndArgs& a, hipStream_t st) {
+  const int64_t total = (int64_t)a.B * a.Hout * a.Wout;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(ending_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// latent FHR cache roll: out[b][p][h][r'] = concat(old[b][p][h][0:R], cur*kinv)[R + ch - Rnew + r']
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void fhr_cache_kernel(FhrCacheArgs a) {
+  const int64_t total = (int64_t)a.B * a.P * a.heads * a.Rnew;
+  const T* old = reinterpret_cast<const T*>(a.old);
+  const T* cur = reinterpret_cast<const T*>(a.cur);
+  T* out = reinterpret_cast<T*>(a.out);
+  const int shift = a.R + a.ch - a.Rnew;
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
+    const int rn = (int)(idx % a.Rnew);
+    const int64_t t = idx / a.Rnew;
+    const int h = (int)(t % a.heads);
+    const int64_t bp = t / a.heads;            // b * P + p
+    const int b = (int)(bp / a.P);
+    const int r = rn + shift;
+    T v;
+    if (r < a.R) {
+      v = old[(bp * a.heads + h) * a.R + r];
+    } else {
+      const int j = r - a.R;
+      float x = to_f(cur[bp * a.ldc + a.coff + h * a.ch + j]);
+      if (a.kinv) x *= a.kinv[(int64_t)b * a.heads * a.ch + h * a.ch + j];
+      v = from_f<T>(x);
+    }
+    out[idx] = v;
+  }
+}
+
+template <typename T>
+void launch_fhr_cache(const FhrCacheArgs& a, hipStream_t st) {
+  const int64_t total = (int64_t)a.B * a.P * a.heads * a.Rnew;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(fhr_cache_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+}
+
+__global__ void cast_kernel(const float* src, void* dst, int64_t n, int to_bf16) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    if (to_bf16) reinterpret_cast<bf16*>(dst)[i] = (bf16)src[i];
+    else reinterpret_cast<float*>(dst)[i] = src[i];
+  }
+}
+void launch_cast_f32(const float* src, void* dst, int64_t n, int to_bf16, hipStream_t st) {
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(cast_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, n, to_bf16);
+}
+
+#define INST(T)                                                          \
+  template void launch_dw<T>(const DwArgs&, hipStream_t);                \
+  template void launch_window<T>(const WinArgs&, hipStream_t);           \
+  template void launch_stem<T>(const StemArgs&, hipStream_t);            \
+  template void launch_ending<T>(const EndArgs&, hipStream_t);           \
+  template void launch_fhr_cache<T>(const FhrCacheArgs&, hipStream_t);
+INST(float)
+INST(bf16)
+
+}  // namespace turtle

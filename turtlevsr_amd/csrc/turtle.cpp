@@ -1,0 +1,955 @@
+// libturtle_hip: weight packing, frame driver and the C ABI (include/turtle_hip.h).
+//
+// The frame driver issues the per-frame kernel sequence of Turtle_t1.forward
+// (turtle_t1_arch.py:1045-1132) on the caller's stream. Every block is restructured around the
+// HBM roofline: LayerNorm is folded into the following pointwise GEMM, attention outputs are
+// folded into the projection weights (W_eff), GELU / gate / bias / scale / residual live in
+// epilogues, skip concats are multi-source GEMM operands and the SAB never materialises N x N.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/turtle_hip.h"
+#include "kernels.h"
+
+using namespace turtle;
+
+static thread_local std::string g_err;
+
+struct TurtleError : std::runtime_error {
+  int code;
+  TurtleError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+#define TFAIL(code, msg) throw TurtleError(code, msg)
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) TFAIL(TURTLE_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+static const size_t NONE = (size_t)-1;
+
+// ------------------------------------------------------------------------------------------
+// architecture (mirror of turtlevsr_amd/arch.py, itself make_model + Turtle_t1.__init__)
+// ------------------------------------------------------------------------------------------
+struct Blk {
+  std::string prefix;
+  int dim, attn, ffn, heads, ntc, ws, hidden;
+  int level;          // 0..7 index into Arch::levels
+  int cache_slot;     // -1 or 0..7 (only the cache-carrying block of a level)
+};
+
+struct Level {
+  std::string name;
+  int dim;
+  int scale;          // pixels per side relative to the padded frame (1, 2, 4, 8)
+  std::vector<Blk> blocks;
+};
+
+struct Arch {
+  TurtleConfig cfg;
+  int dim, in_ch, out_ch;
+  std::vector<Level> levels;   // encoder_level1..3, latent, decoder_level3..1, refinement
+  std::vector<std::pair<std::string, std::vector<int64_t>>> params;   // state_dict order
+};
+
+static const char* attn_name(int a) {
+  switch (a) {
+    case TURTLE_ATTN_REDUCED: return "ReducedAttn";
+    case TURTLE_ATTN_CHANNEL: return "Channel";
+    case TURTLE_ATTN_FHR: return "FHR";
+    case TURTLE_ATTN_CHM: return "CHM";
+    case TURTLE_ATTN_NONE: return "NoAttn";
+  }
+  return "?";
+}
+
+static void build_arch(Arch& A) {
+  const TurtleConfig& c = A.cfg;
+  if (c.dim <= 0 || c.dim % 8) TFAIL(TURTLE_EINVAL, "dim must be a positive multiple of 8");
+  if (c.n_colors < 1 || c.n_colors > 4) TFAIL(TURTLE_EINVAL, "n_colors must be 1..4");
+  if (c.middle_blocks < 2) TFAIL(TURTLE_EINVAL, "LatentCacheBlock should have more than 2 layers (turtle_t1_arch.py:899-901)");
+  if (c.super_resolution && c.use_both_input) TFAIL(TURTLE_EINVAL, "TurtleSuper_t1 with use_both_input is not runnable in the reference");
+  A.dim = c.dim;
+  A.in_ch = c.n_colors * (c.use_both_input ? 2 : 1);
+  A.out_ch = c.n_colors;
+  const int d = c.dim, ntc = c.num_frames_tocache;
+  auto chk = [](int at, int ft) {
+    if (at < 0 || at > 4) TFAIL(TURTLE_EINVAL, "attention type not defined (turtle_t1_arch.py:790-792)");
+    if (ft < 0 || ft > 1) TFAIL(TURTLE_EINVAL, "FFW type not defined (turtle_t1_arch.py:800-802)");
+  };
+  auto level = [&](const char* name, int dd, int scale, int n, int t1, int t2, int ffn, int heads, int nt, int sp, int slot) {
+    Level L{name, dd, scale, {}};
+    for (int i = 0; i < n; ++i) {
+      int at = i == n - 1 ? t2 : t1;
+      chk(at, ffn);
+      Blk b{std::string(name) + ".transformer_blocks." + std::to_string(i), dd, at, ffn, heads, nt, 2 * sp,
+            (int)(dd * c.ffn_expansion_factor), (int)A.levels.size(), i == n - 1 ? slot : -1};
+      L.blocks.push_back(b);
+    }
+    A.levels.push_back(L);
+  };
+  level("encoder_level1", d, 1, c.enc_blocks[0], c.level_attn[0][0], c.level_attn[0][1], c.level_ffn[0], c.num_heads[0], ntc, 1, 0);
+  level("encoder_level2", 2 * d, 2, c.enc_blocks[1], c.level_attn[1][0], c.level_attn[1][1], c.level_ffn[1], c.num_heads[1], ntc, 1, 1);
+  level("encoder_level3", 4 * d, 4, c.enc_blocks[2], c.level_attn[2][0], c.level_attn[2][1], c.level_ffn[2], c.num_heads[2], ntc, 1, 2);
+  {
+    Level L{"latent", 8 * d, 8, {}};
+    const int n = c.middle_blocks;
+    for (int i = 0; i < n; ++i) {
+      int at = i == 0 ? c.latent_attn[0] : (i == n - 1 ? c.latent_attn[2] : c.latent_attn[1]);
+      chk(at, c.latent_ffn);
+      Blk b{"latent.transformer_blocks." + std::to_string(i), 8 * d, at, c.latent_ffn, c.num_heads[3], ntc, 2,
+            (int)(8 * d * c.ffn_expansion_factor), 3, i == 0 ? 3 : (i == n - 1 ? 4 : -1)};
+      L.blocks.push_back(b);
+    }
+    A.levels.push_back(L);
+  }
+  level("decoder_level3", 4 * d, 4, c.dec_blocks[0], c.level_attn[3][0], c.level_attn[3][1], c.level_ffn[3], c.num_heads[2], ntc, 2, 5);
+  level("decoder_level2", 2 * d, 2, c.dec_blocks[1], c.level_attn[4][0], c.level_attn[4][1], c.level_ffn[4], c.num_heads[1], ntc, 4, 6);
+  level("decoder_level1", d, 1, c.dec_blocks[2], c.level_attn[5][0], c.level_attn[5][1], c.level_ffn[5], c.num_heads[0], 2, 8, 7);
+  level("refinement", d, 1, c.num_refinement_blocks, c.level_attn[6][0], c.level_attn[6][1], c.level_ffn[6], c.num_heads[0], ntc, 1, -1);
+  for (auto& L : A.levels) {
+    if (L.blocks.empty()) TFAIL(TURTLE_EINVAL, "every level needs >= 1 block");
+    for (auto& b : L.blocks) {
+      if (b.hidden % 8) TFAIL(TURTLE_EINVAL, "GatedFeedForward hidden width must be a multiple of 8");
+      if (b.attn != TURTLE_ATTN_REDUCED && b.attn != TURTLE_ATTN_NONE) {
+        if (b.heads <= 0 || b.dim % b.heads || (b.dim / b.heads) % 16)
+          TFAIL(TURTLE_EINVAL, "channels per head must be a multiple of 16");
+      }
+    }
+  }
+
+  // state_dict entries in registration order (see turtlevsr_amd/params.py)
+  auto P = [&](const std::string& n, std::vector<int64_t> s) { A.params.push_back({n, s}); };
+  auto conv = [&](const std::string& n, int cin, int cout, int k, int groups, bool bias) {
+    P(n + ".weight", {cout, cin / groups, k, k});
+    if (bias) P(n + ".bias", {cout});
+  };
+  const bool bias = c.bias != 0;
+  auto ln = [&](const std::string& n, int ch) {
+    P(n + ".body.weight", {ch});
+    if (!c.layernorm_biasfree) P(n + ".body.bias", {ch});
+  };
+  auto chan = [&](const std::string& n, int ch, int heads) {
+    P(n + ".temperature", {heads, 1, 1});
+    conv(n + ".qkv", ch, 3 * ch, 1, 1, bias);
+    conv(n + ".qkv_dwconv", 3 * ch, 3 * ch, 3, 3 * ch, bias);
+    conv(n + ".project_out", ch, ch, 1, 1, bias);
+  };
+  auto block = [&](const Blk& b) {
+    const int ch = b.dim;
+    ln(b.prefix + ".norm1", ch);
+    const std::string a = b.prefix + ".attn";
+    if (b.attn == TURTLE_ATTN_REDUCED) {
+      P(a + ".beta", {1, ch, 1, 1});
+      conv(a + ".conv1", ch, 2 * ch, 1, 1, true);
+      conv(a + ".conv2", 2 * ch, 2 * ch, 3, 2 * ch, true);
+      conv(a + ".conv3", 2 * ch, ch, 1, 1, true);
+    } else if (b.attn == TURTLE_ATTN_CHANNEL || b.attn == TURTLE_ATTN_FHR) {
+      chan(a, ch, b.heads);
+    } else if (b.attn == TURTLE_ATTN_CHM) {
+      const std::string s = a + ".spatial_aligner";
+      P(s + ".temperature", {1, 1, 1});
+      conv(s + ".qk", ch, 2 * ch, 1, 1, bias);
+      conv(s + ".qk_dwconv", 2 * ch, 2 * ch, 3, 2 * ch, bias);
+      conv(s + ".v", ch, ch, 1, 1, bias);
+      conv(s + ".v_dwconv", ch, ch, 3, ch, bias);
+      conv(s + ".k2", ch, 2 * ch, 1, 1, bias);
+      conv(s + ".k2_dwconv", 2 * ch, 2 * ch, b.ws, 2 * ch, bias);
+      conv(s + ".q2", ch, 2 * ch, 1, 1, bias);
+      conv(s + ".q2_dwconv", 2 * ch, 2 * ch, b.ws, 2 * ch, bias);
+      conv(s + ".project_out", ch, ch, 1, 1, bias);
+      chan(a + ".ChanAttn", ch, b.heads);
+      conv(a + ".kv", ch, 2 * ch, 1, 1, bias);
+      conv(a + ".kv_dwconv", 2 * ch, 2 * ch, 3, 2 * ch, bias);
+    }
+    ln(b.prefix + ".norm2", ch);
+    const std::string f = b.prefix + ".ffn";
+    if (b.ffn == TURTLE_FFN_GFFW) {
+      conv(f + ".project_in", ch, 2 * b.hidden, 1, 1, bias);
+      conv(f + ".dwconv", 2 * b.hidden, 2 * b.hidden, 3, 2 * b.hidden, bias);
+      conv(f + ".project_out", b.hidden, ch, 1, 1, bias);
+    } else {
+      P(f + ".gamma", {1, ch, 1, 1});
+      conv(f + ".conv4", ch, 2 * ch, 1, 1, true);
+      conv(f + ".conv5", 2 * ch, ch, 1, 1, true);
+    }
+  };
+  auto lvl = [&](int i) { for (auto& b : A.levels[i].blocks) block(b); };
+  conv("input_projection", A.in_ch, d, 3, 1, bias);
+  lvl(0); conv("down1_2.body.0", d, d / 2, 3, 1, false);
+  lvl(1); conv("down2_3.body.0", 2 * d, d, 3, 1, false);
+  lvl(2); conv("down3_4.body.0", 4 * d, 2 * d, 3, 1, false);
+  lvl(3);
+  conv("up4_3.body.0", 8 * d, 16 * d, 3, 1, false); conv("reduce_chan_level3", 8 * d, 4 * d, 1, 1, bias); lvl(4);
+  conv("up3_2.body.0", 4 * d, 8 * d, 3, 1, false); conv("reduce_chan_level2", 4 * d, 2 * d, 1, 1, bias); lvl(5);
+  conv("up2_1.body.0", 2 * d, 4 * d, 3, 1, false); conv("reduce_chan_level1", 2 * d, d, 1, 1, bias); lvl(6);
+  lvl(7);
+  conv("ending", d, A.out_ch, 3, 1, true);
+}
+
+// ------------------------------------------------------------------------------------------
+// packed weights
+// ------------------------------------------------------------------------------------------
+struct GemmW { size_t w = NONE, s = NONE, t = NONE, bias = NONE, scale = NONE; int N = 0, K = 0; bool ln = false; };
+struct DwW { size_t w = NONE, bias = NONE; int C = 0; };
+struct BlockW {
+  GemmW a_in, a_out, q2, k2, kv, f_in, f_out;
+  DwW a_dw, sab_qk_dw, sab_v_dw, fhr_dw, kv_dw, f_dw;
+  size_t q2_win = NONE, q2_winb = NONE, k2_win = NONE, k2_winb = NONE, sab_tau = NONE;
+  size_t wp = NONE, po_bias = NONE, tau = NONE;   // channel-attention projection (fp32) + temperature
+};
+struct ModelW {
+  size_t stem_w = NONE, stem_b = NONE, end_w = NONE, end_b = NONE;
+  GemmW down[3], up[3], reduce[3];
+  std::vector<std::vector<BlockW>> blocks;   // [level][block]
+};
+
+struct Packer {
+  std::vector<char> host;
+  bool bf16;
+  size_t align(size_t a = 256) { size_t o = (host.size() + a - 1) / a * a; host.resize(o); return o; }
+  size_t f32(const std::vector<double>& v) {
+    size_t o = align();
+    host.resize(o + v.size() * 4);
+    float* p = reinterpret_cast<float*>(host.data() + o);
+    for (size_t i = 0; i < v.size(); ++i) p[i] = (float)v[i];
+    return o;
+  }
+  // storage-typed matrix; returns offset and writes back the rounded values (for LN rowsums)
+  size_t stor(std::vector<double>& v) {
+    size_t o = align();
+    if (bf16) {
+      host.resize(o + v.size() * 2);
+      uint16_t* p = reinterpret_cast<uint16_t*>(host.data() + o);
+      for (size_t i = 0; i < v.size(); ++i) {
+        float f = (float)v[i];
+        uint32_t u; std::memcpy(&u, &f, 4);
+        uint32_t r = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+        p[i] = (uint16_t)r;
+        uint32_t back = r << 16; float fb; std::memcpy(&fb, &back, 4);
+        v[i] = fb;
+      }
+    } else {
+      host.resize(o + v.size() * 4);
+      float* p = reinterpret_cast<float*>(host.data() + o);
+      for (size_t i = 0; i < v.size(); ++i) { p[i] = (float)v[i]; v[i] = p[i]; }
+    }
+    return o;
+  }
+};
+
+struct TurtleHandle {
+  Arch arch;
+  std::map<std::string, std::vector<float>> staged;
+  ModelW mw;
+  char* dev = nullptr;
+  size_t dev_bytes = 0;
+  bool loaded = false;
+  bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
+  const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
+  const float* fptr(size_t off) const { return reinterpret_cast<const float*>(ptr(off)); }
+};
+
+static const std::vector<float>& W(TurtleHandle* h, const std::string& n) {
+  auto it = h->staged.find(n);
+  if (it == h->staged.end()) TFAIL(TURTLE_ENOWEIGHT, "missing weight " + n);
+  return it->second;
+}
+static bool has(TurtleHandle* h, const std::string& n) { return h->staged.count(n) != 0; }
+static std::vector<double> dvec(const std::vector<float>& v) { return std::vector<double>(v.begin(), v.end()); }
+
+// 1x1 conv [N][K] (+bias), optionally LayerNorm-folded with norm `lnname`; rows [r0, r1) of W
+static void pack_rows(const std::vector<float>& w, int K, int r0, int r1, std::vector<double>& out) {
+  for (int r = r0; r < r1; ++r)
+    for (int k = 0; k < K; ++k) out.push_back(w[(size_t)r * K + k]);
+}
+
+static GemmW pack_gemm(TurtleHandle* h, Packer& pk, std::vector<double> Wm, int N, int K,
+                       const std::string& lnname, std::vector<double> bias) {
+  GemmW g; g.N = N; g.K = K;
+  std::vector<double> s, t;
+  if (!lnname.empty()) {
+    g.ln = true;
+    const auto& gw = W(h, lnname + ".body.weight");
+    const bool bf = h->arch.cfg.layernorm_biasfree != 0;
+    std::vector<double> orig = Wm;
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < K; ++k) Wm[(size_t)n * K + k] *= gw[k];
+    g.w = pk.stor(Wm);   // rounds Wm in place
+    if (!bf) {
+      const auto& gb = W(h, lnname + ".body.bias");
+      s.assign(N, 0.0); t.assign(N, 0.0);
+      for (int n = 0; n < N; ++n)
+        for (int k = 0; k < K; ++k) { s[n] += Wm[(size_t)n * K + k]; t[n] += orig[(size_t)n * K + k] * gb[k]; }
+      g.s = pk.f32(s); g.t = pk.f32(t);
+    }
+  } else {
+    g.w = pk.stor(Wm);
+  }
+  if (!bias.empty()) g.bias = pk.f32(bias);
+  return g;
+}
+
+static std::vector<double> opt_bias(TurtleHandle* h, const std::string& n) {
+  return has(h, n) ? dvec(W(h, n)) : std::vector<double>();
+}
+
+static DwW pack_dw(TurtleHandle* h, Packer& pk, const std::string& n, int c0, int C, int taps = 9) {
+  // conv weight [Ctot][1][k][k] -> [taps][C] for channels [c0, c0 + C)
+  const auto& w = W(h, n + ".weight");
+  std::vector<double> o((size_t)taps * C);
+  for (int c = 0; c < C; ++c)
+    for (int t = 0; t < taps; ++t) o[(size_t)t * C + c] = w[(size_t)(c0 + c) * taps + t];
+  DwW d; d.C = C; d.w = pk.f32(o);
+  if (has(h, n + ".bias")) {
+    const auto& b = W(h, n + ".bias");
+    d.bias = pk.f32(std::vector<double>(b.begin() + c0, b.begin() + c0 + C));
+  }
+  return d;
+}
+
+// dense 3x3 [Cout][Cin][3][3] -> [Cout'][9][Cin], with an optional output-channel permutation
+static GemmW pack_conv3(TurtleHandle* h, Packer& pk, const std::string& n, int Cin, int Cout, bool shuffle_perm) {
+  const auto& w = W(h, n + ".weight");
+  std::vector<double> o((size_t)Cout * 9 * Cin);
+  const int Cq = Cout / 4;
+  for (int np = 0; np < Cout; ++np) {
+    // PixelShuffle(2): input channel c*4 + s -> output channel c at sub-pixel s; store row s*Cq + c
+    const int src = shuffle_perm ? (np % Cq) * 4 + np / Cq : np;
+    for (int ci = 0; ci < Cin; ++ci)
+      for (int t = 0; t < 9; ++t) o[((size_t)np * 9 + t) * Cin + ci] = w[((size_t)src * Cin + ci) * 9 + t];
+  }
+  GemmW g; g.N = Cout; g.K = 9 * Cin; g.w = pk.stor(o);
+  return g;
+}
+
+static void pack_all(TurtleHandle* h) {
+  Arch& A = h->arch;
+  Packer pk; pk.bf16 = h->bf16();
+  ModelW& M = h->mw;
+  const int d = A.dim;
+  M.stem_w = pk.f32(dvec(W(h, "input_projection.weight")));
+  if (has(h, "input_projection.bias")) M.stem_b = pk.f32(dvec(W(h, "input_projection.bias")));
+  M.end_w = pk.f32(dvec(W(h, "ending.weight")));
+  M.end_b = pk.f32(dvec(W(h, "ending.bias")));
+  const char* downs[3] = {"down1_2.body.0", "down2_3.body.0", "down3_4.body.0"};
+  const char* ups[3] = {"up4_3.body.0", "up3_2.body.0", "up2_1.body.0"};
+  const char* reds[3] = {"reduce_chan_level3", "reduce_chan_level2", "reduce_chan_level1"};
+  for (int i = 0; i < 3; ++i) {
+    const int c = d << i;                 // down i: level i channels -> c/2 (then unshuffle x4)
+    M.down[i] = pack_conv3(h, pk, downs[i], c, c / 2, false);
+    const int cu = d << (3 - i);          // up i: level (3-i) channels -> 2c, shuffled to c/2
+    M.up[i] = pack_conv3(h, pk, ups[i], cu, 2 * cu, true);
+    const int cr = cu;                    // reduce: cat(up c/2, skip c/2) = cu -> cu/2
+    M.reduce[i] = pack_gemm(h, pk, dvec(W(h, std::string(reds[i]) + ".weight")), cr / 2, cr, "",
+                            opt_bias(h, std::string(reds[i]) + ".bias"));
+  }
+  M.blocks.clear();
+  for (auto& L : A.levels) {
+    std::vector<BlockW> bws;
+    for (auto& b : L.blocks) {
+      BlockW bw;
+      const int c = b.dim;
+      const std::string n1 = b.prefix + ".norm1", n2 = b.prefix + ".norm2", a = b.prefix + ".attn", f = b.prefix + ".ffn";
+      if (b.attn == TURTLE_ATTN_REDUCED) {
+        bw.a_in = pack_gemm(h, pk, dvec(W(h, a + ".conv1.weight")), 2 * c, c, n1, dvec(W(h, a + ".conv1.bias")));
+        bw.a_dw = pack_dw(h, pk, a + ".conv2", 0, 2 * c);
+        bw.a_out = pack_gemm(h, pk, dvec(W(h, a + ".conv3.weight")), c, 2 * c, "", dvec(W(h, a + ".conv3.bias")));
+        bw.a_out.scale = pk.f32(dvec(W(h, a + ".beta")));
+      } else if (b.attn == TURTLE_ATTN_CHANNEL || b.attn == TURTLE_ATTN_FHR) {
+        bw.a_in = pack_gemm(h, pk, dvec(W(h, a + ".qkv.weight")), 3 * c, c, n1, opt_bias(h, a + ".qkv.bias"));
+        bw.a_dw = pack_dw(h, pk, a + ".qkv_dwconv", 0, 3 * c);
+        bw.wp = pk.f32(dvec(W(h, a + ".project_out.weight")));
+        if (has(h, a + ".project_out.bias")) bw.po_bias = pk.f32(dvec(W(h, a + ".project_out.bias")));
+        bw.tau = pk.f32(dvec(W(h, a + ".temperature")));
+      } else if (b.attn == TURTLE_ATTN_CHM) {
+        const std::string s = a + ".spatial_aligner", ca = a + ".ChanAttn";
+        // one LN-folded GEMM for everything that reads norm1(x): [SAB qk | SAB v | FHR qkv]
+        std::vector<double> w6, b6;
+        pack_rows(W(h, s + ".qk.weight"), c, 0, 2 * c, w6);
+        pack_rows(W(h, s + ".v.weight"), c, 0, c, w6);
+        pack_rows(W(h, ca + ".qkv.weight"), c, 0, 3 * c, w6);
+        if (A.cfg.bias) {
+          for (auto x : W(h, s + ".qk.bias")) b6.push_back(x);
+          for (auto x : W(h, s + ".v.bias")) b6.push_back(x);
+          for (auto x : W(h, ca + ".qkv.bias")) b6.push_back(x);
+        }
+        bw.a_in = pack_gemm(h, pk, w6, 6 * c, c, n1, b6);
+        bw.sab_qk_dw = pack_dw(h, pk, s + ".qk_dwconv", 0, 2 * c);
+        bw.sab_v_dw = pack_dw(h, pk, s + ".v_dwconv", 0, c);
+        bw.fhr_dw = pack_dw(h, pk, ca + ".qkv_dwconv", 0, 3 * c);
+        bw.q2 = pack_gemm(h, pk, dvec(W(h, s + ".q2.weight")), 2 * c, c, "", opt_bias(h, s + ".q2.bias"));
+        bw.k2 = pack_gemm(h, pk, dvec(W(h, s + ".k2.weight")), 2 * c, c, "", opt_bias(h, s + ".k2.bias"));
+        const int taps = b.ws * b.ws;
+        DwW qw = pack_dw(h, pk, s + ".q2_dwconv", 0, 2 * c, taps), kw = pack_dw(h, pk, s + ".k2_dwconv", 0, 2 * c, taps);
+        bw.q2_win = qw.w; bw.q2_winb = qw.bias; bw.k2_win = kw.w; bw.k2_winb = kw.bias;
+        bw.sab_tau = pk.f32(dvec(W(h, s + ".temperature")));
+        // kv(project_out_sab(o)) = (W_kv W_po) o + (W_kv b_po + b_kv): one GEMM over the T frames
+        const auto& wkv = W(h, a + ".kv.weight");
+        const auto& wpo = W(h, s + ".project_out.weight");
+        std::vector<double> wm((size_t)2 * c * c, 0.0), bm;
+        for (int o = 0; o < 2 * c; ++o)
+          for (int j = 0; j < c; ++j) {
+            double acc = 0;
+            for (int i = 0; i < c; ++i) acc += (double)wkv[(size_t)o * c + i] * wpo[(size_t)i * c + j];
+            wm[(size_t)o * c + j] = acc;
+          }
+        if (has(h, a + ".kv.bias") || has(h, s + ".project_out.bias")) {
+          bm.assign(2 * c, 0.0);
+          for (int o = 0; o < 2 * c; ++o) {
+            double acc = has(h, a + ".kv.bias") ? W(h, a + ".kv.bias")[o] : 0.0;
+            if (has(h, s + ".project_out.bias"))
+              for (int i = 0; i < c; ++i) acc += (double)wkv[(size_t)o * c + i] * W(h, s + ".project_out.bias")[i];
+            bm[o] = acc;
+          }
+        }
+        bw.kv = pack_gemm(h, pk, wm, 2 * c, c, "", bm);
+        bw.kv_dw = pack_dw(h, pk, a + ".kv_dwconv", 0, 2 * c);
+        bw.wp = pk.f32(dvec(W(h, ca + ".project_out.weight")));
+        if (has(h, ca + ".project_out.bias")) bw.po_bias = pk.f32(dvec(W(h, ca + ".project_out.bias")));
+        bw.tau = pk.f32(dvec(W(h, ca + ".temperature")));
+      }
+      if (b.ffn == TURTLE_FFN_GFFW) {
+        bw.f_in = pack_gemm(h, pk, dvec(W(h, f + ".project_in.weight")), 2 * b.hidden, c, n2, opt_bias(h, f + ".project_in.bias"));
+        bw.f_dw = pack_dw(h, pk, f + ".dwconv", 0, 2 * b.hidden);
+        bw.f_out = pack_gemm(h, pk, dvec(W(h, f + ".project_out.weight")), c, b.hidden, "", opt_bias(h, f + ".project_out.bias"));
+      } else {
+        bw.f_in = pack_gemm(h, pk, dvec(W(h, f + ".conv4.weight")), 2 * c, c, n2, dvec(W(h, f + ".conv4.bias")));
+        bw.f_out = pack_gemm(h, pk, dvec(W(h, f + ".conv5.weight")), c, 2 * c, "", dvec(W(h, f + ".conv5.bias")));
+        bw.f_out.scale = pk.f32(dvec(W(h, f + ".gamma")));
+      }
+      bws.push_back(bw);
+    }
+    M.blocks.push_back(bws);
+  }
+  pk.align();
+  if (h->dev) { (void)hipFree(h->dev); h->dev = nullptr; }
+  HIPCHK(hipMalloc(&h->dev, pk.host.size()));
+  HIPCHK(hipMemcpy(h->dev, pk.host.data(), pk.host.size(), hipMemcpyHostToDevice));
+  h->dev_bytes = pk.host.size();
+}
+
+// ------------------------------------------------------------------------------------------
+// frame driver
+// ------------------------------------------------------------------------------------------
+struct Arena {
+  char* base;
+  size_t cap, off = 0, peak = 0;
+  bool dry;
+  void* alloc(size_t bytes) {
+    size_t o = (off + 255) / 256 * 256;
+    off = o + bytes;
+    peak = std::max(peak, off);
+    if (!dry && off > cap) TFAIL(TURTLE_EINVAL, "workspace too small");
+    return dry ? nullptr : base + o;
+  }
+};
+
+struct CacheIO {
+  const void* k_in[8]; const void* v_in[8]; int t_in[8];
+  void* k_out[8]; void* v_out[8];
+};
+
+template <typename T>
+struct Runner {
+  TurtleHandle* h;
+  hipStream_t st;
+  Arena ar;
+  int B, Hp, Wp;
+  const CacheIO* io;
+  static constexpr size_t ES = sizeof(T);
+
+  T* buf(int64_t elems) { return reinterpret_cast<T*>(ar.alloc((size_t)elems * ES)); }
+  float* fbuf(int64_t elems) { return reinterpret_cast<float*>(ar.alloc((size_t)elems * 4)); }
+  bool dry() const { return ar.dry; }
+
+  static SrcList src1(const void* p, int64_t ld, int off, int K, int mul = 1, int add = 0) {
+    SrcList s{}; s.n = 1; s.Ktot = K; s.s[0] = SrcDesc{p, ld, off, K, mul, add};
+    return s;
+  }
+  void gemm(const GemmW& w, const SrcList& a, int64_t M, int HW, int Wimg, void* out, int64_t ldo, int offo,
+            const void* res = nullptr, int64_t ldr = 0, int offr = 0, int gelu = 0,
+            int store = STORE_NHWC, const void* wptr = nullptr, int64_t wstride = 0, int wdiv = 1,
+            int N = -1, const float* bias = nullptr, int conv3 = 0, int cin = 0) {
+    if (dry()) return;
+    GemmArgs g{};
+    g.a = a; g.M = M; g.N = N >= 0 ? N : w.N; g.HW = HW; g.Wimg = Wimg;
+    g.w = wptr ? wptr : h->ptr(w.w); g.ldw = a.Ktot; g.wstride = wstride; g.wdiv = wdiv;
+    g.conv3 = conv3; g.cin = cin;
+    g.ln = w.ln; g.ln_s = h->fptr(w.s); g.ln_t = h->fptr(w.t);
+    g.bias = bias ? bias : h->fptr(w.bias); g.scale = h->fptr(w.scale); g.gelu = gelu;
+    g.res = res; g.ldr = ldr; g.offr = offr;
+    g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store;
+    if (wstride && HW % 128) TFAIL(TURTLE_EINVAL, "per-image weights need HW % 128 == 0");
+    if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
+    launch_gemm<T>(g, st);
+  }
+  void dw(const DwW& w, const void* in, int64_t ldi, int offi, void* out, int64_t ldo, int offo,
+          int nimg, int H, int Wd, int mode, int tok_ws = 0, int64_t tok_stride = 0) {
+    if (dry()) return;
+    DwArgs a{};
+    a.in = in; a.ldi = ldi; a.offi = offi; a.out = out; a.ldo = ldo; a.offo = offo;
+    a.w = h->fptr(w.w); a.bias = h->fptr(w.bias);
+    a.nimg = nimg; a.H = H; a.W = Wd; a.C = mode == DW_GATE ? w.C / 2 : w.C; a.mode = mode;
+    a.tok_ws = tok_ws; a.tok_img_stride = tok_stride;
+    launch_dw<T>(a, st);
+  }
+
+  struct Seg { const void* base; int64_t ld; int off; int hstride; int mul, add; int norm; int64_t col; int colh; };
+
+  // channel attention core: Gram over (q, key segments), softmax, W_eff, then out = x + W_eff [v srcs]
+  void chan_attn(const BlockW& bw, const Blk& b, const T* q, int64_t ldq, int qoff, const std::vector<Seg>& segs,
+                 const SrcList& vsrc, int HW, int Wimg, T* x, float* kinv, int cur_seg) {
+    const int c = b.dim, ch = c / b.heads, nseg = (int)segs.size(), ncol = nseg * ch;
+    int nchunk = std::max(1, std::min((HW + 2047) / 2048, std::max(1, 1024 / (B * b.heads))));
+    int chunk = (HW + nchunk - 1) / nchunk;
+    chunk = (chunk + 31) / 32 * 32;
+    nchunk = (HW + chunk - 1) / chunk;
+    const int stride = ch * ncol + ch + ncol;
+    float* part = fbuf((int64_t)B * b.heads * nchunk * stride);
+    float* red = fbuf((int64_t)B * b.heads * stride);
+    float* attn = fbuf((int64_t)B * b.heads * ch * ncol);
+    T* weff = buf((int64_t)B * c * vsrc.Ktot);
+    if (dry()) return;
+    GramArgs g{};
+    g.q = q; g.ldq = ldq; g.qoff = qoff; g.nseg = nseg;
+    unsigned mask = 0;
+    for (int s = 0; s < nseg; ++s) {
+      g.seg[s] = GramSeg{segs[s].base, segs[s].ld, segs[s].off, segs[s].hstride, segs[s].mul, segs[s].add, segs[s].norm};
+      if (segs[s].norm) mask |= 1u << s;
+    }
+    g.B = B; g.heads = b.heads; g.ch = ch; g.HW = HW; g.nchunk = nchunk; g.chunk = chunk; g.part = part;
+    launch_gram<T>(g, st);
+    AttnFinArgs f{};
+    f.part = part; f.nchunk = nchunk; f.B = B; f.heads = b.heads; f.ch = ch; f.nseg = nseg; f.norm_mask = mask;
+    f.tau = h->fptr(bw.tau); f.red = red; f.attn = attn; f.kinv = kinv; f.cur_seg = cur_seg;
+    launch_attn_finalize(f, st);
+    WeffArgs we{};
+    we.attn = attn; we.wp = h->fptr(bw.wp); we.B = B; we.heads = b.heads; we.ch = ch; we.nseg = nseg; we.C = c;
+    for (int s = 0; s < nseg; ++s) { we.seg_col[s] = segs[s].col; we.seg_hstride[s] = segs[s].colh; }
+    we.Keff = vsrc.Ktot; we.weff = weff;
+    launch_weff<T>(we, st);
+    GemmW pw; pw.N = c; pw.K = vsrc.Ktot;
+    gemm(pw, vsrc, (int64_t)B * HW, HW, Wimg, x, c, 0, x, c, 0, 0, STORE_NHWC, weff, (int64_t)c * vsrc.Ktot, 1, c,
+         h->fptr(bw.po_bias));
+  }
+
+  void block(const Blk& b, const BlockW& bw, T* x, int H, int Wd) {
+    const int c = b.dim, HW = H * Wd;
+    const int64_t P = (int64_t)B * HW;
+    const size_t mark = ar.off;
+    if (b.attn == TURTLE_ATTN_REDUCED) {
+      T* t1 = buf(P * 2 * c);
+      T* t2 = buf(P * 2 * c);
+      gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * c, 0);
+      dw(bw.a_dw, t1, 2 * c, 0, t2, 2 * c, 0, B, H, Wd, DW_GELU);
+      gemm(bw.a_out, src1(t2, 2 * c, 0, 2 * c), P, HW, Wd, x, c, 0, x, c, 0);
+    } else if (b.attn == TURTLE_ATTN_CHANNEL || (b.attn == TURTLE_ATTN_FHR && b.cache_slot < 0)) {
+      T* t1 = buf(P * 3 * c);
+      T* t2 = buf(P * 3 * c);
+      gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
+      dw(bw.a_dw, t1, 3 * c, 0, t2, 3 * c, 0, B, H, Wd, DW_PLAIN);
+      const int ch = c / b.heads;
+      std::vector<Seg> segs{{t2, 3 * c, c, ch, 1, 0, 1, 0, ch}};
+      chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t2, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1);
+    } else if (b.attn == TURTLE_ATTN_FHR) {
+      fhr(b, bw, x, H, Wd);
+    } else if (b.attn == TURTLE_ATTN_CHM) {
+      chm(b, bw, x, H, Wd);
+    }
+    ar.off = mark;
+    // feed-forward
+    if (b.ffn == TURTLE_FFN_GFFW) {
+      const int hd = b.hidden;
+      T* t1 = buf(P * 2 * hd);
+      T* t2 = buf(P * hd);
+      gemm(bw.f_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * hd, 0);
+      dw(bw.f_dw, t1, 2 * hd, 0, t2, hd, 0, B, H, Wd, DW_GATE);
+      gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
+    } else {
+      T* t1 = buf(P * 2 * c);
+      gemm(bw.f_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * c, 0, nullptr, 0, 0, /*gelu*/ 1);
+      gemm(bw.f_out, src1(t1, 2 * c, 0, 2 * c), P, HW, Wd, x, c, 0, x, c, 0);
+    }
+    ar.off = mark;
+  }
+
+  // latent FrameHistoryRouter with cache slot (turtle_t1_arch.py:218-286)
+  void fhr(const Blk& b, const BlockW& bw, T* x, int H, int Wd) {
+    const int c = b.dim, HW = H * Wd, ch = c / b.heads, slot = b.cache_slot;
+    const int64_t P = (int64_t)B * HW;
+    const int R = io->t_in[slot];
+    const int Rnew = std::min(R + ch, b.ntc * ch);
+    T* t1 = buf(P * 3 * c);
+    T* t2 = buf(P * 3 * c);
+    float* kinv = fbuf((int64_t)B * c);
+    gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
+    dw(bw.a_dw, t1, 3 * c, 0, t2, 3 * c, 0, B, H, Wd, DW_PLAIN);
+    std::vector<Seg> segs;
+    const int Tc = R / ch;
+    for (int t = 0; t < Tc; ++t)
+      segs.push_back(Seg{io->k_in[slot], (int64_t)b.heads * R, t * ch, R, 1, 0, 0, (int64_t)t * ch, R});
+    segs.push_back(Seg{t2, 3 * c, c, ch, 1, 0, 1, (int64_t)b.heads * R, ch});
+    SrcList vs{};
+    if (R) { vs.s[vs.n++] = SrcDesc{io->v_in[slot], (int64_t)b.heads * R, 0, b.heads * R, 1, 0}; }
+    vs.s[vs.n++] = SrcDesc{t2, 3 * c, 2 * c, c, 1, 0};
+    vs.Ktot = b.heads * R + c;
+    // the new cache reads the pre-attention current k/v, so roll it before x is updated in place
+    chan_attn(bw, b, t2, 3 * c, 0, segs, vs, HW, Wd, x, kinv, Tc);
+    if (dry()) return;
+    FhrCacheArgs fk{};
+    fk.old = io->k_in[slot]; fk.R = R; fk.cur = t2; fk.ldc = 3 * c; fk.coff = c; fk.kinv = kinv;
+    fk.out = io->k_out[slot]; fk.Rnew = Rnew; fk.B = B; fk.P = HW; fk.heads = b.heads; fk.ch = ch;
+    launch_fhr_cache<T>(fk, st);
+    FhrCacheArgs fv = fk;
+    fv.old = io->v_in[slot]; fv.coff = 2 * c; fv.kinv = nullptr; fv.out = io->v_out[slot];
+    launch_fhr_cache<T>(fv, st);
+  }
+
+  // Causal History Model: SAB + kv conv on the aligned frames + FHR (turtle_t1_arch.py:612-662)
+  void chm(const Blk& b, const BlockW& bw, T* x, int H, int Wd) {
+    const int c = b.dim, HW = H * Wd, ch = c / b.heads, ws = b.ws, slot = b.cache_slot;
+    const int64_t P = (int64_t)B * HW;
+    const int th = H / ws, tw = Wd / ws, N = th * tw, d2 = 2 * c, D = ws * ws * c;
+    if (N < 5) TFAIL(TURTLE_EINVAL, "selected index k out of range: SAB needs >= 5 tokens (input too small)");
+    const int Tin = slot >= 0 ? io->t_in[slot] : 0;
+    const int NT = Tin + 1;
+    const int Tnew = std::min(NT, b.ntc);
+    // SAB caches: fresh outputs (slot) or scratch (a CHM outside a cache slot discards them)
+    T* kout = slot >= 0 ? reinterpret_cast<T*>(io->k_out[slot]) : buf((int64_t)B * Tnew * N * d2);
+    T* vout = slot >= 0 ? reinterpret_cast<T*>(io->v_out[slot]) : buf((int64_t)B * Tnew * N * D);
+    const T* kin = slot >= 0 ? reinterpret_cast<const T*>(io->k_in[slot]) : nullptr;
+    const T* vin = slot >= 0 ? reinterpret_cast<const T*>(io->v_in[slot]) : nullptr;
+    T* t6 = buf(P * 6 * c);
+    T* qkd = buf(P * 2 * c);
+    T* fq = buf(P * 3 * c);
+    T* q2f = buf(P * d2);
+    T* k2f = buf(P * d2);
+    T* qtok = buf((int64_t)B * N * d2);
+    float* topv = fbuf((int64_t)B * NT * N * 5);
+    int* topi = reinterpret_cast<int*>(fbuf((int64_t)B * NT * N * 5));
+    T* xs = buf(P * NT * c);
+    T* kv = buf(P * NT * 2 * c);
+    T* kvd = buf(P * NT * 2 * c);
+    // LN(x) -> [SAB qk | SAB v | FHR qkv]
+    gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t6, 6 * c, 0);
+    dw(bw.sab_qk_dw, t6, 6 * c, 0, qkd, 2 * c, 0, B, H, Wd, DW_PLAIN);
+    dw(bw.sab_v_dw, t6, 6 * c, 2 * c, vout + (int64_t)(Tnew - 1) * N * D, 0, 0, B, H, Wd, DW_PLAIN, ws, (int64_t)Tnew * N * D);
+    dw(bw.fhr_dw, t6, 6 * c, 3 * c, fq, 3 * c, 0, B, H, Wd, DW_PLAIN);
+    gemm(bw.q2, src1(qkd, 2 * c, 0, c), P, HW, Wd, q2f, d2, 0);
+    gemm(bw.k2, src1(qkd, 2 * c, c, c), P, HW, Wd, k2f, d2, 0);
+    if (!dry()) {
+      WinArgs wa{};
+      wa.in = q2f; wa.ldi = d2; wa.offi = 0; wa.w = h->fptr(bw.q2_win); wa.bias = h->fptr(bw.q2_winb);
+      wa.out = qtok; wa.out_img_stride = (int64_t)N * d2; wa.nimg = B; wa.H = H; wa.W = Wd; wa.C = d2; wa.ws = ws;
+      launch_window<T>(wa, st);
+      wa.in = k2f; wa.w = h->fptr(bw.k2_win); wa.bias = h->fptr(bw.k2_winb);
+      wa.out = kout + (int64_t)(Tnew - 1) * N * d2; wa.out_img_stride = (int64_t)Tnew * N * d2;
+      launch_window<T>(wa, st);
+      // keep the last Tnew-1 cached frames in the new cache (reference: cat then [-ntc:])
+      if (Tnew > 1) {
+        const int keep = Tnew - 1, first = Tin - keep;
+        HIPCHK(hipMemcpy2DAsync(kout, (size_t)Tnew * N * d2 * ES, kin + (int64_t)first * N * d2, (size_t)Tin * N * d2 * ES,
+                                (size_t)keep * N * d2 * ES, B, hipMemcpyDeviceToDevice, st));
+        HIPCHK(hipMemcpy2DAsync(vout, (size_t)Tnew * N * D * ES, vin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
+                                (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
+      }
+      if (NT > TURTLE_MAX_T) TFAIL(TURTLE_EINVAL, "too many cached frames");
+      SabScoreArgs sa{};
+      sa.q = qtok; sa.q_bstride = (int64_t)N * d2; sa.B = B; sa.T = NT; sa.N = N; sa.d = d2;
+      sa.tau = h->fptr(bw.sab_tau); sa.topv = topv; sa.topi = topi;
+      SabAvArgs va{};
+      va.q = qtok; va.q_bstride = (int64_t)N * d2; va.B = B; va.T = NT; va.N = N; va.d = d2;
+      va.th = th; va.tw = tw; va.ws = ws; va.C = c; va.tau = sa.tau; va.topv = topv; va.topi = topi; va.out = xs;
+      for (int t = 0; t < NT; ++t) {
+        if (t < Tin) {
+          sa.k[t] = kin + (int64_t)t * N * d2; sa.k_bstride[t] = (int64_t)Tin * N * d2;
+          va.v[t] = vin + (int64_t)t * N * D; va.v_bstride[t] = (int64_t)Tin * N * D;
+        } else {
+          sa.k[t] = kout + (int64_t)(Tnew - 1) * N * d2; sa.k_bstride[t] = (int64_t)Tnew * N * d2;
+          va.v[t] = vout + (int64_t)(Tnew - 1) * N * D; va.v_bstride[t] = (int64_t)Tnew * N * D;
+        }
+        va.k[t] = sa.k[t]; va.k_bstride[t] = sa.k_bstride[t];
+      }
+      launch_sab_score<T>(sa, st);
+      launch_sab_av<T>(va, st);
+    }
+    // kv = (W_kv W_po) xs over the B*T aligned frames, then dw3x3 per frame
+    gemm(bw.kv, src1(xs, c, 0, c), P * NT, HW, Wd, kv, 2 * c, 0);
+    dw(bw.kv_dw, kv, 2 * c, 0, kvd, 2 * c, 0, B * NT, H, Wd, DW_PLAIN);
+    // FHR(x, k_hist, v_hist): keys = [hist frames..., current]
+    std::vector<Seg> segs;
+    SrcList vs{};
+    for (int t = 0; t < NT; ++t) {
+      segs.push_back(Seg{kvd, 2 * c, 0, ch, NT, t, 1, (int64_t)t * c, ch});
+      vs.s[vs.n++] = SrcDesc{kvd, 2 * c, c, c, NT, t};
+    }
+    segs.push_back(Seg{fq, 3 * c, c, ch, 1, 0, 1, (int64_t)NT * c, ch});
+    vs.s[vs.n++] = SrcDesc{fq, 3 * c, 2 * c, c, 1, 0};
+    vs.Ktot = (NT + 1) * c;
+    if ((int)segs.size() > TURTLE_MAX_SEG || vs.n > TURTLE_MAX_SRC) TFAIL(TURTLE_EINVAL, "too many history frames");
+    chan_attn(bw, b, fq, 3 * c, 0, segs, vs, HW, Wd, x, nullptr, -1);
+  }
+
+  void level(int li, T* x, int H, int Wd) {
+    const auto& L = h->arch.levels[li];
+    static const BlockW none{};   // workspace sizing runs before (or without) packed weights
+    for (size_t i = 0; i < L.blocks.size(); ++i)
+      block(L.blocks[i], dry() && h->mw.blocks.empty() ? none : h->mw.blocks[li][i], x, H, Wd);
+  }
+
+  void run(const float* inp, int Hin, int Win, float* out, int Hout, int Wout) {
+    const Arch& A = h->arch;
+    const int d = A.dim;
+    const int64_t P1 = (int64_t)B * Hp * Wp;
+    T* e1 = buf(P1 * d);
+    T* e2 = buf(P1 / 4 * 2 * d);
+    T* e3 = buf(P1 / 16 * 4 * d);
+    T* lat = buf(P1 / 64 * 8 * d);
+    T* d3 = buf(P1 / 16 * 4 * d);
+    T* d2 = buf(P1 / 4 * 2 * d);
+    T* d1 = buf(P1 * d);
+    T* up = buf(P1 * d);      // Upsample output, largest at level 1: P1 * d/2... sized generously
+    if (!dry()) {
+      StemArgs s{};
+      s.inp = inp; s.in_bstride = (int64_t)2 * A.cfg.n_colors * Hin * Win; s.in_fstride = (int64_t)A.cfg.n_colors * Hin * Win;
+      s.B = B; s.Cimg = A.cfg.n_colors; s.Hin = Hin; s.Win = Win; s.Hp = Hp; s.Wp = Wp;
+      s.use_both = A.cfg.use_both_input; s.sr = A.cfg.super_resolution;
+      s.w = h->fptr(h->mw.stem_w); s.bias = h->fptr(h->mw.stem_b); s.Cout = d; s.out = e1;
+      launch_stem<T>(s, st);
+    }
+    int H = Hp, Wd = Wp;
+    level(0, e1, H, Wd);
+    auto down = [&](int i, const T* x, int c, T* y, int H0, int W0) {
+      gemm(h->mw.down[i], src1(x, c, 0, 9 * c), (int64_t)B * H0 * W0, H0 * W0, W0, y, 2 * c, 0, nullptr, 0, 0, 0,
+           STORE_UNSHUFFLE, nullptr, 0, 1, -1, nullptr, 1, c);
+    };
+    down(0, e1, d, e2, Hp, Wp);
+    level(1, e2, Hp / 2, Wp / 2);
+    down(1, e2, 2 * d, e3, Hp / 2, Wp / 2);
+    level(2, e3, Hp / 4, Wp / 4);
+    down(2, e3, 4 * d, lat, Hp / 4, Wp / 4);
+    level(3, lat, Hp / 8, Wp / 8);
+    auto upcat = [&](int i, const T* x, int c, int H0, int W0, const T* skip, T* y) {
+      // Upsample (3x3 c->2c + PixelShuffle) into `up`, then reduce_chan over [up | skip]
+      gemm(h->mw.up[i], src1(x, c, 0, 9 * c), (int64_t)B * H0 * W0, H0 * W0, W0, up, c / 2, 0, nullptr, 0, 0, 0,
+           STORE_SHUFFLE, nullptr, 0, 1, -1, nullptr, 1, c);
+      SrcList s{}; s.n = 2; s.Ktot = c;
+      s.s[0] = SrcDesc{up, c / 2, 0, c / 2, 1, 0};
+      s.s[1] = SrcDesc{skip, c / 2, 0, c / 2, 1, 0};
+      const int H1 = 2 * H0, W1 = 2 * W0;
+      gemm(h->mw.reduce[i], s, (int64_t)B * H1 * W1, H1 * W1, W1, y, c / 2, 0);
+    };
+    upcat(0, lat, 8 * d, Hp / 8, Wp / 8, e3, d3);
+    level(4, d3, Hp / 4, Wp / 4);
+    upcat(1, d3, 4 * d, Hp / 4, Wp / 4, e2, d2);
+    level(5, d2, Hp / 2, Wp / 2);
+    upcat(2, d2, 2 * d, Hp / 2, Wp / 2, e1, d1);
+    level(6, d1, Hp, Wp);
+    level(7, d1, Hp, Wp);
+    if (!dry()) {
+      EndArgs e{};
+      e.x = d1; e.Cin = d; e.w = h->fptr(h->mw.end_w); e.bias = h->fptr(h->mw.end_b);
+      e.inp = inp; e.in_bstride = (int64_t)2 * A.cfg.n_colors * Hin * Win; e.in_fstride = (int64_t)A.cfg.n_colors * Hin * Win;
+      e.B = B; e.Cimg = A.cfg.n_colors; e.Hin = Hin; e.Win = Win; e.Hp = Hp; e.Wp = Wp; e.Hout = Hout; e.Wout = Wout;
+      e.sr = A.cfg.super_resolution; e.out = out;
+      launch_ending<T>(e, st);
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+template <typename F>
+static int guard(F&& f) {
+  try {
+    f();
+    return TURTLE_OK;
+  } catch (const TurtleError& e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return TURTLE_EINVAL;
+  }
+}
+
+static void padded(const TurtleHandle* h, int H, int W, int& Hp, int& Wp, int& Hout, int& Wout) {
+  const int s = h->arch.cfg.super_resolution ? 4 : 1;
+  Hout = H * s; Wout = W * s;
+  Hp = (Hout + 31) / 32 * 32;
+  Wp = (Wout + 31) / 32 * 32;
+}
+
+template <typename T>
+static size_t ws_size(TurtleHandle* h, int B, int H, int W) {
+  int Hp, Wp, Ho, Wo;
+  padded(h, H, W, Hp, Wp, Ho, Wo);
+  CacheIO io{};
+  for (const auto& L : h->arch.levels)
+    for (const auto& b : L.blocks)
+      if (b.cache_slot >= 0) io.t_in[b.cache_slot] = b.attn == TURTLE_ATTN_FHR ? b.ntc * (b.dim / b.heads) : b.ntc;
+  Runner<T> r{h, nullptr, Arena{nullptr, 0, 0, 0, true}, B, Hp, Wp, &io};
+  r.run(nullptr, H, W, nullptr, Ho, Wo);
+  return r.ar.peak + 4096;
+}
+
+extern "C" {
+
+const char* turtle_last_error(void) { return g_err.c_str(); }
+
+int turtle_create(const TurtleConfig* cfg, TurtleHandle** out) {
+  return guard([&] {
+    if (!cfg || !out) TFAIL(TURTLE_EINVAL, "null argument");
+    auto* h = new TurtleHandle();
+    h->arch.cfg = *cfg;
+    try {
+      build_arch(h->arch);
+    } catch (...) {
+      delete h;
+      throw;
+    }
+    *out = h;
+  });
+}
+
+void turtle_destroy(TurtleHandle* h) {
+  if (!h) return;
+  if (h->dev) (void)hipFree(h->dev);
+  delete h;
+}
+
+int turtle_num_weights(const TurtleHandle* h) { return h ? (int)h->arch.params.size() : 0; }
+
+int turtle_weight_info(const TurtleHandle* h, int idx, const char** name, int* ndim, int64_t shape[4]) {
+  return guard([&] {
+    if (!h || idx < 0 || idx >= (int)h->arch.params.size()) TFAIL(TURTLE_EINVAL, "weight index out of range");
+    const auto& p = h->arch.params[idx];
+    *name = p.first.c_str();
+    *ndim = (int)p.second.size();
+    for (int i = 0; i < 4; ++i) shape[i] = i < *ndim ? p.second[i] : 1;
+  });
+}
+
+int turtle_set_weight(TurtleHandle* h, const char* name, const float* data, int64_t numel) {
+  return guard([&] {
+    if (!h || !name || !data) TFAIL(TURTLE_EINVAL, "null argument");
+    for (const auto& p : h->arch.params) {
+      if (p.first != name) continue;
+      int64_t n = 1;
+      for (auto s : p.second) n *= s;
+      if (n != numel) TFAIL(TURTLE_ENOWEIGHT, std::string("size mismatch for ") + name);
+      h->staged[name] = std::vector<float>(data, data + numel);
+      h->loaded = false;
+      return;
+    }
+    TFAIL(TURTLE_ENOWEIGHT, std::string("unexpected key ") + name + " in state_dict");
+  });
+}
+
+int turtle_load_weights(TurtleHandle* h) {
+  return guard([&] {
+    if (!h) TFAIL(TURTLE_EINVAL, "null handle");
+    for (const auto& p : h->arch.params)
+      if (!h->staged.count(p.first)) TFAIL(TURTLE_ENOWEIGHT, "missing key " + p.first + " in state_dict");
+    pack_all(h);
+    h->loaded = true;
+  });
+}
+
+int turtle_cache_layout(const TurtleHandle* h, int B, int H, int W, const int t_in[8], int kind[8],
+                        int64_t k_shape[40], int64_t v_shape[40]) {
+  return guard([&] {
+    if (!h || B <= 0 || H <= 0 || W <= 0) TFAIL(TURTLE_EINVAL, "bad shape");
+    int Hp, Wp, Ho, Wo;
+    padded(h, H, W, Hp, Wp, Ho, Wo);
+    for (int i = 0; i < 40; ++i) k_shape[i] = v_shape[i] = 1;
+    for (int i = 0; i < 8; ++i) kind[i] = 0;
+    for (const auto& L : h->arch.levels)
+      for (const auto& b : L.blocks) {
+        if (b.cache_slot < 0) continue;
+        const int s = b.cache_slot, Hl = Hp / L.scale, Wl = Wp / L.scale, c = b.dim;
+        int64_t* ks = k_shape + 5 * s;
+        int64_t* vs = v_shape + 5 * s;
+        if (b.attn == TURTLE_ATTN_FHR) {
+          const int ch = c / b.heads;
+          const int rows = std::min(t_in[s] + ch, b.ntc * ch);
+          kind[s] = 1;
+          ks[0] = vs[0] = B; ks[1] = vs[1] = b.heads; ks[2] = vs[2] = rows; ks[3] = vs[3] = (int64_t)Hl * Wl;
+        } else if (b.attn == TURTLE_ATTN_CHM) {
+          const int N = (Hl / b.ws) * (Wl / b.ws);
+          const int frames = std::min(t_in[s] + 1, b.ntc);
+          kind[s] = 2;
+          ks[0] = vs[0] = B; ks[1] = vs[1] = frames; ks[2] = vs[2] = 1; ks[3] = vs[3] = N;
+          ks[4] = 2 * c; vs[4] = (int64_t)b.ws * b.ws * c;
+        }
+      }
+  });
+}
+
+int turtle_workspace_size(const TurtleHandle* h, int B, int H, int W, size_t* bytes) {
+  return guard([&] {
+    if (!h || !bytes || B <= 0 || H <= 0 || W <= 0) TFAIL(TURTLE_EINVAL, "bad argument");
+    auto* hh = const_cast<TurtleHandle*>(h);
+    *bytes = h->bf16() ? ws_size<bf16>(hh, B, H, W) : ws_size<float>(hh, B, H, W);
+  });
+}
+
+int turtle_forward(TurtleHandle* h, const float* inp, int B, int H, int W, float* out,
+                   const void* const k_in[8], const void* const v_in[8], const int t_in[8],
+                   void* const k_out[8], void* const v_out[8], void* workspace, size_t workspace_bytes,
+                   void* stream) {
+  return guard([&] {
+    if (!h) TFAIL(TURTLE_EINVAL, "null handle");
+    if (!h->loaded) TFAIL(TURTLE_ESTATE, "turtle_load_weights has not been called");
+    if (!inp || !out || B <= 0 || H <= 0 || W <= 0) TFAIL(TURTLE_EINVAL, "bad input");
+    int Hp, Wp, Ho, Wo;
+    padded(h, H, W, Hp, Wp, Ho, Wo);
+    CacheIO io{};
+    int kind[8];
+    int64_t ks[40], vs[40];
+    turtle_cache_layout(h, B, H, W, t_in, kind, ks, vs);
+    for (int i = 0; i < 8; ++i) {
+      io.k_in[i] = k_in ? k_in[i] : nullptr;
+      io.v_in[i] = v_in ? v_in[i] : nullptr;
+      io.t_in[i] = t_in ? t_in[i] : 0;
+      io.k_out[i] = k_out ? k_out[i] : nullptr;
+      io.v_out[i] = v_out ? v_out[i] : nullptr;
+      if (kind[i] && (!io.k_out[i] || !io.v_out[i])) TFAIL(TURTLE_EINVAL, "missing cache output buffer for slot " + std::to_string(i));
+      if (kind[i] && io.t_in[i] && (!io.k_in[i] || !io.v_in[i])) TFAIL(TURTLE_EINVAL, "missing cache input for slot " + std::to_string(i));
+      if (!kind[i]) io.t_in[i] = 0;
+    }
+    // validate incoming cache extents
+    for (const auto& L : h->arch.levels)
+      for (const auto& b : L.blocks) {
+        if (b.cache_slot < 0) continue;
+        const int s = b.cache_slot;
+        if (b.attn == TURTLE_ATTN_FHR) {
+          const int ch = b.dim / b.heads;
+          if (io.t_in[s] % ch || io.t_in[s] > b.ntc * ch) TFAIL(TURTLE_EINVAL, "bad FHR cache rows");
+          if (io.t_in[s] / ch + 1 > TURTLE_MAX_SEG) TFAIL(TURTLE_EINVAL, "FHR cache too long");
+        } else if (b.attn == TURTLE_ATTN_CHM) {
+          if (io.t_in[s] > b.ntc) TFAIL(TURTLE_EINVAL, "bad SAB cache frames");
+          if (io.t_in[s] + 2 > TURTLE_MAX_SEG) TFAIL(TURTLE_EINVAL, "SAB cache too long");
+        }
+      }
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    auto go = [&](auto tag) {
+      using T = decltype(tag);
+      Runner<T> r{h, st, Arena{reinterpret_cast<char*>(workspace), workspace_bytes, 0, 0, false}, B, Hp, Wp, &io};
+      r.run(inp, H / 1, W / 1, out, Ho, Wo);
+    };
+    if (h->bf16()) go(bf16{}); else go(float{});
+    HIPCHK(hipGetLastError());
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,192 @@
+"""Turtle_t1 / TurtleSuper_t1 as drop-in ``nn.Module``s backed by libturtle_hip.so.
+
+Interface of the reference plug-in (basicsr/models/archs/turtle_t1_arch.py):
+
+* ``make_model(opt)`` reads the same option keys (10-53) and returns the module;
+* ``state_dict()`` has the same 633 keys / shapes (module paths of 932-1043), so reference
+  checkpoints load with ``strict=True``;
+* ``forward(inp_img_[B,2,C,H,W], k_cached=None, v_cached=None) -> (out[B,C,H,W], k_list[8],
+  v_list[8])`` (1045-1132): frame 0 passes None, later frames pass the previous return value.
+  The returned caches are ordinary torch tensors with the reference's shapes; entries are None
+  where the reference returns None.
+
+Every forward runs on the HIP library; there is no PyTorch / CPU fallback: a module on a
+non-ROCm device or a missing library raises ``RuntimeError``.
+
+Compute dtype: ``fp32`` (default, reference parity) or ``bf16`` (MFMA bf16, fp32 accumulation),
+chosen by ``opt['hip_dtype']`` or ``set_compute_dtype``. Cache tensors are returned in the
+compute dtype. The latent FrameHistoryRouter caches are strided views ([B, heads, rows, P] with
+strides (P*heads*rows, rows, 1, heads*rows)); incoming caches of any layout are accepted.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .arch import resolve
+from .params import TurtleParams
+
+_DT = {"fp32": (_lib.DTYPE_F32, torch.float32), "bf16": (_lib.DTYPE_BF16, torch.bfloat16)}
+
+
+class _Handle:
+    def __init__(self, cfg):
+        L = _lib.lib()
+        h = C.c_void_p()
+        _lib.check(L.turtle_create(C.byref(cfg), C.byref(h)))
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h:
+                _lib.lib().turtle_destroy(self.h)
+        except Exception:
+            pass
+
+
+class TurtleHIP(TurtleParams):
+    """Turtle_t1 (``sr=False``) / TurtleSuper_t1 (``sr=True``) on MI355X."""
+
+    def __init__(self, opt: dict, sr: bool = False, dtype: str = "fp32"):
+        arch = resolve(opt)
+        super().__init__(arch)
+        self.sr = sr
+        self.padder_size = 32
+        self._dtype_name = dtype
+        self._handle = None
+        self._sig = None
+        self._ws = None
+        self.set_compute_dtype(dtype)
+
+    # ---------------------------------------------------------------------------------------
+    def set_compute_dtype(self, dtype: str):
+        if dtype not in _DT:
+            raise ValueError(f"hip dtype must be one of {list(_DT)}")
+        self._dtype_name = dtype
+        self._handle = None
+        self._sig = None
+        return self
+
+    @property
+    def compute_dtype(self) -> torch.dtype:
+        return _DT[self._dtype_name][1]
+
+    def _signature(self):
+        ps = list(self.parameters())
+        dev = ps[0].device
+        return (dev, self._dtype_name, sum(p._version for p in ps), tuple(p.data_ptr() for p in ps[:4]))
+
+    def refresh_weights(self):
+        """Pack the current parameters into the device layout (done automatically on change)."""
+        L = _lib.lib()
+        dev = next(self.parameters()).device
+        if dev.type != "cuda":
+            raise RuntimeError("TurtleHIP runs on a ROCm device only: call .to('cuda') first")
+        if self._handle is None:
+            self._handle = _Handle(_lib.config_from_arch(self.arch, self.sr, _DT[self._dtype_name][0]))
+        h = self._handle.h
+        with torch.cuda.device(dev):
+            for name, t in self.state_dict().items():
+                a = t.detach().float().cpu().contiguous()
+                _lib.check(L.turtle_set_weight(h, name.encode(), C.c_void_p(a.data_ptr()), a.numel()))
+            _lib.check(L.turtle_load_weights(h))
+        self._sig = self._signature()
+
+    def _load_from_state_dict(self, *args, **kw):
+        super()._load_from_state_dict(*args, **kw)
+        self._sig = None
+
+    # ---------------------------------------------------------------------------------------
+    def cache_layout(self, B: int, H: int, W: int, t_in: List[int]):
+        L = _lib.lib()
+        kind = (C.c_int * 8)()
+        ks = (C.c_int64 * 40)()
+        vs = (C.c_int64 * 40)()
+        _lib.check(L.turtle_cache_layout(self._handle.h, B, H, W, (C.c_int * 8)(*t_in), kind, ks, vs))
+        return list(kind), [tuple(ks[5 * i:5 * i + 5]) for i in range(8)], [tuple(vs[5 * i:5 * i + 5]) for i in range(8)]
+
+    @staticmethod
+    def _fhr_strides(shape4):
+        B, heads, rows, P = shape4
+        return (P * heads * rows, rows, 1, heads * rows)
+
+    def _workspace(self, B, H, W, dev):
+        key = (B, H, W, dev, self._dtype_name)
+        if self._ws is None or self._ws[0] != key:
+            n = C.c_size_t()
+            _lib.check(_lib.lib().turtle_workspace_size(self._handle.h, B, H, W, C.byref(n)))
+            self._ws = (key, torch.empty(int(n.value), dtype=torch.uint8, device=dev))
+        return self._ws[1]
+
+    def forward(self, inp_img_: torch.Tensor, k_cached: Optional[list] = None, v_cached: Optional[list] = None):
+        if inp_img_.dim() != 5 or inp_img_.shape[1] != 2:
+            raise ValueError("expected inp_img_ of shape [B, 2, C, H, W]")
+        if inp_img_.device.type != "cuda":
+            raise RuntimeError("TurtleHIP.forward needs ROCm device tensors (no CPU path)")
+        if self._sig is None or self._sig != self._signature():
+            self.refresh_weights()
+        B, _, Cc, H, W = inp_img_.shape
+        dev = inp_img_.device
+        inp = inp_img_.detach().to(torch.float32).contiguous()
+        if k_cached is None:
+            k_cached, v_cached = [None] * 8, [None] * 8
+        kind0, _, _ = self.cache_layout(B, H, W, [0] * 8)
+        cdt = self.compute_dtype
+        t_in, k_in, v_in = [0] * 8, [None] * 8, [None] * 8
+        for i in range(8):
+            kc, vc = k_cached[i], v_cached[i]
+            if kind0[i] == 0 or kc is None or vc is None:
+                continue
+            if kind0[i] == 1:            # FHR rows [B, heads, rows, P]
+                t_in[i] = int(kc.shape[2])
+                st = self._fhr_strides(tuple(kc.shape))
+                k_in[i] = self._as_layout(kc, st, cdt, dev)
+                v_in[i] = self._as_layout(vc, st, cdt, dev)
+            else:                        # SAB frames [B, T, 1, N, d]
+                t_in[i] = int(kc.shape[1])
+                k_in[i] = kc.detach().to(device=dev, dtype=cdt).contiguous()
+                v_in[i] = vc.detach().to(device=dev, dtype=cdt).contiguous()
+        kind, kshape, vshape = self.cache_layout(B, H, W, t_in)
+        k_out, v_out = [None] * 8, [None] * 8
+        for i in range(8):
+            if kind[i] == 1:
+                s4 = kshape[i][:4]
+                k_out[i] = torch.empty_strided(s4, self._fhr_strides(s4), dtype=cdt, device=dev)
+                v_out[i] = torch.empty_strided(s4, self._fhr_strides(s4), dtype=cdt, device=dev)
+            elif kind[i] == 2:
+                k_out[i] = torch.empty(kshape[i], dtype=cdt, device=dev)
+                v_out[i] = torch.empty(vshape[i], dtype=cdt, device=dev)
+        s = 4 if self.sr else 1
+        out = torch.empty(B, Cc, H * s, W * s, dtype=torch.float32, device=dev)
+        ws = self._workspace(B, H, W, dev)
+
+        def ptrs(lst):
+            return (C.c_void_p * 8)(*[C.c_void_p(t.data_ptr()) if t is not None else None for t in lst])
+
+        with torch.cuda.device(dev):
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            _lib.check(_lib.lib().turtle_forward(
+                self._handle.h, C.c_void_p(inp.data_ptr()), B, H, W, C.c_void_p(out.data_ptr()),
+                ptrs(k_in), ptrs(v_in), (C.c_int * 8)(*t_in), ptrs(k_out), ptrs(v_out),
+                C.c_void_p(ws.data_ptr()), ws.numel(), C.c_void_p(stream)))
+        # keep inputs alive until the stream has consumed them (caller-owned caches are freed lazily)
+        self._keepalive = (inp, k_in, v_in)
+        return out, k_out, v_out
+
+    @staticmethod
+    def _as_layout(t: torch.Tensor, strides, dtype, dev):
+        t = t.detach().to(device=dev, dtype=dtype)
+        if t.stride() == tuple(strides):
+            return t
+        o = torch.empty_strided(tuple(t.shape), strides, dtype=dtype, device=dev)
+        o.copy_(t)
+        return o
+
+
+def make_model(opt: dict, sr: bool = False) -> TurtleHIP:
+    """make_model(opt) of turtle_t1_arch.py:10-53 (``sr=True``: turtlesuper_t1_arch.py)."""
+    return TurtleHIP(opt, sr=sr, dtype=opt.get("hip_dtype", "fp32"))
