@@ -34,6 +34,9 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # torch's bundled HIP runtime must be the one our library binds to (same soname
+    # libamdhip64.so.7): load torch first, or two HIP runtimes would coexist in the process.
+    import torch  # noqa: F401
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"libturtle_hip.so not found at {LIB_PATH}: run `python -m turtlevsr_amd.build`")
     L = C.CDLL(LIB_PATH)

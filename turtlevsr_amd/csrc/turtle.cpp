@@ -487,7 +487,6 @@ struct Runner {
     g.bias = bias ? bias : h->fptr(w.bias); g.scale = h->fptr(w.scale); g.gelu = gelu;
     g.res = res; g.ldr = ldr; g.offr = offr;
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store;
-    if (wstride && HW % 128) TFAIL(TURTLE_EINVAL, "per-image weights need HW % 128 == 0");
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
     launch_gemm<T>(g, st);
   }
