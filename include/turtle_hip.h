@@ -98,6 +98,25 @@ int turtle_forward(TurtleHandle* h, const float* inp, int B, int H, int W, float
                    void* const k_out[8], void* const v_out[8],
                    void* workspace, size_t workspace_bytes, void* stream);
 
+/* Per-kernel-class timing with HIP events on the forward's stream (measurement only).
+ * turtle_profile_begin(h, cls): from now on every launch of class `cls` (TURTLE_K_*, or
+ * TURTLE_K_ALL) issued by turtle_forward is bracketed by two events, and its algorithmic HBM
+ * bytes and FLOPs (each distinct input read once, each output written once) are accumulated.
+ * turtle_profile_end(h, out): waits for the events, stops profiling and writes, for each class
+ * c < TURTLE_K_COUNT: out[4c] = summed kernel ms, out[4c+1] = launches, out[4c+2] = bytes,
+ * out[4c+3] = FLOPs. */
+#define TURTLE_K_GEMM 0       /* pointwise 1x1 and implicit 3x3 convolutions (MFMA)        */
+#define TURTLE_K_DW 1         /* depthwise 3x3 (+GELU / gate)                              */
+#define TURTLE_K_ATTN 2       /* channel-attention Gram + finalize + W_eff                 */
+#define TURTLE_K_SAB_SCORE 3  /* SAB q.k^T + top-5                                         */
+#define TURTLE_K_SAB_AV 4     /* SAB clipped softmax + sparse A.v gather                   */
+#define TURTLE_K_WINDOW 5     /* SAB window conv + L2 norm                                 */
+#define TURTLE_K_OTHER 6      /* stem, ending, cache roll / copies                          */
+#define TURTLE_K_COUNT 7
+#define TURTLE_K_ALL 99
+int turtle_profile_begin(TurtleHandle* h, int kernel_class);
+int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
+
 const char* turtle_last_error(void);
 
 #ifdef __cplusplus

@@ -245,8 +245,14 @@ struct Packer {
   }
 };
 
+struct ProfRec { int cls; hipEvent_t a, b; double bytes, flops; };
+
 struct TurtleHandle {
   Arch arch;
+  int prof_cls = -1;
+  std::vector<ProfRec> prof;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
   std::map<std::string, std::vector<float>> staged;
   ModelW mw;
   char* dev = nullptr;
@@ -467,6 +473,27 @@ struct Runner {
   static constexpr size_t ES = sizeof(T);
 
   T* buf(int64_t elems) { return reinterpret_cast<T*>(ar.alloc((size_t)elems * ES)); }
+
+  hipEvent_t event() {
+    if (h->ev_used == h->ev_pool.size()) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreate(&e));
+      h->ev_pool.push_back(e);
+    }
+    return h->ev_pool[h->ev_used++];
+  }
+  // launch `f` as kernel class `cls`, bracketed by events when that class is being profiled
+  template <typename F>
+  void launch(int cls, double bytes, double flops, F&& f) {
+    if (dry()) return;
+    const bool p = h->prof_cls == TURTLE_K_ALL || h->prof_cls == cls;
+    if (!p) { f(); return; }
+    ProfRec r{cls, event(), event(), bytes, flops};
+    HIPCHK(hipEventRecord(r.a, st));
+    f();
+    HIPCHK(hipEventRecord(r.b, st));
+    h->prof.push_back(r);
+  }
   float* fbuf(int64_t elems) { return reinterpret_cast<float*>(ar.alloc((size_t)elems * 4)); }
   bool dry() const { return ar.dry; }
 
@@ -488,7 +515,12 @@ struct Runner {
     g.res = res; g.ldr = ldr; g.offr = offr;
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store;
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
-    launch_gemm<T>(g, st);
+    // algorithmic traffic: A once (a 3x3 reads each input pixel once), W per weight set, out
+    // (+ residual) once
+    const double Ka = conv3 ? cin : a.Ktot;
+    const double nset = wstride ? (double)(M / HW) / wdiv : 1.0;
+    const double bytes = ES * ((double)M * Ka + nset * g.N * a.Ktot + (double)M * g.N * (res ? 2 : 1));
+    launch(TURTLE_K_GEMM, bytes, 2.0 * M * g.N * a.Ktot, [&] { launch_gemm<T>(g, st); });
   }
   void dw(const DwW& w, const void* in, int64_t ldi, int offi, void* out, int64_t ldo, int offo,
           int nimg, int H, int Wd, int mode, int tok_ws = 0, int64_t tok_stride = 0) {
@@ -498,7 +530,8 @@ struct Runner {
     a.w = h->fptr(w.w); a.bias = h->fptr(w.bias);
     a.nimg = nimg; a.H = H; a.W = Wd; a.C = mode == DW_GATE ? w.C / 2 : w.C; a.mode = mode;
     a.tok_ws = tok_ws; a.tok_img_stride = tok_stride;
-    launch_dw<T>(a, st);
+    const double px = (double)nimg * H * Wd, cin = mode == DW_GATE ? 2.0 * a.C : a.C;
+    launch(TURTLE_K_DW, ES * px * (cin + a.C), 18.0 * px * cin, [&] { launch_dw<T>(a, st); });
   }
 
   struct Seg { const void* base; int64_t ld; int off; int hstride; int mul, add; int norm; int64_t col; int colh; };
@@ -525,16 +558,18 @@ struct Runner {
       if (segs[s].norm) mask |= 1u << s;
     }
     g.B = B; g.heads = b.heads; g.ch = ch; g.HW = HW; g.nchunk = nchunk; g.chunk = chunk; g.part = part;
-    launch_gram<T>(g, st);
+    launch(TURTLE_K_ATTN, ES * (double)B * HW * c * (1 + nseg), 2.0 * B * b.heads * ch * ncol * (double)HW,
+           [&] { launch_gram<T>(g, st); });
     AttnFinArgs f{};
     f.part = part; f.nchunk = nchunk; f.B = B; f.heads = b.heads; f.ch = ch; f.nseg = nseg; f.norm_mask = mask;
     f.tau = h->fptr(bw.tau); f.red = red; f.attn = attn; f.kinv = kinv; f.cur_seg = cur_seg;
-    launch_attn_finalize(f, st);
+    launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride, 0, [&] { launch_attn_finalize(f, st); });
     WeffArgs we{};
     we.attn = attn; we.wp = h->fptr(bw.wp); we.B = B; we.heads = b.heads; we.ch = ch; we.nseg = nseg; we.C = c;
     for (int s = 0; s < nseg; ++s) { we.seg_col[s] = segs[s].col; we.seg_hstride[s] = segs[s].colh; }
     we.Keff = vsrc.Ktot; we.weff = weff;
-    launch_weff<T>(we, st);
+    launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot, 2.0 * B * c * (double)b.heads * ncol * ch,
+           [&] { launch_weff<T>(we, st); });
     GemmW pw; pw.N = c; pw.K = vsrc.Ktot;
     gemm(pw, vsrc, (int64_t)B * HW, HW, Wimg, x, c, 0, x, c, 0, 0, STORE_NHWC, weff, (int64_t)c * vsrc.Ktot, 1, c,
          h->fptr(bw.po_bias));
@@ -606,10 +641,10 @@ struct Runner {
     FhrCacheArgs fk{};
     fk.old = io->k_in[slot]; fk.R = R; fk.cur = t2; fk.ldc = 3 * c; fk.coff = c; fk.kinv = kinv;
     fk.out = io->k_out[slot]; fk.Rnew = Rnew; fk.B = B; fk.P = HW; fk.heads = b.heads; fk.ch = ch;
-    launch_fhr_cache<T>(fk, st);
+    launch(TURTLE_K_OTHER, ES * (double)B * HW * b.heads * (R + ch + Rnew), 0, [&] { launch_fhr_cache<T>(fk, st); });
     FhrCacheArgs fv = fk;
     fv.old = io->v_in[slot]; fv.coff = 2 * c; fv.kinv = nullptr; fv.out = io->v_out[slot];
-    launch_fhr_cache<T>(fv, st);
+    launch(TURTLE_K_OTHER, ES * (double)B * HW * b.heads * (R + ch + Rnew), 0, [&] { launch_fhr_cache<T>(fv, st); });
   }
 
   // Causal History Model: SAB + kv conv on the aligned frames + FHR (turtle_t1_arch.py:612-662)
@@ -648,17 +683,20 @@ struct Runner {
       WinArgs wa{};
       wa.in = q2f; wa.ldi = d2; wa.offi = 0; wa.w = h->fptr(bw.q2_win); wa.bias = h->fptr(bw.q2_winb);
       wa.out = qtok; wa.out_img_stride = (int64_t)N * d2; wa.nimg = B; wa.H = H; wa.W = Wd; wa.C = d2; wa.ws = ws;
-      launch_window<T>(wa, st);
+      const double wbytes = ES * ((double)P * d2 + (double)B * N * d2), wflops = 2.0 * P * d2;
+      launch(TURTLE_K_WINDOW, wbytes, wflops, [&] { launch_window<T>(wa, st); });
       wa.in = k2f; wa.w = h->fptr(bw.k2_win); wa.bias = h->fptr(bw.k2_winb);
       wa.out = kout + (int64_t)(Tnew - 1) * N * d2; wa.out_img_stride = (int64_t)Tnew * N * d2;
-      launch_window<T>(wa, st);
+      launch(TURTLE_K_WINDOW, wbytes, wflops, [&] { launch_window<T>(wa, st); });
       // keep the last Tnew-1 cached frames in the new cache (reference: cat then [-ntc:])
       if (Tnew > 1) {
         const int keep = Tnew - 1, first = Tin - keep;
-        HIPCHK(hipMemcpy2DAsync(kout, (size_t)Tnew * N * d2 * ES, kin + (int64_t)first * N * d2, (size_t)Tin * N * d2 * ES,
-                                (size_t)keep * N * d2 * ES, B, hipMemcpyDeviceToDevice, st));
-        HIPCHK(hipMemcpy2DAsync(vout, (size_t)Tnew * N * D * ES, vin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
-                                (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
+        launch(TURTLE_K_OTHER, 2.0 * ES * B * keep * (double)N * (d2 + D), 0, [&] {
+          HIPCHK(hipMemcpy2DAsync(kout, (size_t)Tnew * N * d2 * ES, kin + (int64_t)first * N * d2, (size_t)Tin * N * d2 * ES,
+                                  (size_t)keep * N * d2 * ES, B, hipMemcpyDeviceToDevice, st));
+          HIPCHK(hipMemcpy2DAsync(vout, (size_t)Tnew * N * D * ES, vin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
+                                  (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
+        });
       }
       if (NT > TURTLE_MAX_T) TFAIL(TURTLE_EINVAL, "too many cached frames");
       SabScoreArgs sa{};
@@ -677,8 +715,11 @@ struct Runner {
         }
         va.k[t] = sa.k[t]; va.k_bstride[t] = sa.k_bstride[t];
       }
-      launch_sab_score<T>(sa, st);
-      launch_sab_av<T>(va, st);
+      launch(TURTLE_K_SAB_SCORE, ES * (double)B * N * d2 * (1 + NT) + 8.0 * B * NT * N * 5,
+             2.0 * B * NT * (double)N * N * d2, [&] { launch_sab_score<T>(sa, st); });
+      // <= 46 surviving keys per row (5 top + 41 ball): SURVEY.md §8(a) sparse A.v
+      launch(TURTLE_K_SAB_AV, ES * ((double)B * NT * N * D + (double)B * NT * HW * c) + 8.0 * B * NT * N * 5,
+             2.0 * B * NT * (double)N * 46 * D, [&] { launch_sab_av<T>(va, st); });
     }
     // kv = (W_kv W_po) xs over the B*T aligned frames, then dw3x3 per frame
     gemm(bw.kv, src1(xs, c, 0, c), P * NT, HW, Wd, kv, 2 * c, 0);
@@ -722,7 +763,8 @@ struct Runner {
       s.B = B; s.Cimg = A.cfg.n_colors; s.Hin = Hin; s.Win = Win; s.Hp = Hp; s.Wp = Wp;
       s.use_both = A.cfg.use_both_input; s.sr = A.cfg.super_resolution;
       s.w = h->fptr(h->mw.stem_w); s.bias = h->fptr(h->mw.stem_b); s.Cout = d; s.out = e1;
-      launch_stem<T>(s, st);
+      launch(TURTLE_K_OTHER, 4.0 * B * A.in_ch * Hin * Win + ES * (double)P1 * d, 18.0 * P1 * d * A.in_ch,
+             [&] { launch_stem<T>(s, st); });
     }
     int H = Hp, Wd = Wp;
     level(0, e1, H, Wd);
@@ -759,7 +801,8 @@ struct Runner {
       e.inp = inp; e.in_bstride = (int64_t)2 * A.cfg.n_colors * Hin * Win; e.in_fstride = (int64_t)A.cfg.n_colors * Hin * Win;
       e.B = B; e.Cimg = A.cfg.n_colors; e.Hin = Hin; e.Win = Win; e.Hp = Hp; e.Wp = Wp; e.Hout = Hout; e.Wout = Wout;
       e.sr = A.cfg.super_resolution; e.out = out;
-      launch_ending<T>(e, st);
+      launch(TURTLE_K_OTHER, ES * (double)P1 * d + 8.0 * B * A.out_ch * Hout * Wout, 18.0 * P1 * d * A.out_ch,
+             [&] { launch_ending<T>(e, st); });
     }
   }
 };
@@ -805,6 +848,35 @@ extern "C" {
 
 const char* turtle_last_error(void) { return g_err.c_str(); }
 
+int turtle_profile_begin(TurtleHandle* h, int kernel_class) {
+  return guard([&] {
+    if (!h) TFAIL(TURTLE_EINVAL, "null handle");
+    h->prof.clear();
+    h->ev_used = 0;
+    h->prof_cls = kernel_class;
+  });
+}
+
+int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]) {
+  return guard([&] {
+    if (!h || !out) TFAIL(TURTLE_EINVAL, "null argument");
+    for (int i = 0; i < 4 * TURTLE_K_COUNT; ++i) out[i] = 0;
+    for (auto& r : h->prof) {
+      HIPCHK(hipEventSynchronize(r.b));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, r.a, r.b));
+      if (r.cls < 0 || r.cls >= TURTLE_K_COUNT) continue;
+      out[4 * r.cls] += ms;
+      out[4 * r.cls + 1] += 1;
+      out[4 * r.cls + 2] += r.bytes;
+      out[4 * r.cls + 3] += r.flops;
+    }
+    h->prof.clear();
+    h->ev_used = 0;
+    h->prof_cls = -1;
+  });
+}
+
 int turtle_create(const TurtleConfig* cfg, TurtleHandle** out) {
   return guard([&] {
     if (!cfg || !out) TFAIL(TURTLE_EINVAL, "null argument");
@@ -822,6 +894,7 @@ int turtle_create(const TurtleConfig* cfg, TurtleHandle** out) {
 
 void turtle_destroy(TurtleHandle* h) {
   if (!h) return;
+  for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->dev) (void)hipFree(h->dev);
   delete h;
 }

@@ -177,6 +177,21 @@ class TurtleHIP(TurtleParams):
         self._keepalive = (inp, k_in, v_in)
         return out, k_out, v_out
 
+    # ---------------------------------------------------------------------------------------
+    def profile_begin(self, kernel_class: str = "all"):
+        """Bracket every launch of `kernel_class` (see _lib.K_CLASSES, or 'all') with HIP events."""
+        cls = _lib.K_ALL if kernel_class == "all" else _lib.K_CLASSES.index(kernel_class)
+        if self._handle is None or self._sig is None:
+            self.refresh_weights()
+        _lib.check(_lib.lib().turtle_profile_begin(self._handle.h, cls))
+
+    def profile_end(self) -> dict:
+        """Per class: summed kernel ms, launches, algorithmic bytes and FLOPs."""
+        out = (C.c_double * (4 * len(_lib.K_CLASSES)))()
+        _lib.check(_lib.lib().turtle_profile_end(self._handle.h, out))
+        return {k: dict(ms=out[4 * i], launches=int(out[4 * i + 1]), bytes=out[4 * i + 2], flops=out[4 * i + 3])
+                for i, k in enumerate(_lib.K_CLASSES)}
+
     @staticmethod
     def _as_layout(t: torch.Tensor, strides, dtype, dev):
         t = t.detach().to(device=dev, dtype=dtype)
