@@ -34,6 +34,12 @@ template <> struct Vec<float> {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
   TURTLE_DEV void zero() { v[0] = v[1] = v[2] = v[3] = 0.f; }
+  // unconditional load from a valid address, zeroed when !ok (no branch around the load, so the
+  // compiler keeps several loads in flight instead of waiting on each: guide §5 trap (c))
+  TURTLE_DEV void load_pred(const float* p, bool ok) {
+    float4 q = *reinterpret_cast<const float4*>(p);
+    v[0] = ok ? q.x : 0.f; v[1] = ok ? q.y : 0.f; v[2] = ok ? q.z : 0.f; v[3] = ok ? q.w : 0.f;
+  }
 };
 template <> struct Vec<bf16> {
   static constexpr int N = 8;
@@ -41,6 +47,15 @@ template <> struct Vec<bf16> {
   TURTLE_DEV void load(const bf16* p) {
     uint4 q = *reinterpret_cast<const uint4*>(p);
     uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  TURTLE_DEV void load_pred(const bf16* p, bool ok) {
+    uint4 q = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {ok ? q.x : 0u, ok ? q.y : 0u, ok ? q.z : 0u, ok ? q.w : 0u};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       v[2 * i] = __uint_as_float(w[i] << 16);
@@ -58,6 +73,20 @@ template <> struct Vec<bf16> {
     for (int i = 0; i < 8; ++i) v[i] = 0.f;
   }
 };
+
+// One unconditional 16-byte global load. The address is made opaque to the optimiser so a
+// select between a real and a dummy (zero) address stays a v_cndmask instead of being turned into
+// two predicated loads behind branches, each drained with s_waitcnt vmcnt(0).
+TURTLE_DEV uint4 ld16(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(1))) const uint4 gUint4;
+  uint64_t a = reinterpret_cast<uint64_t>(p);
+  asm volatile("" : "+v"(a));
+  return *reinterpret_cast<gUint4*>(a);   // global_load_dwordx4 (not flat)
+#else
+  return *reinterpret_cast<const uint4*>(p);
+#endif
+}
 
 TURTLE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 

@@ -5,132 +5,170 @@
 // A is the K-concatenation of up to TURTLE_MAX_SRC pixel-major sources (skip concats, cached
 // history frames, the multi-frame K of the Frame History Router), or the 9 shifted taps of a dense
 // 3x3 convolution (Downsample / Upsample, turtle_t1_arch.py:136-154) - no im2col buffer.
-// Optional prologue: per-pixel LayerNorm statistics over the single source's K
-// (turtle_t1_arch.py:83-99); the LN affine is folded into W at pack time, so the epilogue applies
+// LayerNorm (turtle_t1_arch.py:83-99) costs no extra pass: its affine is folded into W at pack
+// time and the per-pixel statistics are accumulated from the A tiles already staged in LDS, so
 //   v = rstd_m * (acc - mu_m * s[n]) + t[n]      (s = rowsum(W*g), t = W.b)
 // Epilogue: + bias, GELU, * per-channel scale (ReducedAttn beta / FeedForward gamma), + residual,
-// and a store remap (plain, PixelShuffle(2), PixelUnshuffle(2)).
+// store remap (plain, PixelShuffle(2), PixelUnshuffle(2)).
 //
-// Tiling (CDNA4): 256 threads = 4 waves in 2x2; block tile BM pixels x BN channels x BK;
-// MFMA 16x16x32 bf16 (or 16x16x4 f32 in parity mode), i = output channel (A operand = W rows),
-// j = pixel (B operand = X rows), so both operands are k-contiguous 16-byte LDS reads and each
-// lane's accumulator holds 4 consecutive channels of one pixel (one 8/16-byte store).
-// Double-buffered LDS with register prefetch of the next K tile.
+// Most Turtle GEMMs are HBM-bound (K = 64..640 against N = 64..2560 at 0.1-2 M pixels), so the
+// kernel is organised for bytes, not FLOPs:
+//   * grid: output-channel tiles vary fastest and the block id is remapped so that the tiles of
+//     one pixel panel run on the same XCD - the A panel is fetched from HBM once and re-read
+//     from that XCD's L2;
+//   * single LDS buffer + register prefetch of the next K tile (2 barriers per K step) keeps LDS
+//     at (BM+BN)*144 B so 3-4 blocks share a CU;
+//   * the accumulator tile is staged through LDS and written (and the residual read) as whole
+//     16-byte row chunks.
+// MFMA 16x16x32 bf16 (16x16x4 f32 in parity mode); i = output channel (A operand = W rows),
+// j = pixel (B operand = X rows): both operands are k-contiguous 16-byte LDS reads.
 #include "common.h"
 #include "kernels.h"
 #include "mma.h"
 
 namespace turtle {
 
+// Out-of-range operand lanes load from this zero line instead of being masked after the load,
+// so no instruction consumes a load result before the tile is written to LDS and all loads of
+// a K step stay in flight together (guide §5, trap (c)).
+__device__ __attribute__((aligned(64))) uint4 g_zero_line[4];
+
+template <typename T, int BM, int BN>
+struct GemmSmem {
+  static constexpr int PIPE = (BM + BN) * ROWB;
+  static constexpr int OROW = BN * (int)sizeof(T) + 16;       // staged output row bytes
+  static constexpr int OUT = BM * OROW;
+  static constexpr int BYTES = (PIPE > OUT ? PIPE : OUT) + 2 * BM * 4 + 4 * BN * 4;
+};
+
 template <typename T, int BM, int BN>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   using M = Mma<T>;
+  using S = GemmSmem<T, BM, BN>;
   constexpr int BK = M::BK, VEC = M::VEC, KV = BK / VEC;        // vectors per tile row
   constexpr int TM = BM / 32, TN = BN / 32;                      // 16x16 tiles per wave
   constexpr int XV = BM * KV / 256, WV = BN * KV / 256;          // vectors per thread
-  __shared__ __attribute__((aligned(16))) char smem[2 * (BM + BN) * ROWB + 2 * BM * 4];
-  auto sX = [&](int buf) { return smem + buf * (BM + BN) * ROWB; };
-  auto sW = [&](int buf) { return smem + buf * (BM + BN) * ROWB + BM * ROWB; };
-  float* s_mu = reinterpret_cast<float*>(smem + 2 * (BM + BN) * ROWB);
+  __shared__ __attribute__((aligned(16))) char smem[S::BYTES];
+  char* sX = smem;
+  char* sW = smem + BM * ROWB;
+  float* s_mu = reinterpret_cast<float*>(smem + (S::BYTES - 2 * BM * 4 - 4 * BN * 4));
   float* s_rs = s_mu + BM;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  // per-image weights (W_eff): tile each image separately so a block never spans two images
+
+  // ---- block -> (pixel tile, channel tile); XCD-aware bijective remap of the linear id ----
+  const int ntn = (g.N + BN - 1) / BN;
+  const int nblk = gridDim.x;
+  int lin = blockIdx.x;
+  {
+    const int q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
+    lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;   // blocks of one XCD: contiguous ids
+  }
+  const int nt = lin % ntn;
+  const int mt = lin / ntn;
   int64_t m0, mlim;
-  if (g.wstride) {
+  if (g.wstride) {    // per-image weights (W_eff): a block never spans two images
     const int tpi = (g.HW + BM - 1) / BM;
-    const int64_t im = blockIdx.x / tpi;
-    m0 = im * g.HW + (int64_t)(blockIdx.x % tpi) * BM;
+    const int64_t im = mt / tpi;
+    m0 = im * g.HW + (int64_t)(mt % tpi) * BM;
     mlim = min(g.M, (im + 1) * (int64_t)g.HW);
   } else {
-    m0 = (int64_t)blockIdx.x * BM;
+    m0 = (int64_t)mt * BM;
     mlim = g.M;
   }
-  const int n0 = blockIdx.y * BN;
+  const int n0 = nt * BN;
   const int K = g.a.Ktot;
   const int nk = (K + BK - 1) / BK;
   const int img0 = (int)(m0 / g.HW);
   const T* Wp = reinterpret_cast<const T*>(g.w) + (g.wstride ? (int64_t)(img0 / g.wdiv) * g.wstride : 0);
 
-  // ---- LayerNorm statistics prologue: 2 threads per pixel row, shifted one-pass sums ----
-  if (g.ln) {
-    const SrcDesc& s = g.a.s[0];
-    for (int r = tid >> 1; r < BM; r += 128) {
-      int64_t m = m0 + r;
-      float a = 0.f, b = 0.f, sh = 0.f;
-      if (m < mlim) {
-        int64_t img = m / g.HW, p = m - img * g.HW;
-        const T* row = reinterpret_cast<const T*>(s.base) + ((img * s.img_mul + s.img_add) * g.HW + p) * s.ld + s.off;
-        sh = to_f(row[0]);
-        for (int k = (tid & 1) * VEC; k < s.K; k += 2 * VEC) {
-          Vec<T> v; v.load(row + k);
-#pragma unroll
-          for (int i = 0; i < VEC; ++i) { float d = v.v[i] - sh; a += d; b += d * d; }
-        }
-      }
-      a += __shfl_xor(a, 1, 64);
-      b += __shfl_xor(b, 1, 64);
-      if ((tid & 1) == 0) {
-        float mean_d = a / s.K;
-        float var = fmaxf(b / s.K - mean_d * mean_d, 0.f);
-        s_mu[r] = sh + mean_d;
-        s_rs[r] = rsqrtf(var + 1e-5f);
-      }
-    }
+  // ---- per-channel epilogue vectors staged once in LDS (no per-element global loads) ----
+  float* e_s = s_mu + 2 * BM;                       // [BN] each: ln_s, ln_t, bias, scale
+  float* e_t = e_s + BN;
+  float* e_b = e_t + BN;
+  float* e_c = e_b + BN;
+  if (tid < BN) {
+    const int n = n0 + tid;
+    const bool ok = n < g.N;
+    e_s[tid] = (ok && g.ln_s) ? g.ln_s[n] : 0.f;
+    e_t[tid] = (ok && g.ln_t) ? g.ln_t[n] : 0.f;
+    e_b[tid] = (ok && g.bias) ? g.bias[n] : 0.f;
+    e_c[tid] = (ok && g.scale) ? g.scale[n] : 1.f;
   }
 
-  // ---- per-thread load geometry (constant over K) ----
+  // ---- per-thread load geometry: rows are fixed over K, so resolve pixel coordinates once ----
   const int kv = tid % KV;
-  Vec<T> xr[XV], wr[WV];
+  int r_img[XV], r_p[XV], r_y[XV], r_x[XV];
+  bool r_ok[XV];
+#pragma unroll
+  for (int i = 0; i < XV; ++i) {
+    const int r = tid / KV + i * (256 / KV);
+    const int64_t m = m0 + r;
+    r_ok[i] = m < mlim;
+    const int mm = r_ok[i] ? (int)m : (int)m0;
+    r_img[i] = mm / g.HW;
+    r_p[i] = mm - r_img[i] * g.HW;
+    r_y[i] = g.conv3 ? r_p[i] / g.Wimg : 0;
+    r_x[i] = g.conv3 ? r_p[i] - r_y[i] * g.Wimg : 0;
+  }
+  const int Himg = g.conv3 ? g.HW / g.Wimg : 0;
+  uint4 xr[XV], wr[WV];
 
   auto load_tile = [&](int kt) {
     const int k = kt * BK + kv * VEC;
-    // locate the source of this k (uniform per thread within a tile)
-    int si = 0, kb = 0;
-    bool kin = k < K;
+    const bool kin = k < K;
+    // source of this k: static-index scan over the (uniform, SGPR-resident) descriptors with
+    // per-lane selects - no dynamic indexing of the kernel-argument block
+    const T* base = reinterpret_cast<const T*>(g.a.s[0].base);
+    int64_t sld = g.a.s[0].ld;
+    int soff = g.a.s[0].off, smul = g.a.s[0].img_mul, sadd = g.a.s[0].img_add, kb = 0;
     if (!g.conv3) {
-      while (si < g.a.n - 1 && k >= kb + g.a.s[si].K) { kb += g.a.s[si].K; ++si; }
-    }
-    const SrcDesc& s = g.a.s[si];
+      int kbj = g.a.s[0].K;
 #pragma unroll
-    for (int i = 0; i < XV; ++i) {
-      int r = tid / KV + i * (256 / KV);
-      int64_t m = m0 + r;
-      xr[i].zero();
-      if (kin && m < mlim) {
-        int64_t img = m / g.HW, p = m - img * g.HW;
-        const T* src;
-        if (g.conv3) {
-          int tap = k / g.cin, ci = k - tap * g.cin;
-          int y = (int)(p / g.Wimg) + tap / 3 - 1, x = (int)(p % g.Wimg) + tap % 3 - 1;
-          int Himg = g.HW / g.Wimg;
-          if (y < 0 || y >= Himg || x < 0 || x >= g.Wimg) continue;
-          src = reinterpret_cast<const T*>(s.base) + ((img * g.HW + (int64_t)y * g.Wimg + x) * s.ld + s.off + ci);
-        } else {
-          src = reinterpret_cast<const T*>(s.base) + (((img * s.img_mul + s.img_add) * g.HW + p) * s.ld + s.off + (k - kb));
+      for (int j = 1; j < TURTLE_MAX_SRC; ++j) {
+        if (j < g.a.n) {
+          const bool hit = k >= kbj;
+          base = hit ? reinterpret_cast<const T*>(g.a.s[j].base) : base;
+          sld = hit ? g.a.s[j].ld : sld;
+          soff = hit ? g.a.s[j].off : soff;
+          smul = hit ? g.a.s[j].img_mul : smul;
+          sadd = hit ? g.a.s[j].img_add : sadd;
+          kb = hit ? kbj : kb;
+          kbj += g.a.s[j].K;
         }
-        xr[i].load(src);
       }
     }
-#pragma unroll
-    for (int i = 0; i < WV; ++i) {
-      int r = tid / KV + i * (256 / KV);
-      int n = n0 + r;
-      wr[i].zero();
-      if (kin && n < g.N) wr[i].load(Wp + (int64_t)n * g.ldw + k);
-    }
-  };
-  auto store_tile = [&](int buf) {
+    // branch-free addressing (one basic block, so the loads issue back to back): a plain source
+    // is the conv3 formula with dy = dx = 0 and no border test
+    const int tap = g.conv3 ? k / g.cin : 4;
+    const int ci = g.conv3 ? k - (tap * g.cin) : k - kb;
+    const int dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
 #pragma unroll
     for (int i = 0; i < XV; ++i) {
-      int r = tid / KV + i * (256 / KV);
-      xr[i].store(reinterpret_cast<T*>(sX(buf) + r * ROWB) + kv * VEC);
+      const int y = r_y[i] + dy, x = r_x[i] + dx;
+      const bool inb = !g.conv3 || (y >= 0 && y < Himg && x >= 0 && x < g.Wimg);
+      const bool ok = kin && r_ok[i] && inb;
+      const int64_t off = ((int64_t)(r_img[i] * smul + sadd) * g.HW + r_p[i] + dy * g.Wimg + dx) * sld + soff + ci;
+      xr[i] = ld16(ok ? reinterpret_cast<const void*>(base + off) : g_zero_line);
     }
 #pragma unroll
     for (int i = 0; i < WV; ++i) {
-      int r = tid / KV + i * (256 / KV);
-      wr[i].store(reinterpret_cast<T*>(sW(buf) + r * ROWB) + kv * VEC);
+      const int n = n0 + tid / KV + i * (256 / KV);
+      const bool ok = kin && n < g.N;
+      wr[i] = ld16(ok ? reinterpret_cast<const void*>(Wp + (int64_t)n * g.ldw + k) : g_zero_line);
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int i = 0; i < XV; ++i) {
+      const int r = tid / KV + i * (256 / KV);
+      *reinterpret_cast<uint4*>(sX + r * ROWB + kv * 16) = xr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < WV; ++i) {
+      const int r = tid / KV + i * (256 / KV);
+      *reinterpret_cast<uint4*>(sW + r * ROWB + kv * 16) = wr[i];
     }
   };
 
@@ -140,93 +178,140 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // LN statistics: 2 threads per pixel row, shifted sums over the staged A tiles
+  const int lr = tid >> 1, lh = tid & 1;
+  float ls = 0.f, lq = 0.f, lsh = 0.f;
+
   load_tile(0);
-  store_tile(0);
-  __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
+    store_tile();
+    __syncthreads();
+    if (kt + 1 < nk) load_tile(kt + 1);            // in flight during the MFMAs below
+    if (g.ln && lr < BM) {
+      const T* row = reinterpret_cast<const T*>(sX + lr * ROWB);
+      if (kt == 0) lsh = to_f(row[0]);
+      const int kend = min(BK, K - kt * BK);
+      for (int c = lh * VEC; c < kend; c += 2 * VEC) {
+        Vec<T> v; v.load(row + c);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) { const float d = v.v[i] - lsh; ls += d; lq = fmaf(d, d, lq); }
+      }
+    }
 #pragma unroll
     for (int ks = 0; ks < BK / M::KSUB; ++ks)
-      mma_step<T>(sW(buf), sX(buf), lane, ks, acc, TM, TN, wn * (BN / 2), wm * (BM / 2));
-    if (kt + 1 < nk) store_tile(buf ^ 1);
+      mma_step<T>(sW, sX, lane, ks, acc, TM, TN, wn * (BN / 2), wm * (BM / 2));
+    __syncthreads();
+  }
+  if (g.ln) {
+    ls += __shfl_xor(ls, 1, 64);
+    lq += __shfl_xor(lq, 1, 64);
+    if (lh == 0 && lr < BM) {
+      const float md = ls / K;
+      s_mu[lr] = lsh + md;
+      s_rs[lr] = rsqrtf(fmaxf(lq / K - md * md, 0.f) + 1e-5f);
+    }
     __syncthreads();
   }
 
-  // ---- epilogue ----
+  // ---- epilogue phase 1: per-element math in registers, stage the tile in LDS as T ----
   const int q = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int tm = 0; tm < TM; ++tm) {
     const int r = wm * (BM / 2) + tm * 16 + c16;
-    const int64_t m = m0 + r;
-    if (m >= mlim) continue;
     const float mu = g.ln ? s_mu[r] : 0.f, rs = g.ln ? s_rs[r] : 1.f;
-    const int64_t img = m / g.HW, p = m - img * g.HW;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      const int nb = n0 + wn * (BN / 2) + tn * 16 + q * 4;
-      if (nb >= g.N) continue;
+      const int cl = wn * (BN / 2) + tn * 16 + q * 4;
+      const float4 es = *reinterpret_cast<const float4*>(e_s + cl), et = *reinterpret_cast<const float4*>(e_t + cl);
+      const float4 eb = *reinterpret_cast<const float4*>(e_b + cl), ec = *reinterpret_cast<const float4*>(e_c + cl);
+      const float fs[4] = {es.x, es.y, es.z, es.w}, ft[4] = {et.x, et.y, et.z, et.w};
+      const float fb[4] = {eb.x, eb.y, eb.z, eb.w}, fc[4] = {ec.x, ec.y, ec.z, ec.w};
       float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int n = nb + e;
         float x = acc[tm][tn][e];
-        if (n < g.N) {
-          if (g.ln) x = rs * (x - (g.ln_s ? mu * g.ln_s[n] : 0.f)) + (g.ln_t ? g.ln_t[n] : 0.f);
-          if (g.bias) x += g.bias[n];
-          if (g.gelu) x = gelu_erf(x);
-          if (g.scale) x *= g.scale[n];
-          if (g.res) x += to_f(reinterpret_cast<const T*>(g.res)[m * g.ldr + g.offr + n]);
-        }
-        v[e] = x;
+        if (g.ln) x = rs * (x - mu * fs[e]) + ft[e];
+        x += fb[e];
+        if (g.gelu) x = gelu_erf(x);
+        v[e] = x * fc[e];
       }
-      T* o = reinterpret_cast<T*>(g.out);
-      if (g.store_mode == STORE_UNSHUFFLE) {
-        const int Wi = g.Wimg, Hi = g.HW / Wi;
-        const int y = (int)(p / Wi), x = (int)(p % Wi);
-        const int64_t dp = (img * (Hi / 2) + y / 2) * (Wi / 2) + x / 2;
-        const int sub = (y & 1) * 2 + (x & 1);
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (nb + e < g.N) o[dp * g.ldo + g.offo + (nb + e) * 4 + sub] = from_f<T>(v[e]);
-        continue;
-      }
-      int64_t dst;
-      int cn = nb;
-      if (g.store_mode == STORE_SHUFFLE) {
-        const int Cq = g.N / 4, s = nb / Cq;
-        cn = nb - s * Cq;
-        const int Wi = g.Wimg, Hi = g.HW / Wi;
-        const int y = (int)(p / Wi), x = (int)(p % Wi);
-        dst = ((img * 2 * Hi + 2 * y + (s >> 1)) * (2 * Wi) + 2 * x + (s & 1)) * g.ldo + g.offo + cn;
+      if constexpr (sizeof(T) == 4) {
+        *reinterpret_cast<float4*>(smem + r * S::OROW + cl * 4) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
-        dst = m * g.ldo + g.offo + cn;
-      }
-      if (nb + 3 < g.N) {
-        if constexpr (sizeof(T) == 4) {
-          *reinterpret_cast<float4*>(o + dst) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
-          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          bf16x4 w = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-          *reinterpret_cast<bf16x4*>(o + dst) = w;
-        }
-      } else {
-        for (int e = 0; e < 4 && nb + e < g.N; ++e) o[dst + e] = from_f<T>(v[e]);
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        *reinterpret_cast<bf16x4*>(smem + r * S::OROW + cl * 2) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       }
     }
   }
+  __syncthreads();
+
+  // ---- epilogue phase 2: 16-byte row chunks, residual add, store remap ----
+  // every chunk's loads (staged tile + residual) are issued before any store, unconditionally
+  constexpr int CV = BN / VEC;                    // chunks per row
+  constexpr int NCH = BM * CV / 256;              // chunks per thread
+  T* o = reinterpret_cast<T*>(g.out);
+  const T* res = reinterpret_cast<const T*>(g.res);
+  Vec<T> v[NCH];
+  bool okc[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int idx = tid + j * 256, r = idx / CV, cc = idx % CV;
+    const int64_t m = m0 + r;
+    const int nb = n0 + cc * VEC;
+    okc[j] = m < mlim && nb < g.N;
+    v[j].load(reinterpret_cast<const T*>(smem + r * S::OROW) + cc * VEC);
+    if (res) {
+      const bool full = okc[j] && nb + VEC <= g.N;
+      Vec<T> rv; rv.load_pred(res + (full ? m * g.ldr + g.offr + nb : 0), full);
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) v[j].v[e] += rv.v[e];
+      if (okc[j] && !full)
+        for (int e = 0; e < VEC && nb + e < g.N; ++e) v[j].v[e] += to_f(res[m * g.ldr + g.offr + nb + e]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    if (!okc[j]) continue;
+    const int idx = tid + j * 256, r = idx / CV, cc = idx % CV;
+    const int64_t m = m0 + r;
+    const int nb = n0 + cc * VEC;
+    const bool full = nb + VEC <= g.N;
+    int64_t dst;
+    if (g.store_mode == STORE_NHWC) {
+      dst = m * g.ldo + g.offo + nb;
+    } else {
+      const int mi = (int)m, img = mi / g.HW, p = mi - img * g.HW;
+      const int Wi = g.Wimg, Hi = g.HW / Wi;
+      const int y = p / Wi, x = p - y * Wi;
+      if (g.store_mode == STORE_UNSHUFFLE) {
+        const int64_t dp = ((int64_t)img * (Hi / 2) + y / 2) * (Wi / 2) + x / 2;
+        const int sub = (y & 1) * 2 + (x & 1);
+        for (int e = 0; e < VEC && nb + e < g.N; ++e) o[dp * g.ldo + g.offo + (nb + e) * 4 + sub] = from_f<T>(v[j].v[e]);
+        continue;
+      }
+      // PixelShuffle: weights were permuted so output channel n' = s*Cq + c (a chunk stays in
+      // one sub-pixel s)
+      const int Cq = g.N / 4, sp = nb / Cq, cn = nb - sp * Cq;
+      dst = (((int64_t)img * 2 * Hi + 2 * y + (sp >> 1)) * (2 * Wi) + 2 * x + (sp & 1)) * g.ldo + g.offo + cn;
+    }
+    if (full) v[j].store(o + dst);
+    else for (int e = 0; e < VEC && nb + e < g.N; ++e) o[dst + e] = from_f<T>(v[j].v[e]);
+  }
+}
+
+template <typename T, int BM, int BN>
+static void launch_cfg(const GemmArgs& g, hipStream_t st) {
+  const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + BM - 1) / BM) : (g.M + BM - 1) / BM;
+  const int64_t nblk = mt * ((g.N + BN - 1) / BN);
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN>), dim3((unsigned)nblk), dim3(256), 0, st, g);
 }
 
 template <typename T>
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
-  const int bn = g.N <= 64 ? 64 : 128;
-  const int bm = 128;
-  const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + bm - 1) / bm) : (g.M + bm - 1) / bm;
-  dim3 grid((unsigned)mt, (unsigned)((g.N + bn - 1) / bn));
-  if (bn == 64)
-    hipLaunchKernelGGL((gemm_kernel<T, 128, 64>), grid, dim3(256), 0, st, g);
-  else
-    hipLaunchKernelGGL((gemm_kernel<T, 128, 128>), grid, dim3(256), 0, st, g);
+  // BN = 128 when it tiles N exactly (or N is large), else 64 (N = 64, 192, 320, tiny widths)
+  const bool wide = g.N >= 128 && (g.N % 128 == 0 || g.N > 1024);
+  if (wide) launch_cfg<T, 128, 128>(g, st);
+  else launch_cfg<T, 128, 64>(g, st);
 }
 
 template void launch_gemm<float>(const GemmArgs&, hipStream_t);
