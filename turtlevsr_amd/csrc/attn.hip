@@ -14,82 +14,149 @@
 
 namespace turtle {
 
-constexpr int GP = 32;           // pixels per Gram staging tile
+#ifndef TURTLE_GRAM_TR
+#define TURTLE_GRAM_TR 1
+#endif
+template <typename T> constexpr int gram_gp() { return sizeof(T) == 2 ? 32 : 16; }  // pixels per step
 constexpr int GMAXT = 24;        // max 16x16 accumulator tiles per wave (ch=64, 6 segments)
+constexpr int GMAXV = 7;         // max 16-byte staging vectors per thread per step
 
+__device__ __attribute__((aligned(64))) uint4 g_zero_gram[4];
+
+// q^T [k_seg0 | k_seg1 | ...] over a pixel chunk, plus per-column sums of squares.
+// LDS holds [pixel][channel] tiles exactly as they sit in HBM (16-byte row chunks); the MFMA
+// operands need 8 consecutive pixels of one channel per lane, which ds_read_b64_tr_b16 delivers
+// (two 4-row transposed reads), so nothing is transposed in registers.
 template <typename T>
 __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float gsm[];
+  extern __shared__ __attribute__((aligned(16))) char gsm[];
+  constexpr int VEC = Vec<T>::N, ES = sizeof(T), GP = gram_gp<T>();
   const int ch = a.ch, ncol = a.nseg * ch;
-  float* sq = gsm;                 // [GP][ch]
-  float* sk = gsm + GP * ch;       // [GP][ncol]
+  const int RQ = ch * ES + 16, RK = ncol * ES + 16;          // LDS row strides (bytes)
+  char* sq = gsm;                                            // [GP][RQ]
+  char* sk = gsm + GP * RQ;                                  // [GP][RK]
+  float* nrm = reinterpret_cast<float*>(gsm + GP * (RQ + RK)); // [ch + ncol]
   const int bh = blockIdx.x / a.nchunk, chunk = blockIdx.x % a.nchunk;
   const int b = bh / a.heads, h = bh % a.heads;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int p_beg = chunk * a.chunk, p_end = min(a.HW, p_beg + a.chunk);
-  const int ti_n = ch / 16, tj_n = ncol / 16, TT = ti_n * tj_n;
-  constexpr int VEC = Vec<T>::N;
-  const int qv = ch / VEC, kvn = ncol / VEC;
+  const int tj_n = ncol / 16, TT = (ch / 16) * tj_n;
+  const int qv = ch / VEC, CVt = (ch + ncol) / VEC;          // vectors per pixel
+  const int NV = GP * CVt;
+
+  for (int i = tid; i < ch + ncol; i += 256) nrm[i] = 0.f;
+
+  // per-thread staging geometry (fixed across steps)
+  const T* src[GMAXV];
+  int64_t pstride[GMAXV];
+  int lds_off[GMAXV], vpx[GMAXV];
+#pragma unroll
+  for (int j = 0; j < GMAXV; ++j) {
+    const int v = tid + 256 * j;
+    const int px = v / CVt, cv = v % CVt;
+    vpx[j] = v < NV ? px : -1;
+    if (cv < qv) {
+      src[j] = reinterpret_cast<const T*>(a.q) + (int64_t)b * a.HW * a.ldq + a.qoff + h * ch + cv * VEC;
+      pstride[j] = a.ldq;
+      lds_off[j] = px * RQ + cv * VEC * ES;
+    } else {
+      const int kc = (cv - qv) * VEC, s = kc / ch, jj = kc - s * ch;
+      const GramSeg& g = a.seg[s < a.nseg ? s : 0];
+      src[j] = reinterpret_cast<const T*>(g.base) + ((int64_t)b * g.img_mul + g.img_add) * a.HW * g.ld + g.off +
+               (int64_t)h * g.hstride + jj;
+      pstride[j] = g.ld;
+      lds_off[j] = GP * RQ + px * RK + kc * ES;
+    }
+  }
 
   f32x4 acc[GMAXT];
 #pragma unroll
   for (int t = 0; t < GMAXT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float nq = 0.f, nk0 = 0.f, nk1 = 0.f;   // column sums of squares (threads own columns)
+  float sqs[GMAXV][VEC];
+#pragma unroll
+  for (int j = 0; j < GMAXV; ++j)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) sqs[j][e] = 0.f;
 
+  uint4 stg[GMAXV];
+  auto load = [&](int p0) {
+#pragma unroll
+    for (int j = 0; j < GMAXV; ++j) {
+      const int p = p0 + vpx[j];
+      const bool ok = vpx[j] >= 0 && p < p_end;
+      stg[j] = ld16(ok ? reinterpret_cast<const void*>(src[j] + (int64_t)p * pstride[j]) : g_zero_gram);
+    }
+  };
+
+  load(p_beg);
   for (int p0 = p_beg; p0 < p_end; p0 += GP) {
-    // stage q and the key segments of GP pixels as fp32
-    for (int v = tid; v < GP * (qv + kvn); v += 256) {
-      const int pr = v / (qv + kvn), cvi = v % (qv + kvn);
-      const int p = p0 + pr;
-      Vec<T> x; x.zero();
-      float* dst;
-      if (cvi < qv) {
-        if (p < p_end)
-          x.load(reinterpret_cast<const T*>(a.q) + ((int64_t)b * a.HW + p) * a.ldq + a.qoff + h * ch + cvi * VEC);
-        dst = sq + pr * ch + cvi * VEC;
+#pragma unroll
+    for (int j = 0; j < GMAXV; ++j) {
+      if (vpx[j] < 0) continue;
+      *reinterpret_cast<uint4*>(gsm + lds_off[j]) = stg[j];
+      float x[VEC];
+      if constexpr (sizeof(T) == 2) {
+        const uint32_t w[4] = {stg[j].x, stg[j].y, stg[j].z, stg[j].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { x[2 * i] = __uint_as_float(w[i] << 16); x[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
       } else {
-        const int kc = (cvi - qv) * VEC, s = kc / ch, j = kc % ch;
-        const GramSeg& g = a.seg[s];
-        if (p < p_end)
-          x.load(reinterpret_cast<const T*>(g.base) +
-                 (((int64_t)b * g.img_mul + g.img_add) * a.HW + p) * g.ld + g.off + (int64_t)h * g.hstride + j);
-        dst = sk + pr * ncol + kc;
+        x[0] = __uint_as_float(stg[j].x); x[1] = __uint_as_float(stg[j].y);
+        x[2] = __uint_as_float(stg[j].z); x[3] = __uint_as_float(stg[j].w);
       }
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) dst[i] = x.v[i];
+      for (int e = 0; e < VEC; ++e) sqs[j][e] = fmaf(x[e], x[e], sqs[j][e]);
     }
     __syncthreads();
-    // column sums of squares
-    if (tid < ch + ncol) {
-      for (int pr = 0; pr < GP; ++pr) {
-        float x = tid < ch ? sq[pr * ch + tid] : sk[pr * ncol + tid - ch];
-        nq += x * x;
-      }
-    }
-    if (tid + 256 < ch + ncol) {
-      for (int pr = 0; pr < GP; ++pr) {
-        float x = sk[pr * ncol + tid + 256 - ch];
-        nk0 += x * x;
-      }
-    }
-    // MFMA: D[i][j] += sum_kk q[kk][i] k[kk][j]; lane supplies A[i=l&15][kk=l>>4], B[kk][j=l&15]
-#pragma unroll
-    for (int kk = 0; kk < GP; kk += 4) {
-      const int pr = kk + (lane >> 4);
+    if (p0 + GP < p_end) load(p0 + GP);
+    if constexpr (sizeof(T) == 2 && TURTLE_GRAM_TR) {
+      // lane l: rows (pixels) 8*(l>>4) + q (+4), columns c0 + 4p; receives column c0 + (l&15)
+      const int g16 = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+      typedef short v4s __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(3))) v4s lds_v4s;
 #pragma unroll
       for (int t = 0; t < GMAXT; ++t) {
         const int tile = wid + 4 * t;
         if (tile < TT) {
-          const int it = tile / tj_n, jt = tile % tj_n;
-          const float av = sq[pr * ch + it * 16 + (lane & 15)];
-          const float bv = sk[pr * ncol + jt * 16 + (lane & 15)];
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
+          const int it = tile / tj_n, jt = tile - it * tj_n;
+          const char* qa = sq + (8 * g16 + qq) * RQ + (it * 16 + 4 * pp) * 2;
+          const char* ka = sk + (8 * g16 + qq) * RK + (jt * 16 + 4 * pp) * 2;
+          const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)qa);
+          const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(qa + 4 * RQ));
+          const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)ka);
+          const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(ka + 4 * RK));
+          typedef short v8s __attribute__((ext_vector_type(8)));
+          const bf16x8 af = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+          const bf16x8 bfr = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[t], 0, 0, 0);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < GP; kk += 4) {
+        const int pr = kk + (lane >> 4);
+#pragma unroll
+        for (int t = 0; t < GMAXT; ++t) {
+          const int tile = wid + 4 * t;
+          if (tile < TT) {
+            const int it = tile / tj_n, jt = tile - it * tj_n;
+            const float av = to_f(*reinterpret_cast<const T*>(sq + pr * RQ + (it * 16 + (lane & 15)) * ES));
+            const float bv = to_f(*reinterpret_cast<const T*>(sk + pr * RK + (jt * 16 + (lane & 15)) * ES));
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
+          }
         }
       }
     }
     __syncthreads();
   }
-  (void)nk1;
+  // column sums of squares: per-thread partials -> LDS atomics
+#pragma unroll
+  for (int j = 0; j < GMAXV; ++j) {
+    if (vpx[j] < 0) continue;
+    const int cv = (tid + 256 * j) % CVt;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) atomicAdd(&nrm[cv * VEC + e], sqs[j][e]);
+  }
+  __syncthreads();
   const int stride = ch * ncol + ch + ncol;
   float* out = a.part + ((int64_t)bh * a.nchunk + chunk) * stride;
 #pragma unroll
@@ -102,14 +169,13 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
         out[(it * 16 + (lane >> 4) * 4 + r) * ncol + jt * 16 + (lane & 15)] = acc[t][r];
     }
   }
-  if (tid < ch + ncol) out[ch * ncol + tid] = nq;          // [nq (ch) | nk (ncol)]
-  if (tid + 256 < ch + ncol) out[ch * ncol + tid + 256] = nk0;
+  for (int i = tid; i < ch + ncol; i += 256) out[ch * ncol + i] = nrm[i];   // [nq (ch) | nk (ncol)]
 }
 
 template <typename T>
 void launch_gram(const GramArgs& a, hipStream_t st) {
   const int ncol = a.nseg * a.ch;
-  const size_t lds = (size_t)GP * (a.ch + ncol) * sizeof(float);
+  const size_t lds = (size_t)gram_gp<T>() * ((a.ch + ncol) * sizeof(T) + 32) + (a.ch + ncol) * sizeof(float);
   hipLaunchKernelGGL(gram_kernel<T>, dim3((unsigned)(a.B * a.heads * a.nchunk)), dim3(256), lds, st, a);
 }
 

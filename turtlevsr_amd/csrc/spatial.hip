@@ -15,73 +15,98 @@ namespace turtle {
 // depthwise 3x3: one thread = one pixel x VEC channels
 // ------------------------------------------------------------------------------------------
 template <typename T>
+TURTLE_DEV void unpack16(const uint4& q, float (&v)[Vec<T>::N]);
+template <>
+TURTLE_DEV void unpack16<bf16>(const uint4& q, float (&v)[8]) {
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(w[i] << 16); v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+}
+template <>
+TURTLE_DEV void unpack16<float>(const uint4& q, float (&v)[4]) {
+  v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+}
+
+__device__ __attribute__((aligned(64))) uint4 g_zero_dw[4];
+
+// one thread = one pixel x VEC channels; the 9 (18 for the gate) neighbour vectors are loaded
+// unconditionally (out-of-image taps read a zero line), so all of them are in flight together.
+// Block ids are remapped so each XCD sweeps a contiguous band of rows (vertical reuse in its L2).
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
   constexpr int VEC = Vec<T>::N;
   const int CV = a.C / VEC;
   const int64_t total = (int64_t)a.nimg * a.H * a.W * CV;
-  const int Cw = a.mode == DW_GATE ? 2 * a.C : a.C;
+  const int Cw = MODE == DW_GATE ? 2 * a.C : a.C;
   const T* in = reinterpret_cast<const T*>(a.in);
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int cv = (int)(idx % CV);
-    const int64_t pix = idx / CV;
-    const int x = (int)(pix % a.W);
-    const int64_t t = pix / a.W;
-    const int y = (int)(t % a.H);
-    const int64_t img = t / a.H;
-    const int c0 = cv * VEC;
-    float acc1[VEC], acc2[VEC];
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      acc1[i] = a.bias ? a.bias[c0 + i] : 0.f;
-      acc2[i] = (a.mode == DW_GATE && a.bias) ? a.bias[a.C + c0 + i] : 0.f;
-    }
-#pragma unroll
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int yy = y + dy;
-      if (yy < 0 || yy >= a.H) continue;
-#pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int xx = x + dx;
-        if (xx < 0 || xx >= a.W) continue;
-        const int tap = (dy + 1) * 3 + (dx + 1);
-        const T* p = in + ((img * a.H + yy) * a.W + xx) * a.ldi + a.offi + c0;
-        const float* wt = a.w + tap * Cw + c0;
-        Vec<T> v; v.load(p);
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) acc1[i] = fmaf(wt[i], v.v[i], acc1[i]);
-        if (a.mode == DW_GATE) {
-          Vec<T> v2; v2.load(p + a.C);
-#pragma unroll
-          for (int i = 0; i < VEC; ++i) acc2[i] = fmaf(wt[a.C + i], v2.v[i], acc2[i]);
-        }
-      }
-    }
-    Vec<T> o;
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) {
-      float r = acc1[i];
-      if (a.mode == DW_GELU) r = gelu_erf(r);
-      else if (a.mode == DW_GATE) r = gelu_erf(r) * acc2[i];
-      o.v[i] = r;
-    }
-    int64_t dst;
-    if (a.tok_ws > 0) {
-      const int ws = a.tok_ws, h = a.H / ws, w = a.W / ws;
-      const int p1 = y / h, i = y - p1 * h, p2 = x / w, j = x - p2 * w;
-      dst = img * a.tok_img_stride + ((int64_t)i * w + j) * ((int64_t)ws * ws * a.C) + (int64_t)(p1 * ws + p2) * a.C + c0;
-    } else {
-      dst = pix * a.ldo + a.offo + c0;
-    }
-    o.store(reinterpret_cast<T*>(a.out) + dst);
+  int lin = blockIdx.x;
+  {
+    const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
+    lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;
   }
+  const int64_t idx = (int64_t)lin * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const int cv = (int)(idx % CV);
+  const int64_t pix = idx / CV;
+  const int x = (int)(pix % a.W);
+  const int64_t t = pix / a.W;
+  const int y = (int)(t % a.H);
+  const int64_t img = t / a.H;
+  const int c0 = cv * VEC;
+  uint4 q1[9], q2[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+    const bool ok = yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+    const T* p = in + ((img * a.H + yy) * a.W + xx) * a.ldi + a.offi + c0;
+    q1[tap] = ld16(ok ? reinterpret_cast<const void*>(p) : g_zero_dw);
+    if constexpr (MODE == DW_GATE) q2[tap] = ld16(ok ? reinterpret_cast<const void*>(p + a.C) : g_zero_dw);
+  }
+  float acc1[VEC], acc2[VEC];
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    acc1[i] = a.bias ? a.bias[c0 + i] : 0.f;
+    acc2[i] = (MODE == DW_GATE && a.bias) ? a.bias[a.C + c0 + i] : 0.f;
+  }
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const float* wt = a.w + tap * Cw + c0;
+    float v[VEC];
+    unpack16<T>(q1[tap], v);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc1[i] = fmaf(wt[i], v[i], acc1[i]);
+    if constexpr (MODE == DW_GATE) {
+      unpack16<T>(q2[tap], v);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc2[i] = fmaf(wt[a.C + i], v[i], acc2[i]);
+    }
+  }
+  Vec<T> o;
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) {
+    float r = acc1[i];
+    if (MODE == DW_GELU) r = gelu_erf(r);
+    else if (MODE == DW_GATE) r = gelu_erf(r) * acc2[i];
+    o.v[i] = r;
+  }
+  int64_t dst;
+  if (a.tok_ws > 0) {
+    const int ws = a.tok_ws, h = a.H / ws, w = a.W / ws;
+    const int p1 = y / h, i = y - p1 * h, p2 = x / w, j = x - p2 * w;
+    dst = img * a.tok_img_stride + ((int64_t)i * w + j) * ((int64_t)ws * ws * a.C) + (int64_t)(p1 * ws + p2) * a.C + c0;
+  } else {
+    dst = pix * a.ldo + a.offo + c0;
+  }
+  o.store(reinterpret_cast<T*>(a.out) + dst);
 }
 
 template <typename T>
 void launch_dw(const DwArgs& a, hipStream_t st) {
   const int64_t total = (int64_t)a.nimg * a.H * a.W * (a.C / Vec<T>::N);
-  int64_t blocks = (total + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(dw_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  const int64_t blocks = (total + 255) / 256;
+  if (a.mode == DW_GATE) hipLaunchKernelGGL((dw_kernel<T, DW_GATE>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else if (a.mode == DW_GELU) hipLaunchKernelGGL((dw_kernel<T, DW_GELU>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((dw_kernel<T, DW_PLAIN>), dim3((unsigned)blocks), dim3(256), 0, st, a);
 }
 
 // ------------------------------------------------------------------------------------------

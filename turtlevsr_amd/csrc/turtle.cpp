@@ -540,7 +540,8 @@ struct Runner {
   void chan_attn(const BlockW& bw, const Blk& b, const T* q, int64_t ldq, int qoff, const std::vector<Seg>& segs,
                  const SrcList& vsrc, int HW, int Wimg, T* x, float* kinv, int cur_seg) {
     const int c = b.dim, ch = c / b.heads, nseg = (int)segs.size(), ncol = nseg * ch;
-    int nchunk = std::max(1, std::min((HW + 2047) / 2048, std::max(1, 1024 / (B * b.heads))));
+    // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each
+    int nchunk = std::max(1, std::min((HW + 255) / 256, std::max(1, 1024 / (B * b.heads))));
     int chunk = (HW + nchunk - 1) / nchunk;
     chunk = (chunk + 31) / 32 * 32;
     nchunk = (HW + chunk - 1) / chunk;
