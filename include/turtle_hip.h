@@ -112,7 +112,8 @@ int turtle_forward(TurtleHandle* h, const float* inp, int B, int H, int W, float
 #define TURTLE_K_SAB_AV 4     /* SAB clipped softmax + sparse A.v gather                   */
 #define TURTLE_K_WINDOW 5     /* SAB window conv + L2 norm                                 */
 #define TURTLE_K_OTHER 6      /* stem, ending, cache roll / copies                          */
-#define TURTLE_K_COUNT 7
+#define TURTLE_K_FUSED 7      /* fused pointwise -> depthwise -> pointwise blocks (fused.hip) */
+#define TURTLE_K_COUNT 8
 #define TURTLE_K_ALL 99
 int turtle_profile_begin(TurtleHandle* h, int kernel_class);
 int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);

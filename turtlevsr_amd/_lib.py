@@ -62,7 +62,7 @@ def lib():
 EXPORTED = ["turtle_create", "turtle_destroy", "turtle_num_weights", "turtle_weight_info", "turtle_set_weight",
             "turtle_load_weights", "turtle_cache_layout", "turtle_workspace_size", "turtle_forward",
             "turtle_profile_begin", "turtle_profile_end", "turtle_last_error"]
-K_CLASSES = ["gemm", "dwconv", "chan_attn", "sab_score", "sab_av", "sab_window", "other"]
+K_CLASSES = ["gemm", "dwconv", "chan_attn", "sab_score", "sab_av", "sab_window", "other", "fused"]
 K_ALL = 99
 
 

@@ -179,88 +179,113 @@ void launch_gram(const GramArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(gram_kernel<T>, dim3((unsigned)(a.B * a.heads * a.nchunk)), dim3(256), lds, st, a);
 }
 
-// reduce the pixel splits: red[bh][e] = sum_c part[bh][c][e]
-__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* part, float* red, int nchunk, int stride, int nbh) {
-  const int64_t total = (int64_t)nbh * stride;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int64_t bh = idx / stride, e = idx % stride;
-    const float* p = part + bh * nchunk * stride + e;
-    float s = 0.f;
-    for (int c = 0; c < nchunk; ++c) s += p[(int64_t)c * stride];
-    red[idx] = s;
+// reduce the pixel splits in two deterministic levels: this kernel sums the chunks of split g
+// (c = g, g + S, ...) into red[bh][g][e]; the softmax kernel adds the S partial sums it reads
+__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* part, float* red, int nchunk, int stride, int S) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= stride) return;
+  const int bh = blockIdx.y, g = blockIdx.z;
+  const float* p = part + ((int64_t)bh * nchunk + g) * stride + e;
+  const int64_t step = (int64_t)S * stride;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int c = g;
+  for (; c + 3 * S < nchunk; c += 4 * S, p += 4 * step) {
+    s0 += p[0]; s1 += p[step]; s2 += p[2 * step]; s3 += p[3 * step];
   }
+  for (; c < nchunk; c += S, p += step) s0 += p[0];
+  red[((int64_t)bh * S + g) * stride + e] = (s0 + s1) + (s2 + s3);
 }
 
-// one block per (b, h): logits, softmax over all key columns, 1/|k_cur|
+// one wave per query row i of (b, h): logits over all key columns (sum of the S partials),
+// softmax, and 1/|k_cur| for the FHR cache (turtle_t1_arch.py:357-366, 598-600)
+constexpr int SM_MAXC = 512 / 64;
 __global__ __launch_bounds__(256) void attn_softmax_kernel(AttnFinArgs a) {
-  const int ch = a.ch, ncol = a.nseg * ch, stride = ch * ncol + ch + ncol;
+  const int ch = a.ch, ncol = a.nseg * ch, stride = ch * ncol + ch + ncol, S = a.nsplit;
   const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
-  const float* G = a.red + (int64_t)bh * stride;
-  const float* nq = G + ch * ncol;
-  const float* nk = nq + ch;
+  const float* R = a.red + (int64_t)bh * S * stride;
+  auto sum_s = [&](int e) {
+    float v = 0.f;
+    for (int g = 0; g < S; ++g) v += R[(int64_t)g * stride + e];
+    return v;
+  };
   __shared__ float kinv_s[512];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (int j = tid; j < ncol; j += 256) {
     const int s = j / ch;
-    kinv_s[j] = ((a.norm_mask >> s) & 1) ? 1.f / fmaxf(sqrtf(nk[j]), 1e-12f) : 1.f;
+    kinv_s[j] = ((a.norm_mask >> s) & 1) ? 1.f / fmaxf(sqrtf(sum_s(ch * ncol + ch + j)), 1e-12f) : 1.f;
   }
   __syncthreads();
-  const float tau = a.tau[h];
-  float* A = a.attn + (int64_t)bh * ch * ncol;
-  for (int i = wid; i < ch; i += 4) {
-    const float qi = tau / fmaxf(sqrtf(nq[i]), 1e-12f);
-    float mx = -INFINITY;
-    for (int j = lane; j < ncol; j += 64) mx = fmaxf(mx, G[i * ncol + j] * qi * kinv_s[j]);
-    mx = wave_max(mx);
-    float sum = 0.f;
-    for (int j = lane; j < ncol; j += 64) {
-      const float e = expf(G[i * ncol + j] * qi * kinv_s[j] - mx);
-      A[i * ncol + j] = e;
-      sum += e;
-    }
-    sum = wave_sum(sum);
-    const float inv = 1.f / sum;
-    for (int j = lane; j < ncol; j += 64) A[i * ncol + j] *= inv;
-  }
-  if (a.kinv && a.cur_seg >= 0)
+  if (blockIdx.y == 0 && a.kinv && a.cur_seg >= 0)
     for (int j = tid; j < ch; j += 256) a.kinv[(int64_t)b * a.heads * ch + h * ch + j] = kinv_s[a.cur_seg * ch + j];
+  const int i = blockIdx.y * 4 + wid;
+  if (i >= ch) return;
+  const float qi = a.tau[h] / fmaxf(sqrtf(sum_s(ch * ncol + i)), 1e-12f);
+  float lg[SM_MAXC];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < SM_MAXC; ++k) {
+    const int j = lane + 64 * k;
+    lg[k] = j < ncol ? sum_s(i * ncol + j) * qi * kinv_s[j] : -INFINITY;
+    mx = fmaxf(mx, lg[k]);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < SM_MAXC; ++k) {
+    lg[k] = lane + 64 * k < ncol ? expf(lg[k] - mx) : 0.f;
+    sum += lg[k];
+  }
+  const float inv = 1.f / wave_sum(sum);
+  float* A = a.attn + ((int64_t)bh * ch + i) * ncol;
+#pragma unroll
+  for (int k = 0; k < SM_MAXC; ++k)
+    if (lane + 64 * k < ncol) A[lane + 64 * k] = lg[k] * inv;
 }
+
+int attn_nsplit(int nchunk) { return nchunk < 32 ? nchunk : 32; }
 
 void launch_attn_finalize(const AttnFinArgs& a, hipStream_t st) {
   const int ncol = a.nseg * a.ch, stride = a.ch * ncol + a.ch + ncol, nbh = a.B * a.heads;
-  int64_t blocks = ((int64_t)nbh * stride + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a.part, a.red, a.nchunk, stride, nbh);
-  hipLaunchKernelGGL(attn_softmax_kernel, dim3((unsigned)nbh), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((stride + 255) / 256), (unsigned)nbh, (unsigned)a.nsplit),
+                     dim3(256), 0, st, a.part, a.red, a.nchunk, stride, a.nsplit);
+  hipLaunchKernelGGL(attn_softmax_kernel, dim3((unsigned)nbh, (unsigned)((a.ch + 3) / 4)), dim3(256), 0, st, a);
 }
 
 // W_eff[b][o][seg_col[s] + h*seg_hstride[s] + j] = sum_i Wp[o][h*ch + i] * A[b,h][i][s*ch + j]
+// block = (4 output channels, b*h); threads stride the key columns, so A rows load coalesced and
+// the Wp operands are wave-uniform (scalar loads)
+constexpr int WE_OT = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void weff_kernel(WeffArgs a) {
   const int ch = a.ch, ncol = a.nseg * ch;
-  const int64_t total = (int64_t)a.B * a.C * a.heads * ncol;
+  const int o0 = blockIdx.x * WE_OT, bh = blockIdx.y, b = bh / a.heads, h = bh % a.heads;
   T* W = reinterpret_cast<T*>(a.weff);
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int col = (int)(idx % ncol);
-    int64_t t = idx / ncol;
-    const int h = (int)(t % a.heads); t /= a.heads;
-    const int o = (int)(t % a.C);
-    const int b = (int)(t / a.C);
-    const int s = col / ch, j = col % ch;
-    const float* wp = a.wp + (int64_t)o * a.C + h * ch;
-    const float* A = a.attn + ((int64_t)(b * a.heads + h) * ch) * ncol + col;
-    float acc = 0.f;
-    for (int i = 0; i < ch; ++i) acc = fmaf(wp[i], A[(int64_t)i * ncol], acc);
-    W[((int64_t)b * a.C + o) * a.Keff + a.seg_col[s] + (int64_t)h * a.seg_hstride[s] + j] = from_f<T>(acc);
+  const float* A = a.attn + (int64_t)bh * ch * ncol;
+  for (int col = threadIdx.x; col < ncol; col += 256) {
+    float acc[WE_OT];
+#pragma unroll
+    for (int t = 0; t < WE_OT; ++t) acc[t] = 0.f;
+    for (int i = 0; i < ch; ++i) {
+      const float av = A[(int64_t)i * ncol + col];
+#pragma unroll
+      for (int t = 0; t < WE_OT; ++t)
+        if (o0 + t < a.C) acc[t] = fmaf(a.wp[(int64_t)(o0 + t) * a.C + h * ch + i], av, acc[t]);
+    }
+    const int sg = col / ch, jj = col - sg * ch;
+    int64_t scol = a.seg_col[0];
+    int shs = a.seg_hstride[0];
+#pragma unroll
+    for (int q = 1; q < TURTLE_MAX_SEG; ++q)
+      if (sg == q) { scol = a.seg_col[q]; shs = a.seg_hstride[q]; }
+#pragma unroll
+    for (int t = 0; t < WE_OT; ++t)
+      if (o0 + t < a.C) W[((int64_t)b * a.C + o0 + t) * a.Keff + scol + (int64_t)h * shs + jj] = from_f<T>(acc[t]);
   }
 }
 
 template <typename T>
 void launch_weff(const WeffArgs& a, hipStream_t st) {
-  const int64_t total = (int64_t)a.B * a.C * a.heads * a.nseg * a.ch;
-  int64_t blocks = (total + 255) / 256;
-  if (blocks > 16384) blocks = 16384;
-  hipLaunchKernelGGL(weff_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(weff_kernel<T>, dim3((unsigned)((a.C + WE_OT - 1) / WE_OT), (unsigned)(a.B * a.heads)), dim3(256), 0, st, a);
 }
 
 template void launch_gram<float>(const GramArgs&, hipStream_t);

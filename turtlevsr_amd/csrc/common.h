@@ -34,6 +34,9 @@ template <> struct Vec<float> {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
   TURTLE_DEV void zero() { v[0] = v[1] = v[2] = v[3] = 0.f; }
+  TURTLE_DEV void from_raw(uint4 q) {
+    v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+  }
   // unconditional load from a valid address, zeroed when !ok (no branch around the load, so the
   // compiler keeps several loads in flight instead of waiting on each: guide §5 trap (c))
   TURTLE_DEV void load_pred(const float* p, bool ok) {
@@ -46,6 +49,14 @@ template <> struct Vec<bf16> {
   float v[8];
   TURTLE_DEV void load(const bf16* p) {
     uint4 q = *reinterpret_cast<const uint4*>(p);
+    uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  TURTLE_DEV void from_raw(uint4 q) {
     uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -85,6 +96,30 @@ TURTLE_DEV uint4 ld16(const void* p) {
   return *reinterpret_cast<gUint4*>(a);   // global_load_dwordx4 (not flat)
 #else
   return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+
+// same, 8 bytes
+TURTLE_DEV uint2 ld8(const void* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(1))) const uint2 gUint2;
+  uint64_t a = reinterpret_cast<uint64_t>(p);
+  asm volatile("" : "+v"(a));
+  return *reinterpret_cast<gUint2*>(a);
+#else
+  return *reinterpret_cast<const uint2*>(p);
+#endif
+}
+
+// same for one fp32 value
+TURTLE_DEV float ld4f(const float* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(1))) const float gF;
+  uint64_t a = reinterpret_cast<uint64_t>(p);
+  asm volatile("" : "+v"(a));
+  return *reinterpret_cast<gF*>(a);
+#else
+  return *p;
 #endif
 }
 

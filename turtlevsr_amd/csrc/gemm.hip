@@ -89,12 +89,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
   float* e_b = e_t + BN;
   float* e_c = e_b + BN;
   if (tid < BN) {
-    const int n = n0 + tid;
-    const bool ok = n < g.N;
-    e_s[tid] = (ok && g.ln_s) ? g.ln_s[n] : 0.f;
-    e_t[tid] = (ok && g.ln_t) ? g.ln_t[n] : 0.f;
-    e_b[tid] = (ok && g.bias) ? g.bias[n] : 0.f;
-    e_c[tid] = (ok && g.scale) ? g.scale[n] : 1.f;
+    // unconditional loads (absent vectors read the constant zero / one lines)
+    const int n = min(n0 + tid, g.N - 1);
+    const float vs = (g.ln_s ? g.ln_s : g.zeros)[n], vt = (g.ln_t ? g.ln_t : g.zeros)[n];
+    const float vb = (g.bias ? g.bias : g.zeros)[n], vc = (g.scale ? g.scale : g.ones)[n];
+    e_s[tid] = vs; e_t[tid] = vt; e_b[tid] = vb; e_c[tid] = vc;
   }
 
   // ---- per-thread load geometry: rows are fixed over K, so resolve pixel coordinates once ----
@@ -265,8 +264,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       Vec<T> rv; rv.load_pred(res + (full ? m * g.ldr + g.offr + nb : 0), full);
 #pragma unroll
       for (int e = 0; e < VEC; ++e) v[j].v[e] += rv.v[e];
-      if (okc[j] && !full)
-        for (int e = 0; e < VEC && nb + e < g.N; ++e) v[j].v[e] += to_f(res[m * g.ldr + g.offr + nb + e]);
+      if (okc[j] && !full) {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e)
+          if (nb + e < g.N) v[j].v[e] += to_f(res[m * g.ldr + g.offr + nb + e]);
+      }
     }
   }
 #pragma unroll
@@ -286,7 +288,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       if (g.store_mode == STORE_UNSHUFFLE) {
         const int64_t dp = ((int64_t)img * (Hi / 2) + y / 2) * (Wi / 2) + x / 2;
         const int sub = (y & 1) * 2 + (x & 1);
-        for (int e = 0; e < VEC && nb + e < g.N; ++e) o[dp * g.ldo + g.offo + (nb + e) * 4 + sub] = from_f<T>(v[j].v[e]);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e)
+          if (nb + e < g.N) o[dp * g.ldo + g.offo + (nb + e) * 4 + sub] = from_f<T>(v[j].v[e]);
         continue;
       }
       // PixelShuffle: weights were permuted so output channel n' = s*Cq + c (a chunk stays in
@@ -294,9 +298,253 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
       const int Cq = g.N / 4, sp = nb / Cq, cn = nb - sp * Cq;
       dst = (((int64_t)img * 2 * Hi + 2 * y + (sp >> 1)) * (2 * Wi) + 2 * x + (sp & 1)) * g.ldo + g.offo + cn;
     }
-    if (full) v[j].store(o + dst);
-    else for (int e = 0; e < VEC && nb + e < g.N; ++e) o[dst + e] = from_f<T>(v[j].v[e]);
+    if (full) {
+      v[j].store(o + dst);
+    } else {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e)
+        if (nb + e < g.N) o[dst + e] = from_f<T>(v[j].v[e]);
+    }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// Panel GEMM (bf16, plain pixel-major store, K <= 512): the block's BM x K pixel panel is loaded
+// into LDS once (all loads in flight together, LayerNorm statistics taken from it), then the
+// block sweeps its range of 128-channel output tiles with no further barrier: each wave owns 32
+// channels, reads its W fragments straight from L2 into registers (refilled for the next tile
+// right after their last use, so the fetch hides behind a whole tile of MFMAs), and its epilogue
+// vectors / residual are fetched at tile start and consumed at tile end. The output tile goes
+// out as 8-byte stores (4 channels per lane, 32 contiguous bytes per pixel per wave).
+// Against the K-loop kernel above this trades per-K-step barriers and exposed load latency for
+// one load phase per block; X is read from HBM exactly once per split.
+// ------------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(64))) float g_one_line[16] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f,
+                                                                1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+constexpr int PANEL_BN = 128;
+
+template <int BM, int KS>
+__global__ __launch_bounds__(256, 2) void gemm_panel_kernel(GemmArgs g, int nsplit) {
+  constexpr int KP = KS * 32;                    // padded K (elements)
+  constexpr int XROWB = KP * 2 + 16;             // LDS row bytes (16 B pad: conflict-free fragments)
+  constexpr int KV = KP / 8;                     // 16-byte vectors per row
+  constexpr int NV = BM * KV / 256;              // panel vectors per thread
+  constexpr int MT = BM / 16, TN = 2;
+  constexpr int TPR = 256 / BM;                  // threads per row for the LN statistics
+  static_assert(BM * KV % 256 == 0, "panel tiling");
+  __shared__ __attribute__((aligned(16))) char smem[BM * XROWB + 2 * BM * 4];
+  char* sX = smem;
+  float* s_mu = reinterpret_cast<float*>(smem + BM * XROWB);
+  float* s_rs = s_mu + BM;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  int lin = blockIdx.x;
+  {
+    const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
+    lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;
+  }
+  const int split = lin % nsplit, panel = lin / nsplit;
+  int64_t m0, mlim;
+  if (g.wstride) {
+    const int tpi = (g.HW + BM - 1) / BM;
+    const int64_t im = panel / tpi;
+    m0 = im * g.HW + (int64_t)(panel % tpi) * BM;
+    mlim = min(g.M, (im + 1) * (int64_t)g.HW);
+  } else {
+    m0 = (int64_t)panel * BM;
+    mlim = g.M;
+  }
+  const int K = g.a.Ktot;
+  const int ntiles = (g.N + PANEL_BN - 1) / PANEL_BN;
+  const int nt_beg = split * ntiles / nsplit, nt_end = (split + 1) * ntiles / nsplit;
+  const bf16* Wp = reinterpret_cast<const bf16*>(g.w) + (g.wstride ? (int64_t)((int)(m0 / g.HW) / g.wdiv) * g.wstride : 0);
+
+  // ---- X panel -> LDS (source select scan per vector, zero line for padding / missing rows) ----
+  {
+    uint4 xv[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + 256 * i, r = v / KV, k = (v - r * KV) * 8;
+      const int64_t m = m0 + r;
+      const bool ok = m < mlim && k < K;
+      const int mm = ok ? (int)m : (int)m0;
+      const int img = mm / g.HW, p = mm - img * g.HW;
+      const bf16* base = reinterpret_cast<const bf16*>(g.a.s[0].base);
+      int64_t sld = g.a.s[0].ld;
+      int soff = g.a.s[0].off, smul = g.a.s[0].img_mul, sadd = g.a.s[0].img_add, kb = 0, kbj = g.a.s[0].K;
+#pragma unroll
+      for (int j = 1; j < TURTLE_MAX_SRC; ++j) {
+        if (j < g.a.n) {
+          const bool hit = k >= kbj;
+          base = hit ? reinterpret_cast<const bf16*>(g.a.s[j].base) : base;
+          sld = hit ? g.a.s[j].ld : sld;
+          soff = hit ? g.a.s[j].off : soff;
+          smul = hit ? g.a.s[j].img_mul : smul;
+          sadd = hit ? g.a.s[j].img_add : sadd;
+          kb = hit ? kbj : kb;
+          kbj += g.a.s[j].K;
+        }
+      }
+      const int64_t off = ((int64_t)(img * smul + sadd) * g.HW + p) * sld + soff + (k - kb);
+      xv[i] = ld16(ok ? reinterpret_cast<const void*>(base + off) : g_zero_line);
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + 256 * i, r = v / KV, kv = v - r * KV;
+      *reinterpret_cast<uint4*>(sX + r * XROWB + kv * 16) = xv[i];
+    }
+  }
+
+  // ---- this wave's W fragments / epilogue vectors / residual for output tile nt ----
+  // Every load below is unconditional from a uniform base with a clamped 32-bit offset: rows past
+  // the panel and channels past N read valid memory that is never stored, K padding meets zeros
+  // in the X panel, and absent vectors / residual point at the constant zero / one lines.
+  const float* ps = g.ln_s ? g.ln_s : g.zeros;
+  const float* pt = g.ln_t ? g.ln_t : g.zeros;
+  const float* pb = g.bias ? g.bias : g.zeros;
+  const float* pc = g.scale ? g.scale : g.ones;
+  const bf16* pr = g.res ? reinterpret_cast<const bf16*>(g.res) : reinterpret_cast<const bf16*>(g.zeros);
+  const int ldr = g.res ? (int)g.ldr : 0, offr = g.res ? g.offr : 0;
+  const int mlast = (int)(mlim - m0) - 1;               // last valid row of the panel
+  bf16x8 wf[TN][KS];
+  auto load_w = [&](int nt, int ks) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int n = min(nt * PANEL_BN + wid * 32 + tn * 16 + (lane & 15), g.N - 1);
+      const int k = min(ks * 32 + (lane >> 4) * 8, K - 8);
+      wf[tn][ks] = *reinterpret_cast<const bf16x8*>(Wp + n * (int)g.ldw + k);
+    }
+  };
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  f4 vs[TN], vt[TN], vb[TN], vc[TN];
+  uint2 rv[MT][TN];                                     // residual, 4 bf16 per lane
+  const bf16* prow = pr + (int64_t)m0 * ldr + offr;     // residual rows of this panel
+  auto load_epi = [&](int nt) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int n = min(nt * PANEL_BN + wid * 32 + tn * 16 + (lane >> 4) * 4, g.N - 4);
+      vs[tn] = *reinterpret_cast<const f4*>(ps + n);
+      vt[tn] = *reinterpret_cast<const f4*>(pt + n);
+      vb[tn] = *reinterpret_cast<const f4*>(pb + n);
+      vc[tn] = *reinterpret_cast<const f4*>(pc + n);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int r = min(mt * 16 + (lane & 15), mlast);
+        rv[mt][tn] = *reinterpret_cast<const uint2*>(prow + r * ldr + n);
+      }
+    }
+  };
+  if (nt_beg < nt_end) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) load_w(nt_beg, ks);
+    load_epi(nt_beg);
+  }
+  __syncthreads();
+
+  // ---- LayerNorm statistics of the panel rows (shifted sums, TPR threads per row) ----
+  if (g.ln) {
+    const int lr = tid / TPR, lh = tid % TPR;
+    const bf16* row = reinterpret_cast<const bf16*>(sX + lr * XROWB);
+    const float sh = to_f(row[0]);
+    float ls = 0.f, lq = 0.f;
+    for (int k = lh * 8; k < K; k += TPR * 8) {
+      Vec<bf16> v; v.load(row + k);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { const float d = v.v[i] - sh; ls += d; lq = fmaf(d, d, lq); }
+    }
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) { ls += __shfl_xor(ls, o, 64); lq += __shfl_xor(lq, o, 64); }
+    if (lh == 0) {
+      const float md = ls / K;
+      s_mu[lr] = sh + md;
+      s_rs[lr] = rsqrtf(fmaxf(lq / K - md * md, 0.f) + 1e-5f);
+    }
+    __syncthreads();
+  }
+
+  bf16* orow = reinterpret_cast<bf16*>(g.out) + (int64_t)m0 * g.ldo + g.offo;
+  const int ldo = (int)g.ldo;
+  for (int nt = nt_beg; nt < nt_end; ++nt) {
+    const bool more = nt + 1 < nt_end;
+    const int nw = nt * PANEL_BN + wid * 32;          // wave's first channel (wave-uniform)
+    f32x4 acc[MT][TN];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) acc[mt][tn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (nw < g.N) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks * 32 < K) {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const bf16x8 xf = *reinterpret_cast<const bf16x8*>(sX + (mt * 16 + (lane & 15)) * XROWB + ks * 64 + (lane >> 4) * 16);
+#pragma unroll
+            for (int tn = 0; tn < TN; ++tn) acc[mt][tn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[tn][ks], xf, acc[mt][tn], 0, 0, 0);
+          }
+        }
+        if (more) load_w(nt + 1, ks);                  // refill behind this K step's MFMAs
+      }
+    } else if (more) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) load_w(nt + 1, ks);
+    }
+    // epilogue of tile nt (vectors / residual fetched a whole tile ago; refetched after it)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      int r = mt * 16 + (lane & 15);
+      asm volatile("" : "+v"(r));   // per-tile reload of the row statistics (not hoisted: VGPRs)
+      const float mu = g.ln ? s_mu[r] : 0.f, rs = g.ln ? s_rs[r] : 1.f;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        const int n = nw + tn * 16 + (lane >> 4) * 4;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = acc[mt][tn][e];
+          if (g.ln) x = rs * (x - mu * vs[tn][e]) + vt[tn][e];
+          x += vb[tn][e];
+          if (g.gelu) x = gelu_erf(x);
+          const uint32_t rw = e < 2 ? rv[mt][tn].x : rv[mt][tn].y;
+          v[e] = x * vc[tn][e] + __uint_as_float((e & 1) ? (rw & 0xffff0000u) : (rw << 16));
+        }
+        if (r <= mlast && n < g.N) {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<bf16x4*>(orow + r * ldo + n) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        }
+      }
+    }
+    if (more) load_epi(nt + 1);
+  }
+}
+
+template <int BM, int KS>
+static void launch_panel(const GemmArgs& g, hipStream_t st) {
+  const int64_t np = g.wstride ? (g.M / g.HW) * ((g.HW + BM - 1) / BM) : (g.M + BM - 1) / BM;
+  const int ntiles = (g.N + PANEL_BN - 1) / PANEL_BN;
+  // split the channel tiles so the grid reaches ~4 blocks per CU
+  int nsplit = (int)std::min<int64_t>(ntiles, std::max<int64_t>(1, (1024 + np - 1) / np));
+  hipLaunchKernelGGL((gemm_panel_kernel<BM, KS>), dim3((unsigned)(np * nsplit)), dim3(256), 0, st, g, nsplit);
+}
+
+// the panel kernel applies to bf16 plain stores with K <= 512 (one LDS panel)
+static bool panel_ok(const GemmArgs& g) {
+  static const bool off = getenv("TURTLE_NO_PANEL") != nullptr;
+  // 32-bit in-panel offsets: rows x leading dimension must stay below 2^31 elements
+  const int64_t big = (int64_t)1 << 30;
+  return !off && !g.conv3 && g.store_mode == STORE_NHWC && g.N % 16 == 0 && g.a.Ktot % 8 == 0 && g.a.Ktot >= 8 &&
+         g.a.Ktot <= 512 && g.ldw % 8 == 0 && (g.res == nullptr || (g.ldr % 4 == 0 && g.offr % 4 == 0)) &&
+         g.ldo % 4 == 0 && g.offo % 4 == 0 && (int64_t)g.N * g.ldw < big && 128 * g.ldo < big && 128 * g.ldr < big &&
+         g.zeros && g.ones && g.N <= 8192;
+}
+static void launch_panel_any(const GemmArgs& g, hipStream_t st) {
+  const int K = g.a.Ktot;
+  if (K <= 64) launch_panel<128, 2>(g, st);
+  else if (K <= 128) launch_panel<128, 4>(g, st);
+  else if (K <= 192) launch_panel<128, 6>(g, st);
+  else if (K <= 256) launch_panel<128, 8>(g, st);
+  else if (K <= 384) launch_panel<64, 12>(g, st);
+  else launch_panel<64, 16>(g, st);
 }
 
 template <typename T, int BM, int BN>
@@ -308,6 +556,9 @@ static void launch_cfg(const GemmArgs& g, hipStream_t st) {
 
 template <typename T>
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    if (panel_ok(g)) { launch_panel_any(g, st); return; }
+  }
   // BN = 128 when it tiles N exactly (or N is large), else 64 (N = 64, 192, 320, tiny widths)
   const bool wide = g.N >= 128 && (g.N % 128 == 0 || g.N > 1024);
   if (wide) launch_cfg<T, 128, 128>(g, st);

@@ -28,6 +28,8 @@ struct GemmArgs {
   int64_t ldo;
   int offo;
   int store_mode;
+  const float* zeros;              // >= 16384 zero floats / 8192 ones (absent vectors, residual)
+  const float* ones;
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
 
@@ -91,15 +93,17 @@ template <typename T> void launch_gram(const GramArgs& a, hipStream_t st);
 
 struct AttnFinArgs {
   const float* part; int nchunk;
+  int nsplit;                      // first-level reduction splits (attn_nsplit(nchunk))
   int B, heads, ch, nseg;
   unsigned norm_mask;              // bit s: segment s is L2-normalised over HW
   const float* tau;                // [heads]
-  float* red;                      // scratch [B*heads][ch*ncol + ch + ncol]
+  float* red;                      // scratch [B*heads][nsplit][ch*ncol + ch + ncol]
   float* attn;                     // [B*heads][ch][ncol]
   float* kinv;                     // [B][heads*ch] 1/max(|k_cur|,eps) of segment `cur_seg`, or null
   int cur_seg;
 };
 void launch_attn_finalize(const AttnFinArgs& a, hipStream_t st);
+int attn_nsplit(int nchunk);
 
 struct WeffArgs {                  // W_eff[b][o][col] = sum_i Wp[o][h*ch+i] * A[b][h][i][seg*ch+j]
   const float* attn; const float* wp;   // wp fp32 [C][C]
@@ -142,6 +146,26 @@ struct EndArgs {                   // ending 3x3 Cin->Cimg + bias + current fram
   float* out;                      // [B][Cimg][Hout][Wout]
 };
 template <typename T> void launch_ending(const EndArgs& a, hipStream_t st);
+
+enum FusedMode { F_DWONLY = 0, F_GELU = 1, F_GATE = 2 };
+struct FusedDst {                  // F_DWONLY output for channels [cbeg, cend)
+  void* p; int64_t ld; int off; int cbeg, cend, ccount; int tok_ws; int64_t tok_stride;
+};
+struct FusedArgs {                 // fused.hip: [LN ->] pw -> dw3x3 -> [act -> pw (+res)]
+  const void* x; int64_t ldx; int offx; int C;
+  int nimg, H, W;
+  const void* w1; int N1;          // [N1][C]
+  int ln; const float* ln_s; const float* ln_t; const float* b1;
+  const float* dww; const float* dwb;   // [9][N1], [N1]
+  int hidden;                      // F_GATE: N1/2, else N1
+  int mode;
+  const void* w2; int N2;          // [N2][hidden], N2 <= 128
+  const float* b2; const float* scale2;
+  const void* res; int64_t ldr; int offr;
+  void* out; int64_t ldo; int offo;
+  FusedDst dst[3]; int ndst;
+};
+template <typename T> void launch_fused(const FusedArgs& a, hipStream_t st);
 
 void launch_cast_f32(const float* src, void* dst, int64_t n, int to_bf16, hipStream_t st);
 

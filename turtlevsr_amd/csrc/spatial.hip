@@ -62,11 +62,20 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
     q1[tap] = ld16(ok ? reinterpret_cast<const void*>(p) : g_zero_dw);
     if constexpr (MODE == DW_GATE) q2[tap] = ld16(ok ? reinterpret_cast<const void*>(p + a.C) : g_zero_dw);
   }
+  // bias: unconditional vector loads (a per-element "bias ? load : 0" would serialise them)
   float acc1[VEC], acc2[VEC];
+  {
+    const float* zb = reinterpret_cast<const float*>(g_zero_dw);
+    const float* b1 = a.bias ? a.bias + c0 : zb;
+    const float* b2 = (MODE == DW_GATE && a.bias) ? a.bias + a.C + c0 : zb;
 #pragma unroll
-  for (int i = 0; i < VEC; ++i) {
-    acc1[i] = a.bias ? a.bias[c0 + i] : 0.f;
-    acc2[i] = (MODE == DW_GATE && a.bias) ? a.bias[a.C + c0 + i] : 0.f;
+    for (int i0 = 0; i0 < VEC; i0 += 4) {
+      const uint4 u1 = ld16(b1 + i0), u2 = ld16(b2 + i0);
+      acc1[i0] = __uint_as_float(u1.x); acc1[i0 + 1] = __uint_as_float(u1.y);
+      acc1[i0 + 2] = __uint_as_float(u1.z); acc1[i0 + 3] = __uint_as_float(u1.w);
+      acc2[i0] = __uint_as_float(u2.x); acc2[i0 + 1] = __uint_as_float(u2.y);
+      acc2[i0 + 2] = __uint_as_float(u2.z); acc2[i0 + 3] = __uint_as_float(u2.w);
+    }
   }
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
@@ -180,72 +189,96 @@ void launch_window(const WinArgs& a, hipStream_t st) {
 // input_projection: zero-padded (or SR bilinear x4 then padded) frame -> 3x3 conv -> pixel-major
 // ------------------------------------------------------------------------------------------
 TURTLE_DEV float frame_px(const StemArgs& a, int b, int f, int c, int y, int x) {
-  // value of channel c of frame f at padded working coordinate (y, x); 0 outside the image
+  // value of channel c of frame f at padded working coordinate (y, x); 0 outside the image.
+  // Branch-free: coordinates are clamped so every load is in bounds and issued unconditionally.
   const float* base = a.inp + (int64_t)b * a.in_bstride + (int64_t)f * a.in_fstride + (int64_t)c * a.Hin * a.Win;
   if (!a.sr) {
-    if (y < 0 || y >= a.Hin || x < 0 || x >= a.Win) return 0.f;
-    return base[(int64_t)y * a.Win + x];
+    const bool in = y >= 0 && y < a.Hin && x >= 0 && x < a.Win;
+    const int yc = min(max(y, 0), a.Hin - 1), xc = min(max(x, 0), a.Win - 1);
+    const float v = base[(int64_t)yc * a.Win + xc];
+    return in ? v : 0.f;
   }
   // TurtleSuper_t1: nn.Upsample(scale_factor=4, bilinear, align_corners=False), then zero pad
-  if (y < 0 || y >= 4 * a.Hin || x < 0 || x >= 4 * a.Win) return 0.f;
-  float sy = fmaxf(0.25f * (y + 0.5f) - 0.5f, 0.f), sx = fmaxf(0.25f * (x + 0.5f) - 0.5f, 0.f);
-  int y0 = (int)sy, x0 = (int)sx;
-  int y1 = y0 < a.Hin - 1 ? y0 + 1 : y0, x1 = x0 < a.Win - 1 ? x0 + 1 : x0;
-  float ly = sy - y0, lx = sx - x0;
-  float v00 = base[(int64_t)y0 * a.Win + x0], v01 = base[(int64_t)y0 * a.Win + x1];
-  float v10 = base[(int64_t)y1 * a.Win + x0], v11 = base[(int64_t)y1 * a.Win + x1];
-  return (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+  const bool in = y >= 0 && y < 4 * a.Hin && x >= 0 && x < 4 * a.Win;
+  const float sy = fmaxf(0.25f * (y + 0.5f) - 0.5f, 0.f), sx = fmaxf(0.25f * (x + 0.5f) - 0.5f, 0.f);
+  const int y0 = min((int)sy, a.Hin - 1), x0 = min((int)sx, a.Win - 1);
+  const int y1 = y0 < a.Hin - 1 ? y0 + 1 : y0, x1 = x0 < a.Win - 1 ? x0 + 1 : x0;
+  const float ly = sy - y0, lx = sx - x0;
+  const float v00 = base[(int64_t)y0 * a.Win + x0], v01 = base[(int64_t)y0 * a.Win + x1];
+  const float v10 = base[(int64_t)y1 * a.Win + x0], v11 = base[(int64_t)y1 * a.Win + x1];
+  const float v = (1.f - ly) * ((1.f - lx) * v00 + lx * v01) + ly * ((1.f - lx) * v10 + lx * v11);
+  return in ? v : 0.f;
 }
 
-template <typename T>
+// 16x16 output pixels per block: the (18x18 x CIN) input patch is staged in LDS once, each thread
+// keeps its 9*CIN taps in registers and sweeps the output channels 8 at a time; the weights are
+// block-uniform (scalar loads), so the inner loop is pure v_fma with SGPR operands.
+constexpr int ST_T = 16;
+template <typename T, int CIN>
 __global__ __launch_bounds__(256) void stem_kernel(StemArgs a) {
-  // one thread per (pixel, 8 output channels)
-  const int CG = (a.Cout + 7) / 8;
-  const int64_t total = (int64_t)a.B * a.Hp * a.Wp * CG;
-  const int cin = a.use_both ? 2 * a.Cimg : a.Cimg;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int cg = (int)(idx % CG);
-    const int64_t pix = idx / CG;
-    const int x = (int)(pix % a.Wp);
-    const int y = (int)((pix / a.Wp) % a.Hp);
-    const int b = (int)(pix / ((int64_t)a.Wp * a.Hp));
+  __shared__ float sIn[CIN][ST_T + 2][ST_T + 2];
+  const int tid = threadIdx.x;
+  const int tx_n = (a.Wp + ST_T - 1) / ST_T;
+  const int x0 = (blockIdx.x % tx_n) * ST_T, y0 = (blockIdx.x / tx_n) * ST_T, b = blockIdx.y;
+  for (int v = tid; v < CIN * (ST_T + 2) * (ST_T + 2); v += 256) {
+    const int ci = v / ((ST_T + 2) * (ST_T + 2)), r = v % ((ST_T + 2) * (ST_T + 2));
+    const int yy = y0 - 1 + r / (ST_T + 2), xx = x0 - 1 + r % (ST_T + 2);
+    const int f = a.use_both ? (ci < a.Cimg ? 0 : 1) : 1;
+    const int c = a.use_both ? ci % a.Cimg : ci;
+    // the conv's own zero padding sits at the padded-frame border
+    const bool inpad = yy >= 0 && yy < a.Hp && xx >= 0 && xx < a.Wp;
+    const float val = frame_px(a, b, f, c, yy, xx);
+    sIn[ci][r / (ST_T + 2)][r % (ST_T + 2)] = inpad ? val : 0.f;
+  }
+  __syncthreads();
+  const int ty = tid / ST_T, tx = tid % ST_T, y = y0 + ty, x = x0 + tx;
+  float in[CIN * 9];
+#pragma unroll
+  for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) in[ci * 9 + t] = sIn[ci][ty + t / 3][tx + t % 3];
+  if (y >= a.Hp || x >= a.Wp) return;
+  T* o = reinterpret_cast<T*>(a.out) + (((int64_t)b * a.Hp + y) * a.Wp + x) * a.Cout;
+  for (int co = 0; co < a.Cout; co += 8) {
     float acc[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = (a.bias && cg * 8 + i < a.Cout) ? a.bias[cg * 8 + i] : 0.f;
-    for (int ci = 0; ci < cin; ++ci) {
-      const int f = a.use_both ? (ci < a.Cimg ? 0 : 1) : 1;
-      const int c = a.use_both ? ci % a.Cimg : ci;
+    for (int i = 0; i < 8; ++i) acc[i] = a.bias ? a.bias[co + i] : 0.f;
 #pragma unroll
-      for (int dy = -1; dy <= 1; ++dy)
+    for (int k = 0; k < CIN * 9; ++k)
 #pragma unroll
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int yy = y + dy, xx = x + dx;
-          // the conv's own zero padding is at the padded-frame border
-          float v = (yy < 0 || yy >= a.Hp || xx < 0 || xx >= a.Wp) ? 0.f : frame_px(a, b, f, c, yy, xx);
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(a.w[(co + i) * CIN * 9 + k], in[k], acc[i]);
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int co = cg * 8 + i;
-            if (co < a.Cout) acc[i] = fmaf(a.w[((co * cin + ci) * 3 + dy + 1) * 3 + dx + 1], v, acc[i]);
-          }
-        }
+    for (int i0 = 0; i0 < 8; i0 += Vec<T>::N) {
+      Vec<T> ov;
+#pragma unroll
+      for (int i = 0; i < Vec<T>::N; ++i) ov.v[i] = acc[i0 + i];
+      ov.store(o + co + i0);
     }
-    T* o = reinterpret_cast<T*>(a.out) + pix * a.Cout + cg * 8;
-    for (int i = 0; i < 8 && cg * 8 + i < a.Cout; ++i) o[i] = from_f<T>(acc[i]);
   }
 }
 
 template <typename T>
 void launch_stem(const StemArgs& a, hipStream_t st) {
-  const int64_t total = (int64_t)a.B * a.Hp * a.Wp * ((a.Cout + 7) / 8);
-  int64_t blocks = (total + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(stem_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  const int cin = a.use_both ? 2 * a.Cimg : a.Cimg;
+  const dim3 grid((unsigned)(((a.Wp + ST_T - 1) / ST_T) * ((a.Hp + ST_T - 1) / ST_T)), (unsigned)a.B);
+  switch (cin) {
+    case 1: hipLaunchKernelGGL((stem_kernel<T, 1>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((stem_kernel<T, 2>), grid, dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((stem_kernel<T, 3>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((stem_kernel<T, 4>), grid, dim3(256), 0, st, a); break;
+    case 6: hipLaunchKernelGGL((stem_kernel<T, 6>), grid, dim3(256), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((stem_kernel<T, 8>), grid, dim3(256), 0, st, a); break;
+    default: break;   // n_colors is 1..4 (turtle.cpp)
+  }
 }
 
 // ------------------------------------------------------------------------------------------
 // ending: 3x3 Cin->Cimg (+bias) + current padded frame, cropped to the output size
 // ------------------------------------------------------------------------------------------
-template <typename T>
+// one thread per output pixel; every tap row is fetched with unconditional 16-byte loads (a zero
+// line for taps outside the padded map), the weights are wave-uniform scalar loads
+__device__ __attribute__((aligned(64))) uint4 g_zero_end[4];
+template <typename T, int CO>
 __global__ __launch_bounds__(256) void ending_kernel(EndArgs a) {
   constexpr int VEC = Vec<T>::N;
   const int64_t total = (int64_t)a.B * a.Hout * a.Wout;
@@ -253,41 +286,55 @@ __global__ __launch_bounds__(256) void ending_kernel(EndArgs a) {
   StemArgs s{};
   s.inp = a.inp; s.in_bstride = a.in_bstride; s.in_fstride = a.in_fstride;
   s.Cimg = a.Cimg; s.Hin = a.Hin; s.Win = a.Win; s.sr = a.sr;
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (int64_t)gridDim.x * 256) {
-    const int x = (int)(idx % a.Wout);
-    const int y = (int)((idx / a.Wout) % a.Hout);
-    const int b = (int)(idx / ((int64_t)a.Wout * a.Hout));
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int yy = y + dy;
-      if (yy < 0 || yy >= a.Hp) continue;
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int xx = x + dx;
-        if (xx < 0 || xx >= a.Wp) continue;
-        const int tap = (dy + 1) * 3 + dx + 1;
-        const T* p = xin + (((int64_t)b * a.Hp + yy) * a.Wp + xx) * a.Cin;
-        for (int c0 = 0; c0 < a.Cin; c0 += VEC) {
-          Vec<T> v; v.load(p + c0);
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = idx < total;
+  const int64_t id = live ? idx : 0;
+  const int x = (int)(id % a.Wout);
+  const int y = (int)((id / a.Wout) % a.Hout);
+  const int b = (int)(id / ((int64_t)a.Wout * a.Hout));
+  float acc[CO];
 #pragma unroll
-          for (int i = 0; i < VEC; ++i)
-            for (int co = 0; co < a.Cimg && co < 4; ++co)
-              acc[co] = fmaf(a.w[((co * a.Cin + c0 + i) * 3 + dy + 1) * 3 + dx + 1], v.v[i], acc[co]);
+  for (int co = 0; co < CO; ++co) acc[co] = a.bias[co];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+    const bool ok = yy >= 0 && yy < a.Hp && xx >= 0 && xx < a.Wp;
+    const T* p = xin + (((int64_t)b * a.Hp + (ok ? yy : 0)) * a.Wp + (ok ? xx : 0)) * a.Cin;
+    for (int c0 = 0; c0 < a.Cin; c0 += 4 * VEC) {
+      uint4 q[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        q[u] = ld16(ok && c0 + u * VEC < a.Cin ? reinterpret_cast<const void*>(p + c0 + u * VEC) : g_zero_end);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        Vec<T> v;
+        v.from_raw(q[u]);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const int c = min(c0 + u * VEC + i, a.Cin - 1);
+#pragma unroll
+          for (int co = 0; co < CO; ++co) acc[co] = fmaf(a.w[(co * a.Cin + c) * 9 + tap], v.v[i], acc[co]);
         }
       }
     }
-    for (int co = 0; co < a.Cimg && co < 4; ++co) {
-      float r = acc[co] + a.bias[co] + frame_px(s, b, 1, co, y, x);
-      a.out[(((int64_t)b * a.Cimg + co) * a.Hout + y) * a.Wout + x] = r;
-    }
   }
+  if (!live) return;
+#pragma unroll
+  for (int co = 0; co < CO; ++co)
+    a.out[(((int64_t)b * a.Cimg + co) * a.Hout + y) * a.Wout + x] = acc[co] + frame_px(s, b, 1, co, y, x);
 }
 
 template <typename T>
 void launch_ending(const EndArgs& a, hipStream_t st) {
   const int64_t total = (int64_t)a.B * a.Hout * a.Wout;
-  int64_t blocks = (total + 255) / 256;
-  if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(ending_kernel<T>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+  switch (a.Cimg) {
+    case 1: hipLaunchKernelGGL((ending_kernel<T, 1>), dim3(blocks), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((ending_kernel<T, 2>), dim3(blocks), dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((ending_kernel<T, 3>), dim3(blocks), dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((ending_kernel<T, 4>), dim3(blocks), dim3(256), 0, st, a); break;
+    default: break;   // n_colors is 1..4 (turtle.cpp)
+  }
 }
 
 // ------------------------------------------------------------------------------------------

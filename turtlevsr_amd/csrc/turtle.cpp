@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <stdexcept>
@@ -201,12 +202,13 @@ struct GemmW { size_t w = NONE, s = NONE, t = NONE, bias = NONE, scale = NONE; i
 struct DwW { size_t w = NONE, bias = NONE; int C = 0; };
 struct BlockW {
   GemmW a_in, a_out, q2, k2, kv, f_in, f_out;
-  DwW a_dw, sab_qk_dw, sab_v_dw, fhr_dw, kv_dw, f_dw;
+  DwW a_dw, sab_qk_dw, sab_v_dw, fhr_dw, kv_dw, f_dw, chm_dw6;
   size_t q2_win = NONE, q2_winb = NONE, k2_win = NONE, k2_winb = NONE, sab_tau = NONE;
   size_t wp = NONE, po_bias = NONE, tau = NONE;   // channel-attention projection (fp32) + temperature
 };
 struct ModelW {
   size_t stem_w = NONE, stem_b = NONE, end_w = NONE, end_b = NONE;
+  size_t zeros = NONE, ones = NONE;          // constant vectors for branch-free kernel operands
   GemmW down[3], up[3], reduce[3];
   std::vector<std::vector<BlockW>> blocks;   // [level][block]
 };
@@ -245,12 +247,13 @@ struct Packer {
   }
 };
 
-struct ProfRec { int cls; hipEvent_t a, b; double bytes, flops; };
+struct ProfRec { int cls; hipEvent_t a, b; double bytes, flops; std::string tag; };
 
 struct TurtleHandle {
   Arch arch;
   int prof_cls = -1;
   std::vector<ProfRec> prof;
+  std::string prof_tag;                               // shape note of the next launch (per-launch dump)
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::map<std::string, std::vector<float>> staged;
@@ -258,6 +261,7 @@ struct TurtleHandle {
   char* dev = nullptr;
   size_t dev_bytes = 0;
   bool loaded = false;
+  bool fuse = getenv("TURTLE_NO_FUSE") == nullptr;   // block-level fused kernels (fused.hip)
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
   const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
   const float* fptr(size_t off) const { return reinterpret_cast<const float*>(ptr(off)); }
@@ -318,6 +322,27 @@ static DwW pack_dw(TurtleHandle* h, Packer& pk, const std::string& n, int c0, in
     const auto& b = W(h, n + ".bias");
     d.bias = pk.f32(std::vector<double>(b.begin() + c0, b.begin() + c0 + C));
   }
+  return d;
+}
+
+// several depthwise 3x3 convs side by side -> one [9][sum C] table (fused multi-output dw)
+static DwW pack_dw_cat(TurtleHandle* h, Packer& pk, const std::vector<std::string>& names, const std::vector<int>& cs) {
+  int Ct = 0;
+  for (int c : cs) Ct += c;
+  std::vector<double> o((size_t)9 * Ct), bias;
+  bool any_bias = false;
+  for (auto& n : names) any_bias |= has(h, n + ".bias");
+  int c0 = 0;
+  for (size_t i = 0; i < names.size(); ++i) {
+    const auto& w = W(h, names[i] + ".weight");
+    for (int c = 0; c < cs[i]; ++c)
+      for (int t = 0; t < 9; ++t) o[(size_t)t * Ct + c0 + c] = w[(size_t)c * 9 + t];
+    if (any_bias)
+      for (int c = 0; c < cs[i]; ++c) bias.push_back(has(h, names[i] + ".bias") ? W(h, names[i] + ".bias")[c] : 0.0);
+    c0 += cs[i];
+  }
+  DwW d; d.C = Ct; d.w = pk.f32(o);
+  if (any_bias) d.bias = pk.f32(bias);
   return d;
 }
 
@@ -391,6 +416,7 @@ static void pack_all(TurtleHandle* h) {
         bw.sab_qk_dw = pack_dw(h, pk, s + ".qk_dwconv", 0, 2 * c);
         bw.sab_v_dw = pack_dw(h, pk, s + ".v_dwconv", 0, c);
         bw.fhr_dw = pack_dw(h, pk, ca + ".qkv_dwconv", 0, 3 * c);
+        bw.chm_dw6 = pack_dw_cat(h, pk, {s + ".qk_dwconv", s + ".v_dwconv", ca + ".qkv_dwconv"}, {2 * c, c, 3 * c});
         bw.q2 = pack_gemm(h, pk, dvec(W(h, s + ".q2.weight")), 2 * c, c, "", opt_bias(h, s + ".q2.bias"));
         bw.k2 = pack_gemm(h, pk, dvec(W(h, s + ".k2.weight")), 2 * c, c, "", opt_bias(h, s + ".k2.bias"));
         const int taps = b.ws * b.ws;
@@ -435,6 +461,8 @@ static void pack_all(TurtleHandle* h) {
     }
     M.blocks.push_back(bws);
   }
+  M.zeros = pk.f32(std::vector<double>(16384, 0.0));
+  M.ones = pk.f32(std::vector<double>(8192, 1.0));
   pk.align();
   if (h->dev) { (void)hipFree(h->dev); h->dev = nullptr; }
   HIPCHK(hipMalloc(&h->dev, pk.host.size()));
@@ -487,12 +515,21 @@ struct Runner {
   void launch(int cls, double bytes, double flops, F&& f) {
     if (dry()) return;
     const bool p = h->prof_cls == TURTLE_K_ALL || h->prof_cls == cls;
-    if (!p) { f(); return; }
-    ProfRec r{cls, event(), event(), bytes, flops};
+    if (!p) { f(); h->prof_tag.clear(); return; }
+    ProfRec r{cls, event(), event(), bytes, flops, std::move(h->prof_tag)};
+    h->prof_tag.clear();
     HIPCHK(hipEventRecord(r.a, st));
     f();
     HIPCHK(hipEventRecord(r.b, st));
     h->prof.push_back(r);
+  }
+  // describe the next launch for the per-launch profile dump (TURTLE_PROF_DUMP)
+  template <typename... A>
+  void tag(const char* fmt, A... args) {
+    if (h->prof_cls < 0) return;
+    char buf[160];
+    snprintf(buf, sizeof buf, fmt, args...);
+    h->prof_tag = buf;
   }
   float* fbuf(int64_t elems) { return reinterpret_cast<float*>(ar.alloc((size_t)elems * 4)); }
   bool dry() const { return ar.dry; }
@@ -514,12 +551,15 @@ struct Runner {
     g.bias = bias ? bias : h->fptr(w.bias); g.scale = h->fptr(w.scale); g.gelu = gelu;
     g.res = res; g.ldr = ldr; g.offr = offr;
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store;
+    g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones);
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
     // algorithmic traffic: A once (a 3x3 reads each input pixel once), W per weight set, out
     // (+ residual) once
     const double Ka = conv3 ? cin : a.Ktot;
     const double nset = wstride ? (double)(M / HW) / wdiv : 1.0;
     const double bytes = ES * ((double)M * Ka + nset * g.N * a.Ktot + (double)M * g.N * (res ? 2 : 1));
+    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d", (long long)M, g.N, a.Ktot, conv3, g.ln,
+        res != nullptr, store, a.n);
     launch(TURTLE_K_GEMM, bytes, 2.0 * M * g.N * a.Ktot, [&] { launch_gemm<T>(g, st); });
   }
   void dw(const DwW& w, const void* in, int64_t ldi, int offi, void* out, int64_t ldo, int offo,
@@ -531,7 +571,39 @@ struct Runner {
     a.nimg = nimg; a.H = H; a.W = Wd; a.C = mode == DW_GATE ? w.C / 2 : w.C; a.mode = mode;
     a.tok_ws = tok_ws; a.tok_img_stride = tok_stride;
     const double px = (double)nimg * H * Wd, cin = mode == DW_GATE ? 2.0 * a.C : a.C;
+    tag("dw nimg=%d H=%d W=%d C=%d mode=%d tok=%d", nimg, H, Wd, a.C, mode, tok_ws);
     launch(TURTLE_K_DW, ES * px * (cin + a.C), 18.0 * px * cin, [&] { launch_dw<T>(a, st); });
+  }
+
+  // [LN ->] pw -> dw3x3 -> [act -> pw (+res)] in one kernel (fused.hip)
+  void fused(int mode, const GemmW& w1, const DwW& dwp, const T* x, int64_t ldx, int offx, int C, int nimg, int H, int Wd,
+             int hidden, const GemmW* w2, const T* res, T* out, const std::vector<FusedDst>& dsts) {
+    if (dry()) return;
+    FusedArgs f{};
+    f.x = x; f.ldx = ldx; f.offx = offx; f.C = C; f.nimg = nimg; f.H = H; f.W = Wd;
+    f.w1 = h->ptr(w1.w); f.N1 = w1.N; f.ln = w1.ln; f.ln_s = h->fptr(w1.s); f.ln_t = h->fptr(w1.t); f.b1 = h->fptr(w1.bias);
+    f.dww = h->fptr(dwp.w); f.dwb = h->fptr(dwp.bias); f.hidden = hidden; f.mode = mode;
+    double px = (double)nimg * H * Wd;
+    double bytes = ES * px * C, flops = 2.0 * px * C * w1.N + 18.0 * px * w1.N;
+    if (w2) {
+      if (w2->N > 128 || w2->N % 16) TFAIL(TURTLE_EINVAL, "fused GEMM2 needs N2 <= 128, N2 % 16 == 0");
+      f.w2 = h->ptr(w2->w); f.N2 = w2->N; f.b2 = h->fptr(w2->bias); f.scale2 = h->fptr(w2->scale);
+      f.res = res; f.ldr = w2->N; f.offr = 0; f.out = out; f.ldo = w2->N; f.offo = 0;
+      bytes += ES * px * w2->N * (res ? 2 : 1);
+      flops += 2.0 * px * hidden * w2->N;
+    } else {
+      if (dsts.empty() || dsts.size() > 3) TFAIL(TURTLE_EINVAL, "fused dw-only needs 1..3 destinations");
+      for (size_t i = 0; i < dsts.size(); ++i) f.dst[i] = dsts[i];
+      f.ndst = (int)dsts.size();
+      bytes += ES * px * w1.N;
+    }
+    if (dwp.C != w1.N) TFAIL(TURTLE_EINVAL, "fused: dw width != pointwise width");
+    if (C > 128) TFAIL(TURTLE_EINVAL, "fused: input width > 128");
+    tag("fused mode=%d nimg=%d H=%d W=%d C=%d N1=%d N2=%d ln=%d ndst=%d", mode, nimg, H, Wd, C, w1.N, f.N2, f.ln, f.ndst);
+    launch(TURTLE_K_FUSED, bytes, flops, [&] { launch_fused<T>(f, st); });
+  }
+  static FusedDst dst_map(void* p, int64_t ld, int off, int cbeg, int cend) {
+    return FusedDst{p, ld, off, cbeg, cend, cend - cbeg, 0, 0};
   }
 
   struct Seg { const void* base; int64_t ld; int off; int hstride; int mul, add; int norm; int64_t col; int colh; };
@@ -540,6 +612,7 @@ struct Runner {
   void chan_attn(const BlockW& bw, const Blk& b, const T* q, int64_t ldq, int qoff, const std::vector<Seg>& segs,
                  const SrcList& vsrc, int HW, int Wimg, T* x, float* kinv, int cur_seg) {
     const int c = b.dim, ch = c / b.heads, nseg = (int)segs.size(), ncol = nseg * ch;
+    if (ncol > 512 || nseg > TURTLE_MAX_SEG) TFAIL(TURTLE_EINVAL, "channel attention: more than 512 key columns");
     // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each
     int nchunk = std::max(1, std::min((HW + 255) / 256, std::max(1, 1024 / (B * b.heads))));
     int chunk = (HW + nchunk - 1) / nchunk;
@@ -547,7 +620,8 @@ struct Runner {
     nchunk = (HW + chunk - 1) / chunk;
     const int stride = ch * ncol + ch + ncol;
     float* part = fbuf((int64_t)B * b.heads * nchunk * stride);
-    float* red = fbuf((int64_t)B * b.heads * stride);
+    const int nsplit = attn_nsplit(nchunk);
+    float* red = fbuf((int64_t)B * b.heads * nsplit * stride);
     float* attn = fbuf((int64_t)B * b.heads * ch * ncol);
     T* weff = buf((int64_t)B * c * vsrc.Ktot);
     if (dry()) return;
@@ -559,16 +633,19 @@ struct Runner {
       if (segs[s].norm) mask |= 1u << s;
     }
     g.B = B; g.heads = b.heads; g.ch = ch; g.HW = HW; g.nchunk = nchunk; g.chunk = chunk; g.part = part;
+    tag("gram B=%d HW=%d c=%d heads=%d nseg=%d nchunk=%d", B, HW, c, b.heads, nseg, nchunk);
     launch(TURTLE_K_ATTN, ES * (double)B * HW * c * (1 + nseg), 2.0 * B * b.heads * ch * ncol * (double)HW,
            [&] { launch_gram<T>(g, st); });
     AttnFinArgs f{};
-    f.part = part; f.nchunk = nchunk; f.B = B; f.heads = b.heads; f.ch = ch; f.nseg = nseg; f.norm_mask = mask;
+    f.part = part; f.nchunk = nchunk; f.nsplit = nsplit; f.B = B; f.heads = b.heads; f.ch = ch; f.nseg = nseg; f.norm_mask = mask;
     f.tau = h->fptr(bw.tau); f.red = red; f.attn = attn; f.kinv = kinv; f.cur_seg = cur_seg;
+    tag("attn_finalize nbh=%d ch=%d ncol=%d nchunk=%d", B * b.heads, ch, ncol, nchunk);
     launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride, 0, [&] { launch_attn_finalize(f, st); });
     WeffArgs we{};
     we.attn = attn; we.wp = h->fptr(bw.wp); we.B = B; we.heads = b.heads; we.ch = ch; we.nseg = nseg; we.C = c;
     for (int s = 0; s < nseg; ++s) { we.seg_col[s] = segs[s].col; we.seg_hstride[s] = segs[s].colh; }
     we.Keff = vsrc.Ktot; we.weff = weff;
+    tag("weff B=%d C=%d heads=%d ncol=%d", B, c, b.heads, ncol);
     launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot, 2.0 * B * c * (double)b.heads * ncol * ch,
            [&] { launch_weff<T>(we, st); });
     GemmW pw; pw.N = c; pw.K = vsrc.Ktot;
@@ -576,21 +653,27 @@ struct Runner {
          h->fptr(bw.po_bias));
   }
 
-  void block(const Blk& b, const BlockW& bw, T* x, int H, int Wd) {
+  // one TurtleAttnBlock (turtle_t1_arch.py:804-811). x / xalt ping-pong: a fused kernel reads its
+  // input with a halo, so it cannot update the residual stream in place.
+  void block(const Blk& b, const BlockW& bw, T*& x, T*& xalt, int H, int Wd) {
     const int c = b.dim, HW = H * Wd;
     const int64_t P = (int64_t)B * HW;
     const size_t mark = ar.off;
+    const bool fz = h->fuse;
     if (b.attn == TURTLE_ATTN_REDUCED) {
-      T* t1 = buf(P * 2 * c);
-      T* t2 = buf(P * 2 * c);
-      gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * c, 0);
-      dw(bw.a_dw, t1, 2 * c, 0, t2, 2 * c, 0, B, H, Wd, DW_GELU);
-      gemm(bw.a_out, src1(t2, 2 * c, 0, 2 * c), P, HW, Wd, x, c, 0, x, c, 0);
+      if (fz && c <= 128) {
+        fused(F_GELU, bw.a_in, bw.a_dw, x, c, 0, c, B, H, Wd, 2 * c, &bw.a_out, x, xalt, {});
+        std::swap(x, xalt);
+      } else {
+        T* t1 = buf(P * 2 * c);
+        T* t2 = buf(P * 2 * c);
+        gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * c, 0);
+        dw(bw.a_dw, t1, 2 * c, 0, t2, 2 * c, 0, B, H, Wd, DW_GELU);
+        gemm(bw.a_out, src1(t2, 2 * c, 0, 2 * c), P, HW, Wd, x, c, 0, x, c, 0);
+      }
     } else if (b.attn == TURTLE_ATTN_CHANNEL || (b.attn == TURTLE_ATTN_FHR && b.cache_slot < 0)) {
-      T* t1 = buf(P * 3 * c);
       T* t2 = buf(P * 3 * c);
-      gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
-      dw(bw.a_dw, t1, 3 * c, 0, t2, 3 * c, 0, B, H, Wd, DW_PLAIN);
+      qkv_dw(bw, x, c, t2, B, H, Wd);
       const int ch = c / b.heads;
       std::vector<Seg> segs{{t2, 3 * c, c, ch, 1, 0, 1, 0, ch}};
       chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t2, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1);
@@ -603,11 +686,16 @@ struct Runner {
     // feed-forward
     if (b.ffn == TURTLE_FFN_GFFW) {
       const int hd = b.hidden;
-      T* t1 = buf(P * 2 * hd);
-      T* t2 = buf(P * hd);
-      gemm(bw.f_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * hd, 0);
-      dw(bw.f_dw, t1, 2 * hd, 0, t2, hd, 0, B, H, Wd, DW_GATE);
-      gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
+      if (fz && c <= 128) {
+        fused(F_GATE, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, &bw.f_out, x, xalt, {});
+        std::swap(x, xalt);
+      } else {
+        T* t1 = buf(P * 2 * hd);
+        T* t2 = buf(P * hd);
+        gemm(bw.f_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * hd, 0);
+        dw(bw.f_dw, t1, 2 * hd, 0, t2, hd, 0, B, H, Wd, DW_GATE);
+        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
+      }
     } else {
       T* t1 = buf(P * 2 * c);
       gemm(bw.f_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * c, 0, nullptr, 0, 0, /*gelu*/ 1);
@@ -616,17 +704,28 @@ struct Runner {
     ar.off = mark;
   }
 
+  // LN(x) -> qkv 1x1 -> qkv_dwconv into `out` [P][3c] (fused, or GEMM + dw)
+  void qkv_dw(const BlockW& bw, const T* x, int c, T* out, int nimg, int H, int Wd) {
+    if (h->fuse && c <= 128) {
+      fused(F_DWONLY, bw.a_in, bw.a_dw, x, c, 0, c, nimg, H, Wd, 3 * c, nullptr, nullptr, nullptr,
+            {dst_map(out, 3 * c, 0, 0, 3 * c)});
+    } else {
+      const int64_t P = (int64_t)nimg * H * Wd;
+      T* t1 = buf(P * 3 * c);
+      gemm(bw.a_in, src1(x, c, 0, c), P, H * Wd, Wd, t1, 3 * c, 0);
+      dw(bw.a_dw, t1, 3 * c, 0, out, 3 * c, 0, nimg, H, Wd, DW_PLAIN);
+    }
+  }
+
   // latent FrameHistoryRouter with cache slot (turtle_t1_arch.py:218-286)
   void fhr(const Blk& b, const BlockW& bw, T* x, int H, int Wd) {
     const int c = b.dim, HW = H * Wd, ch = c / b.heads, slot = b.cache_slot;
     const int64_t P = (int64_t)B * HW;
     const int R = io->t_in[slot];
     const int Rnew = std::min(R + ch, b.ntc * ch);
-    T* t1 = buf(P * 3 * c);
     T* t2 = buf(P * 3 * c);
     float* kinv = fbuf((int64_t)B * c);
-    gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
-    dw(bw.a_dw, t1, 3 * c, 0, t2, 3 * c, 0, B, H, Wd, DW_PLAIN);
+    qkv_dw(bw, x, c, t2, B, H, Wd);
     std::vector<Seg> segs;
     const int Tc = R / ch;
     for (int t = 0; t < Tc; ++t)
@@ -642,9 +741,11 @@ struct Runner {
     FhrCacheArgs fk{};
     fk.old = io->k_in[slot]; fk.R = R; fk.cur = t2; fk.ldc = 3 * c; fk.coff = c; fk.kinv = kinv;
     fk.out = io->k_out[slot]; fk.Rnew = Rnew; fk.B = B; fk.P = HW; fk.heads = b.heads; fk.ch = ch;
+    tag("fhr_cache k B=%d P=%d heads=%d R=%d Rnew=%d", B, HW, b.heads, R, Rnew);
     launch(TURTLE_K_OTHER, ES * (double)B * HW * b.heads * (R + ch + Rnew), 0, [&] { launch_fhr_cache<T>(fk, st); });
     FhrCacheArgs fv = fk;
     fv.old = io->v_in[slot]; fv.coff = 2 * c; fv.kinv = nullptr; fv.out = io->v_out[slot];
+    tag("fhr_cache v B=%d P=%d heads=%d R=%d Rnew=%d", B, HW, b.heads, R, Rnew);
     launch(TURTLE_K_OTHER, ES * (double)B * HW * b.heads * (R + ch + Rnew), 0, [&] { launch_fhr_cache<T>(fv, st); });
   }
 
@@ -662,7 +763,6 @@ struct Runner {
     T* vout = slot >= 0 ? reinterpret_cast<T*>(io->v_out[slot]) : buf((int64_t)B * Tnew * N * D);
     const T* kin = slot >= 0 ? reinterpret_cast<const T*>(io->k_in[slot]) : nullptr;
     const T* vin = slot >= 0 ? reinterpret_cast<const T*>(io->v_in[slot]) : nullptr;
-    T* t6 = buf(P * 6 * c);
     T* qkd = buf(P * 2 * c);
     T* fq = buf(P * 3 * c);
     T* q2f = buf(P * d2);
@@ -671,13 +771,21 @@ struct Runner {
     float* topv = fbuf((int64_t)B * NT * N * 5);
     int* topi = reinterpret_cast<int*>(fbuf((int64_t)B * NT * N * 5));
     T* xs = buf(P * NT * c);
-    T* kv = buf(P * NT * 2 * c);
     T* kvd = buf(P * NT * 2 * c);
-    // LN(x) -> [SAB qk | SAB v | FHR qkv]
-    gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t6, 6 * c, 0);
-    dw(bw.sab_qk_dw, t6, 6 * c, 0, qkd, 2 * c, 0, B, H, Wd, DW_PLAIN);
-    dw(bw.sab_v_dw, t6, 6 * c, 2 * c, vout + (int64_t)(Tnew - 1) * N * D, 0, 0, B, H, Wd, DW_PLAIN, ws, (int64_t)Tnew * N * D);
-    dw(bw.fhr_dw, t6, 6 * c, 3 * c, fq, 3 * c, 0, B, H, Wd, DW_PLAIN);
+    // LN(x) -> [SAB qk | SAB v | FHR qkv] -> their depthwise convs; SAB v goes straight into the new
+    // cache's current frame in the dilated token-major layout
+    T* vcur = vout + (int64_t)(Tnew - 1) * N * D;
+    if (h->fuse && c <= 128) {
+      FusedDst dv{vcur, 0, 0, 2 * c, 3 * c, c, ws, (int64_t)Tnew * N * D};
+      fused(F_DWONLY, bw.a_in, bw.chm_dw6, x, c, 0, c, B, H, Wd, 6 * c, nullptr, nullptr, nullptr,
+            {dst_map(qkd, 2 * c, 0, 0, 2 * c), dv, dst_map(fq, 3 * c, 0, 3 * c, 6 * c)});
+    } else {
+      T* t6 = buf(P * 6 * c);
+      gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t6, 6 * c, 0);
+      dw(bw.sab_qk_dw, t6, 6 * c, 0, qkd, 2 * c, 0, B, H, Wd, DW_PLAIN);
+      dw(bw.sab_v_dw, t6, 6 * c, 2 * c, vcur, 0, 0, B, H, Wd, DW_PLAIN, ws, (int64_t)Tnew * N * D);
+      dw(bw.fhr_dw, t6, 6 * c, 3 * c, fq, 3 * c, 0, B, H, Wd, DW_PLAIN);
+    }
     gemm(bw.q2, src1(qkd, 2 * c, 0, c), P, HW, Wd, q2f, d2, 0);
     gemm(bw.k2, src1(qkd, 2 * c, c, c), P, HW, Wd, k2f, d2, 0);
     if (!dry()) {
@@ -692,6 +800,7 @@ struct Runner {
       // keep the last Tnew-1 cached frames in the new cache (reference: cat then [-ntc:])
       if (Tnew > 1) {
         const int keep = Tnew - 1, first = Tin - keep;
+        tag("sab_cache_shift keep=%d N=%d", keep, N);
         launch(TURTLE_K_OTHER, 2.0 * ES * B * keep * (double)N * (d2 + D), 0, [&] {
           HIPCHK(hipMemcpy2DAsync(kout, (size_t)Tnew * N * d2 * ES, kin + (int64_t)first * N * d2, (size_t)Tin * N * d2 * ES,
                                   (size_t)keep * N * d2 * ES, B, hipMemcpyDeviceToDevice, st));
@@ -723,8 +832,14 @@ struct Runner {
              2.0 * B * NT * (double)N * 46 * D, [&] { launch_sab_av<T>(va, st); });
     }
     // kv = (W_kv W_po) xs over the B*T aligned frames, then dw3x3 per frame
-    gemm(bw.kv, src1(xs, c, 0, c), P * NT, HW, Wd, kv, 2 * c, 0);
-    dw(bw.kv_dw, kv, 2 * c, 0, kvd, 2 * c, 0, B * NT, H, Wd, DW_PLAIN);
+    if (h->fuse && c <= 128) {
+      fused(F_DWONLY, bw.kv, bw.kv_dw, xs, c, 0, c, B * NT, H, Wd, 2 * c, nullptr, nullptr, nullptr,
+            {dst_map(kvd, 2 * c, 0, 0, 2 * c)});
+    } else {
+      T* kv = buf(P * NT * 2 * c);
+      gemm(bw.kv, src1(xs, c, 0, c), P * NT, HW, Wd, kv, 2 * c, 0);
+      dw(bw.kv_dw, kv, 2 * c, 0, kvd, 2 * c, 0, B * NT, H, Wd, DW_PLAIN);
+    }
     // FHR(x, k_hist, v_hist): keys = [hist frames..., current]
     std::vector<Seg> segs;
     SrcList vs{};
@@ -739,11 +854,13 @@ struct Runner {
     chan_attn(bw, b, fq, 3 * c, 0, segs, vs, HW, Wd, x, nullptr, -1);
   }
 
-  void level(int li, T* x, int H, int Wd) {
+  // runs a level on the pair (x, alt); returns the buffer holding the level's output
+  T* level(int li, T* x, T* alt, int H, int Wd) {
     const auto& L = h->arch.levels[li];
     static const BlockW none{};   // workspace sizing runs before (or without) packed weights
     for (size_t i = 0; i < L.blocks.size(); ++i)
-      block(L.blocks[i], dry() && h->mw.blocks.empty() ? none : h->mw.blocks[li][i], x, H, Wd);
+      block(L.blocks[i], dry() && h->mw.blocks.empty() ? none : h->mw.blocks[li][i], x, alt, H, Wd);
+    return x;
   }
 
   void run(const float* inp, int Hin, int Win, float* out, int Hout, int Wout) {
@@ -758,27 +875,35 @@ struct Runner {
     T* d2 = buf(P1 / 4 * 2 * d);
     T* d1 = buf(P1 * d);
     T* up = buf(P1 * d);      // Upsample output, largest at level 1: P1 * d/2... sized generously
+    // ping-pong partners of the residual streams (fused blocks write out of place)
+    T* a1 = buf(P1 * d);
+    T* a2 = buf(P1 / 4 * 2 * d);
+    T* a3 = buf(P1 / 16 * 4 * d);
+    T* a4 = buf(P1 / 64 * 8 * d);
+    T* a5 = buf(P1 / 16 * 4 * d);
+    T* a6 = buf(P1 / 4 * 2 * d);
     if (!dry()) {
       StemArgs s{};
       s.inp = inp; s.in_bstride = (int64_t)2 * A.cfg.n_colors * Hin * Win; s.in_fstride = (int64_t)A.cfg.n_colors * Hin * Win;
       s.B = B; s.Cimg = A.cfg.n_colors; s.Hin = Hin; s.Win = Win; s.Hp = Hp; s.Wp = Wp;
       s.use_both = A.cfg.use_both_input; s.sr = A.cfg.super_resolution;
       s.w = h->fptr(h->mw.stem_w); s.bias = h->fptr(h->mw.stem_b); s.Cout = d; s.out = e1;
+      tag("stem %dx%d", Hp, Wp);
       launch(TURTLE_K_OTHER, 4.0 * B * A.in_ch * Hin * Win + ES * (double)P1 * d, 18.0 * P1 * d * A.in_ch,
              [&] { launch_stem<T>(s, st); });
     }
     int H = Hp, Wd = Wp;
-    level(0, e1, H, Wd);
+    e1 = level(0, e1, a1, H, Wd);
     auto down = [&](int i, const T* x, int c, T* y, int H0, int W0) {
       gemm(h->mw.down[i], src1(x, c, 0, 9 * c), (int64_t)B * H0 * W0, H0 * W0, W0, y, 2 * c, 0, nullptr, 0, 0, 0,
            STORE_UNSHUFFLE, nullptr, 0, 1, -1, nullptr, 1, c);
     };
     down(0, e1, d, e2, Hp, Wp);
-    level(1, e2, Hp / 2, Wp / 2);
+    e2 = level(1, e2, a2, Hp / 2, Wp / 2);
     down(1, e2, 2 * d, e3, Hp / 2, Wp / 2);
-    level(2, e3, Hp / 4, Wp / 4);
+    e3 = level(2, e3, a3, Hp / 4, Wp / 4);
     down(2, e3, 4 * d, lat, Hp / 4, Wp / 4);
-    level(3, lat, Hp / 8, Wp / 8);
+    lat = level(3, lat, a4, Hp / 8, Wp / 8);
     auto upcat = [&](int i, const T* x, int c, int H0, int W0, const T* skip, T* y) {
       // Upsample (3x3 c->2c + PixelShuffle) into `up`, then reduce_chan over [up | skip]
       gemm(h->mw.up[i], src1(x, c, 0, 9 * c), (int64_t)B * H0 * W0, H0 * W0, W0, up, c / 2, 0, nullptr, 0, 0, 0,
@@ -790,18 +915,21 @@ struct Runner {
       gemm(h->mw.reduce[i], s, (int64_t)B * H1 * W1, H1 * W1, W1, y, c / 2, 0);
     };
     upcat(0, lat, 8 * d, Hp / 8, Wp / 8, e3, d3);
-    level(4, d3, Hp / 4, Wp / 4);
+    d3 = level(4, d3, a5, Hp / 4, Wp / 4);
     upcat(1, d3, 4 * d, Hp / 4, Wp / 4, e2, d2);
-    level(5, d2, Hp / 2, Wp / 2);
+    d2 = level(5, d2, a6, Hp / 2, Wp / 2);
     upcat(2, d2, 2 * d, Hp / 2, Wp / 2, e1, d1);
-    level(6, d1, Hp, Wp);
-    level(7, d1, Hp, Wp);
+    // decoder_level1 + refinement ping-pong with a1 (the encoder-1 partner; e1 itself is consumed)
+    T* d1alt = e1 == a1 ? up : a1;
+    d1 = level(6, d1, d1alt, Hp, Wp);
+    d1 = level(7, d1, d1 == d1alt ? (d1alt == up ? a1 : up) : d1alt, Hp, Wp);
     if (!dry()) {
       EndArgs e{};
       e.x = d1; e.Cin = d; e.w = h->fptr(h->mw.end_w); e.bias = h->fptr(h->mw.end_b);
       e.inp = inp; e.in_bstride = (int64_t)2 * A.cfg.n_colors * Hin * Win; e.in_fstride = (int64_t)A.cfg.n_colors * Hin * Win;
       e.B = B; e.Cimg = A.cfg.n_colors; e.Hin = Hin; e.Win = Win; e.Hp = Hp; e.Wp = Wp; e.Hout = Hout; e.Wout = Wout;
       e.sr = A.cfg.super_resolution; e.out = out;
+      tag("ending %dx%d", Hout, Wout);
       launch(TURTLE_K_OTHER, ES * (double)P1 * d + 8.0 * B * A.out_ch * Hout * Wout, 18.0 * P1 * d * A.out_ch,
              [&] { launch_ending<T>(e, st); });
     }
@@ -862,16 +990,20 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]) {
   return guard([&] {
     if (!h || !out) TFAIL(TURTLE_EINVAL, "null argument");
     for (int i = 0; i < 4 * TURTLE_K_COUNT; ++i) out[i] = 0;
+    const char* dump = getenv("TURTLE_PROF_DUMP");   // per-launch lines: class ms bytes flops tag
+    FILE* df = dump ? fopen(dump, "a") : nullptr;
     for (auto& r : h->prof) {
       HIPCHK(hipEventSynchronize(r.b));
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, r.a, r.b));
+      if (df) fprintf(df, "%d\t%.4f\t%.0f\t%.0f\t%s\n", r.cls, ms, r.bytes, r.flops, r.tag.c_str());
       if (r.cls < 0 || r.cls >= TURTLE_K_COUNT) continue;
       out[4 * r.cls] += ms;
       out[4 * r.cls + 1] += 1;
       out[4 * r.cls + 2] += r.bytes;
       out[4 * r.cls + 3] += r.flops;
     }
+    if (df) fclose(df);
     h->prof.clear();
     h->ev_used = 0;
     h->prof_cls = -1;
