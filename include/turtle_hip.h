@@ -118,6 +118,14 @@ int turtle_forward(TurtleHandle* h, const float* inp, int B, int H, int W, float
 int turtle_profile_begin(TurtleHandle* h, int kernel_class);
 int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
 
+/* Kernel-selection switches (performance A/B only; every setting computes the same function).
+ *   "fuse"        1 (default): block-level fused pointwise->depthwise->pointwise kernels where
+ *                 the input width is <= 128; 0: separate GEMM + depthwise launches
+ *   "panel_gemm"  1 (default): panel GEMM for bf16 plain 1x1 convolutions with K <= 512;
+ *                 0: K-loop GEMM everywhere
+ * Unknown names return TURTLE_EINVAL. */
+int turtle_set_option(TurtleHandle* h, const char* name, int value);
+
 const char* turtle_last_error(void);
 
 #ifdef __cplusplus

@@ -90,3 +90,35 @@ def test_fp32_vs_oracle_256():
     ref, _ = R.run_clip(sd, meta["opt"], torch.from_numpy(clip))
     for o, r in zip(outs, ref):
         assert psnr(o.numpy(), r.numpy()) >= 80.0
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_kernel_variants_agree(dtype):
+    """The kernel-selection switches (fused block kernels, panel GEMM) compute the same function:
+    GoPro widths at 128x128, 3 frames, every switch setting against the reference golden clip's
+    arch/weights. fp32: variants agree to 2e-4; bf16: each variant >= 45 dB vs the fp32 build and
+    the variants within 50 dB of each other."""
+    from turtlevsr_amd.synthetic import synthetic_frames
+    _, meta = load("clip_gopro_64")
+    clip = synthetic_frames((1, 3, 3, 128, 128), 11)
+    ref = _run(_model(meta, "fp32").set_option("fuse", 0).set_option("panel_gemm", 0), clip)[0]
+    outs = {}
+    for fuse in (0, 1):
+        for panel in (0, 1):
+            m = _model(meta, dtype).set_option("fuse", fuse).set_option("panel_gemm", panel)
+            outs[(fuse, panel)] = _run(m, clip)[0]
+    for key, o in outs.items():
+        for j, (a, r) in enumerate(zip(o, ref)):
+            if dtype == "fp32":
+                err = float((a - r).abs().max())
+                assert err <= 2e-4, (key, j, err)
+            else:
+                assert psnr(a.numpy(), r.numpy()) >= 45.0, (key, j)
+                assert psnr(a.numpy(), outs[(0, 0)][j].numpy()) >= 50.0, (key, j)
+
+
+def test_set_option_rejects_unknown():
+    _, meta = load("clip_tiny_64")
+    m = _model(meta, "fp32")
+    with pytest.raises(RuntimeError):
+        m.set_option("no_such_switch", 1)

@@ -529,10 +529,9 @@ static void launch_panel(const GemmArgs& g, hipStream_t st) {
 
 // the panel kernel applies to bf16 plain stores with K <= 512 (one LDS panel)
 static bool panel_ok(const GemmArgs& g) {
-  static const bool off = getenv("TURTLE_NO_PANEL") != nullptr;
   // 32-bit in-panel offsets: rows x leading dimension must stay below 2^31 elements
   const int64_t big = (int64_t)1 << 30;
-  return !off && !g.conv3 && g.store_mode == STORE_NHWC && g.N % 16 == 0 && g.a.Ktot % 8 == 0 && g.a.Ktot >= 8 &&
+  return g.allow_panel && !g.conv3 && g.store_mode == STORE_NHWC && g.N % 16 == 0 && g.a.Ktot % 8 == 0 && g.a.Ktot >= 8 &&
          g.a.Ktot <= 512 && g.ldw % 8 == 0 && (g.res == nullptr || (g.ldr % 4 == 0 && g.offr % 4 == 0)) &&
          g.ldo % 4 == 0 && g.offo % 4 == 0 && (int64_t)g.N * g.ldw < big && 128 * g.ldo < big && 128 * g.ldr < big &&
          g.zeros && g.ones && g.N <= 8192;

@@ -30,6 +30,7 @@ struct GemmArgs {
   int store_mode;
   const float* zeros;              // >= 16384 zero floats / 8192 ones (absent vectors, residual)
   const float* ones;
+  int allow_panel;                 // panel kernel permitted (turtle_set_option "panel_gemm")
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
 

@@ -262,6 +262,7 @@ struct TurtleHandle {
   size_t dev_bytes = 0;
   bool loaded = false;
   bool fuse = getenv("TURTLE_NO_FUSE") == nullptr;   // block-level fused kernels (fused.hip)
+  bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
   const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
   const float* fptr(size_t off) const { return reinterpret_cast<const float*>(ptr(off)); }
@@ -551,7 +552,7 @@ struct Runner {
     g.bias = bias ? bias : h->fptr(w.bias); g.scale = h->fptr(w.scale); g.gelu = gelu;
     g.res = res; g.ldr = ldr; g.offr = offr;
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store;
-    g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones);
+    g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel;
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
     // algorithmic traffic: A once (a 3x3 reads each input pixel once), W per weight set, out
     // (+ residual) once
@@ -1007,6 +1008,16 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]) {
     h->prof.clear();
     h->ev_used = 0;
     h->prof_cls = -1;
+  });
+}
+
+int turtle_set_option(TurtleHandle* h, const char* name, int value) {
+  return guard([&] {
+    if (!h || !name) TFAIL(TURTLE_EINVAL, "null argument");
+    const std::string n = name;
+    if (n == "fuse") h->fuse = value != 0;
+    else if (n == "panel_gemm") h->panel = value != 0;
+    else TFAIL(TURTLE_EINVAL, "unknown option '" + n + "'");
   });
 }
 

@@ -178,6 +178,13 @@ class TurtleHIP(TurtleParams):
         return out, k_out, v_out
 
     # ---------------------------------------------------------------------------------------
+    def set_option(self, name: str, value: int):
+        """Kernel-selection switch (turtle_set_option): 'fuse', 'panel_gemm'. Same results."""
+        if self._handle is None or self._sig is None:
+            self.refresh_weights()
+        _lib.check(_lib.lib().turtle_set_option(self._handle.h, name.encode(), int(value)))
+        return self
+
     def profile_begin(self, kernel_class: str = "all"):
         """Bracket every launch of `kernel_class` (see _lib.K_CLASSES, or 'all') with HIP events."""
         cls = _lib.K_ALL if kernel_class == "all" else _lib.K_CLASSES.index(kernel_class)
