@@ -123,6 +123,24 @@ TURTLE_DEV float ld4f(const float* p) {
 #endif
 }
 
+// Two 8-float scalar loads (s_load_dwordx8 x2) of wave-uniform, read-only data (depthwise weights).
+// hipcc will not emit scalar loads through these pointers on its own (the asm in the same loops
+// counts as a possible clobber), so they are issued here and retired by sload_wait(): the wait
+// redefines the values, so no use can be scheduled before it.
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+TURTLE_DEV void sload2x8(const float* p0, const float* p1, f32x8& o0, f32x8& o1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx8 %1, %3, 0x0" : "=&s"(o0), "=&s"(o1) : "s"(p0), "s"(p1));
+#else
+  for (int i = 0; i < 8; ++i) { o0[i] = p0[i]; o1[i] = p1[i]; }
+#endif
+}
+TURTLE_DEV void sload_wait(f32x8& o0, f32x8& o1) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(o0), "+s"(o1));
+#endif
+}
+
 TURTLE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
 TURTLE_DEV float wave_sum(float v) {

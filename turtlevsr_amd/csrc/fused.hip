@@ -8,15 +8,21 @@
 //   F_DWONLY  [LN ->] pointwise -> dw 3x3, stored        qkv/qkv_dwconv (666-684), SAB qk/v
 //           (ChannelAttention, FHR, CHM inputs)          (555-557), CHM kv/kv_dwconv (649)
 //
-// For input widths C <= 128 (levels 1-2, where ~80 % of the pixels are): the haloed input tile
-// [112 rows][C] is loaded into LDS once (LayerNorm statistics computed from it; the LN affine is
-// folded into W1 at pack time as in gemm.hip). The hidden channels are then processed in chunks of
-// HC: GEMM1 (MFMA; A = W1 rows read straight from L2 into registers, one chunk ahead; B = the LDS
-// tile) gives the chunk's pointwise outputs on all 100 haloed pixels -> LDS; the depthwise 3x3 +
-// activation runs out of LDS; GEMM2 (A = W2 rows from L2, B = activated chunk in LDS, double
-// buffered) accumulates the 64 output pixels x N2 channels in registers. Halo pixels outside the
-// image are zeroed after GEMM1 (the reference pads the dw *input* with zeros).
-// HBM traffic per output pixel: ~1.56 C in + C out (+ C residual), against
+// Input widths C <= 128 (levels 1-2, where ~80 % of the pixels are). Structure ("wave slices"):
+//   * the haloed input tile [112 rows][C] is loaded into LDS once; LayerNorm statistics come from
+//     it (the LN affine is folded into W1 at pack time, as in gemm.hip);
+//   * phase A - every wave independently walks its own hidden-channel slices (16 GEMM1 columns
+//     each: 8 x1 + 8 x2 channels for the gate, else 16 channels). Per slice: GEMM1 over the 112
+//     haloed rows (MFMA; W1 fragments straight from L2 into registers, B = the LDS tile) -> LN /
+//     bias / out-of-image halo zeroing -> a wave-private LDS strip -> depthwise 3x3 with lane =
+//     output pixel (the 9x16 tap weights are wave-uniform scalar loads) -> activation -> the
+//     slice's columns of the shared G tile (or, dw-only, straight to HBM). No block barrier:
+//     a wave only ever reads LDS it wrote itself;
+//   * phase B - one barrier, then GEMM2 Y[64 px][N2] += G . W2^T with each wave owning N2/4
+//     output channels (W2 fragments prefetched during phase A). Hidden widths above the G tile's
+//     capacity run as passes (phase A, barrier, phase B, barrier).
+//   * epilogue: + b2, * scale, + residual, 8-byte stores.
+// HBM traffic per output pixel: ~1.56 C in (halo) + C out (+ C residual), against
 // C + 2h + 2h + h + h + 2C for the unfused sequence.
 #include "common.h"
 #include "kernels.h"
@@ -29,27 +35,23 @@ constexpr int FH = FT + 2;            // haloed tile side
 constexpr int FNH = FH * FH;          // 100 haloed pixels
 constexpr int FMT = 7;                // 16-row MFMA tiles covering the haloed pixels (112 rows)
 constexpr int FNO = FT * FT;          // 64 output pixels
-constexpr int FNC = 64;               // GEMM1 columns per chunk
-constexpr int FCMAX = 128;            // max input channels (X tile resident in LDS)
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_fused[4];
 
-template <typename T, int MODE>
-struct FusedCfg {
+template <typename T, int MODE, int CM>
+struct F3 {
   static constexpr int ES = sizeof(T);
-  static constexpr int HC = MODE == F_GATE ? 32 : 64;            // hidden channels per chunk
-  static constexpr int XROW = FCMAX * ES + 16;                     // sX row bytes
-  static constexpr int HROW = FNC * ES + 16;                       // sH row bytes
-  static constexpr int GROW = HC * ES + 16;                        // sG row bytes
+  static constexpr int SL = MODE == F_GATE ? 8 : 16;                // hidden channels per slice
+  static constexpr int HP = MODE == F_GATE ? 160 : (MODE == F_GELU ? 128 : 0);   // hidden per pass
+  static constexpr int XROW = CM * ES + 16;                        // sX row bytes
+  static constexpr int HROW = 16 * ES + 16;                        // wave strip row bytes
+  static constexpr int GROW = HP * ES + 16;                        // sG row bytes
   static constexpr int OFF_H = 112 * XROW;
-  static constexpr int OFF_G = OFF_H + 112 * HROW;
-  static constexpr int OFF_ST = OFF_G + 2 * FNO * GROW;            // mu, rstd [112]
-  static constexpr int OFF_E = OFF_ST + 2 * 112 * 4;               // ln_s, ln_t, b1 [2][64] each
-  static constexpr int OFF_DW = OFF_E + 2 * 3 * FNC * 4;           // dw weights + bias [2][10][64]
-  static constexpr int BYTES = OFF_DW + 2 * 10 * FNC * 4;
+  static constexpr int OFF_G = OFF_H + 4 * 112 * HROW;
+  static constexpr int OFF_ST = OFF_G + (HP ? FNO * GROW : 0);     // mu, rstd [112]
+  static constexpr int BYTES = OFF_ST + 2 * 112 * 4;
 };
 
-// MFMA operand fragment types / single steps (A operand in registers, B from LDS)
 template <typename T> struct Frag;
 template <> struct Frag<bf16> { typedef bf16x8 type; static constexpr int K = 32; };
 template <> struct Frag<float> { typedef float type; static constexpr int K = 4; };
@@ -57,43 +59,54 @@ template <> struct Frag<float> { typedef float type; static constexpr int K = 4;
 TURTLE_DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
 TURTLE_DEV f32x4 mfma(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
-// lane's A/B fragment of one K step from a row-major [row][k] image (row = lane & 15)
+// lane's A/B fragment of one K step from a row-major [row][k] LDS image (row = lane & 15)
 template <typename T>
 TURTLE_DEV typename Frag<T>::type frag_at(const char* row0, int rowbytes, int k0, int lane) {
   const char* p = row0 + (lane & 15) * rowbytes;
   if constexpr (sizeof(T) == 2) return *reinterpret_cast<const bf16x8*>(p + (k0 + (lane >> 4) * 8) * 2);
   else return *reinterpret_cast<const float*>(p + (k0 + (lane >> 4)) * 4);
 }
-// same fragment from global memory (weights; rows past `nrows` or k past `kmax` read as zero)
+// same fragment from global memory (weights); out-of-range rows / k read the zero line
 template <typename T>
-TURTLE_DEV typename Frag<T>::type frag_glb(const T* w, int64_t ld, int row, int nrows, int k0, int kmax, int lane) {
-  const int r = row + (lane & 15);
+TURTLE_DEV typename Frag<T>::type frag_glb(const T* w, int64_t ld, int row, bool rowok, int k0, int kmax, int lane) {
   if constexpr (sizeof(T) == 2) {
     const int k = k0 + (lane >> 4) * 8;
-    const bool ok = r < nrows && k < kmax;
-    const uint4 q = ld16(ok ? reinterpret_cast<const void*>(w + (int64_t)r * ld + k) : g_zero_fused);
-    return __builtin_bit_cast(bf16x8, q);
+    const bool ok = rowok && k < kmax;
+    return __builtin_bit_cast(bf16x8, ld16(ok ? reinterpret_cast<const void*>(w + (int64_t)row * ld + k) : g_zero_fused));
   } else {
     const int k = k0 + (lane >> 4);
-    const bool ok = r < nrows && k < kmax;
-    return ok ? w[(int64_t)r * ld + k] : 0.f;
+    const bool ok = rowok && k < kmax;
+    return ld4f(ok ? w + (int64_t)row * ld + k : reinterpret_cast<const float*>(g_zero_fused));
   }
 }
 
-template <typename T, int MODE>
+template <typename T>
+TURTLE_DEV void unpack8(const uint4& q, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(w[i] << 16); v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+  } else {
+    v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y); v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+  }
+}
+
+template <typename T, int MODE, int CM>
 __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
-  using F = FusedCfg<T, MODE>;
+  using F = F3<T, MODE, CM>;
   using FR = typename Frag<T>::type;
-  constexpr int VEC = Vec<T>::N, ES = F::ES, HC = F::HC, KF = Frag<T>::K;
-  constexpr int K1 = FCMAX / KF;                      // max GEMM1 K steps
-  constexpr int K2 = HC / KF;                         // GEMM2 K steps per chunk
+  constexpr int VEC = Vec<T>::N, ES = F::ES, KF = Frag<T>::K, SL = F::SL;
+  constexpr int K1 = CM / KF;                         // GEMM1 K steps (max)
   __shared__ __attribute__((aligned(16))) char smem[F::BYTES];
   char* sX = smem;
-  char* sH = smem + F::OFF_H;
   float* s_mu = reinterpret_cast<float*>(smem + F::OFF_ST);
   float* s_rs = s_mu + 112;
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  // wave index as a provably uniform (SGPR) value: slice loops and the tap-weight addresses
+  // derived from it then compile to scalar loads
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  char* sHw = smem + F::OFF_H + wid * 112 * F::HROW;   // this wave's private strip
   // ---- tile of this block (XCD-aware: neighbouring tiles share an L2) ----
   const int tx_n = (a.W + FT - 1) / FT, ty_n = (a.H + FT - 1) / FT;
   int lin = blockIdx.x;
@@ -106,75 +119,22 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
   const int ty0 = (trem / tx_n) * FT, tx0 = (trem % tx_n) * FT;
   const int C = a.C;
   const int nk1 = (C + KF - 1) / KF;
-  const int nchunk = (a.hidden + HC - 1) / HC;
   const T* W1 = reinterpret_cast<const T*>(a.w1);
   const T* W2 = reinterpret_cast<const T*>(a.w2);
+  const int hid = a.hidden;
+  const int nslice = MODE == F_GATE ? hid / 8 : a.N1 / 16;
 
-  // GEMM1 column n of chunk c -> W1 row (or -1 past the hidden width)
-  auto w1row = [&](int c, int n) -> int {
-    if (MODE == F_GATE) {
-      const int j = c * HC + (n & (HC - 1));
-      if (j >= a.hidden) return -1;
-      return n < HC ? j : a.hidden + j;
-    }
-    const int j = c * FNC + n;
-    return j < a.N1 ? j : -1;
-  };
-  // per-chunk column vectors (ln_s, ln_t, b1, 9 dw taps, dw bias: 13 x 64 floats) -> LDS slot
-  // (c & 1), in two halves: fetch into registers (unconditional loads, one L2 round trip), store
-  // later. Item v = tid + 256 k is vector v / 64 (wave-uniform), column v % 64.
-  constexpr int NVI = (13 * FNC + 255) / 256;
-  auto fetch_vectors = [&](int c, float (&r)[NVI]) {
-#pragma unroll
-    for (int k = 0; k < NVI; ++k) {
-      const int v = tid + 256 * k, vec = v / FNC, n = v - vec * FNC;
-      const int wrow = w1row(c, n);
-      const float* base = vec == 0 ? a.ln_s : vec == 1 ? a.ln_t : vec == 2 ? a.b1 : vec == 12 ? a.dwb
-                        : vec < 12 ? a.dww + (int64_t)(vec - 3) * a.N1 : nullptr;
-      const bool ok = v < 13 * FNC && base != nullptr && wrow >= 0;
-      r[k] = ld4f(ok ? base + wrow : reinterpret_cast<const float*>(g_zero_fused));
-    }
-  };
-  auto store_vectors = [&](int c, const float (&r)[NVI]) {
-    float* dst = reinterpret_cast<float*>(smem + F::OFF_E) + (c & 1) * 3 * FNC;
-    float* dwd = reinterpret_cast<float*>(smem + F::OFF_DW) + (c & 1) * 10 * FNC;
-#pragma unroll
-    for (int k = 0; k < NVI; ++k) {
-      const int v = tid + 256 * k;
-      if (v < 3 * FNC) dst[v] = r[k];
-      else if (v < 13 * FNC) dwd[v - 3 * FNC] = r[k];
-    }
-  };
-  // W1 fragments of chunk c for this wave's 16 columns (GATE: wave 0,1 -> x1 rows, 2,3 -> x2 rows)
-  auto load_w1 = [&](int c, FR (&f)[K1]) {
-    const int n = wid * 16 + (lane & 15);
-    const int wrow = w1row(c, n);
-#pragma unroll
-    for (int kk = 0; kk < K1; ++kk) {
-      if constexpr (sizeof(T) == 2) {
-        const int k = kk * KF + (lane >> 4) * 8;
-        const bool ok = wrow >= 0 && k < C;
-        f[kk] = __builtin_bit_cast(bf16x8, ld16(ok ? reinterpret_cast<const void*>(W1 + (int64_t)wrow * C + k) : g_zero_fused));
-      } else {
-        const int k = kk * KF + (lane >> 4);
-        f[kk] = (wrow >= 0 && k < C) ? W1[(int64_t)wrow * C + k] : 0.f;
-      }
-    }
-  };
-  // W2 fragments of chunk c: output-channel tiles wid, wid+4 (N2 <= 128)
-  auto load_w2 = [&](int c, FR (&f)[2][K2]) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-      for (int kk = 0; kk < K2; ++kk)
-        f[u][kk] = frag_glb<T>(W2, a.hidden, (wid + 4 * u) * 16, a.N2, c * HC + kk * KF, a.hidden, lane);
+  // GEMM1 column n (0..15) of slice s -> W1 / dw row
+  auto w1row = [&](int s, int n) -> int {
+    if (MODE == F_GATE) return n < 8 ? s * 8 + n : hid + s * 8 + (n - 8);
+    return s * 16 + n;
   };
 
   // ---- haloed X tile -> LDS, once (all loads issued before the first LDS write) ----
   {
     const T* X = reinterpret_cast<const T*>(a.x);
     const int cv = C / VEC;
-    constexpr int XV = (112 * (FCMAX / VEC) + 255) / 256;
+    constexpr int XV = (112 * (CM / VEC) + 255) / 256;
     uint4 xv[XV];
     int xo[XV];
 #pragma unroll
@@ -200,16 +160,6 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
       *reinterpret_cast<uint4*>(sX + r * F::XROW + k * ES) = uint4{0u, 0u, 0u, 0u};
     }
   }
-  // weight fragments: one register set each, refilled for chunk c+1 right after their last use in
-  // chunk c, so the L2 latency hides behind the depthwise stage / the next GEMM1
-  FR w1f[K1];
-  FR w2f[2][K2];
-  load_w1(0, w1f);
-  if constexpr (MODE != F_DWONLY) load_w2(0, w2f);
-  float vn[NVI];                      // vectors of chunk c+1, fetched at the end of chunk c-1
-  fetch_vectors(0, vn);
-  store_vectors(0, vn);
-  if (nchunk > 1) fetch_vectors(1, vn);
   __syncthreads();
   if (a.ln && tid < 224) {
     // LayerNorm statistics of the 112 staged rows: 2 threads per row, shifted sums
@@ -232,150 +182,207 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
   }
   __syncthreads();
 
-  f32x4 acc2[2][4];
+  // per-lane constants of the GEMM1 epilogue: haloed row validity of each M tile
+  unsigned inimg_mask = 0;
 #pragma unroll
-  for (int u = 0; u < 2; ++u)
-#pragma unroll
-    for (int p = 0; p < 4; ++p) acc2[u][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < FMT; ++t) {
+    const int r = t * 16 + (lane & 15);
+    const int hy = r / FH, hx = r - hy * FH;
+    const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
+    if (r < FNH && y >= 0 && y < a.H && x >= 0 && x < a.W) inimg_mask |= 1u << t;
+  }
+  // lane = output pixel in the depthwise stage
+  const int oy = lane >> 3, ox = lane & 7;
 
-  for (int c = 0; c < nchunk; ++c) {
-    const bool more = c + 1 < nchunk;
-    const float* e = reinterpret_cast<const float*>(smem + F::OFF_E) + (c & 1) * 3 * FNC;
-    const float* dwv = reinterpret_cast<const float*>(smem + F::OFF_DW) + (c & 1) * 10 * FNC;
-    // ---- GEMM1: wave w -> 16 columns x 7 row tiles ----
-    f32x4 acc1[FMT];
+  // ---- phase A for slices [s_beg, s_end): this wave's share (s = s_beg + wid, +4, ...) ----
+  auto phase_a = [&](int s_beg, int s_end) {
+    // W1 fragments and the lane's 4 epilogue columns (4(l>>4)..+3) of slice s, fetched one
+    // slice ahead so their L2 latency hides behind the previous slice's depthwise stage
+    FR wf[K1];
+    uint4 es, et, eb;
+    const int c4 = (lane >> 4) * 4;
+    auto fetch = [&](int s) {
+      const int wr = w1row(s, lane & 15);
 #pragma unroll
-    for (int t = 0; t < FMT; ++t) acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kk = 0; kk < K1; ++kk) {
-      if (kk < nk1) {
-#pragma unroll
-        for (int t = 0; t < FMT; ++t) acc1[t] = mfma(w1f[kk], frag_at<T>(sX + t * 16 * F::XROW, F::XROW, kk * KF, lane), acc1[t]);
+      for (int kk = 0; kk < K1; ++kk) {
+        if constexpr (sizeof(T) == 2) {
+          const int k = kk * KF + (lane >> 4) * 8;
+          wf[kk] = __builtin_bit_cast(bf16x8, ld16(k < C ? reinterpret_cast<const void*>(W1 + (int64_t)wr * C + k) : g_zero_fused));
+        } else {
+          const int k = kk * KF + (lane >> 4);
+          wf[kk] = ld4f(k < C ? W1 + (int64_t)wr * C + k : reinterpret_cast<const float*>(g_zero_fused));
+        }
       }
-      // keep the scheduler from hoisting every K step's LDS fragments at once (register blow-up)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (more) load_w1(c + 1, w1f);
-    {
-      const int col = wid * 16 + (lane >> 4) * 4;
+      const int er = w1row(s, c4);                      // 4 consecutive W1 rows
+      const float* zf = reinterpret_cast<const float*>(g_zero_fused);
+      es = ld16(a.ln_s ? reinterpret_cast<const void*>(a.ln_s + er) : zf);
+      et = ld16(a.ln_t ? reinterpret_cast<const void*>(a.ln_t + er) : zf);
+      eb = ld16(a.b1 ? reinterpret_cast<const void*>(a.b1 + er) : zf);
+    };
+    if (s_beg + wid < s_end) fetch(s_beg + wid);
+    for (int s = s_beg + wid; s < s_end; s += 4) {
+      const float fs[4] = {__uint_as_float(es.x), __uint_as_float(es.y), __uint_as_float(es.z), __uint_as_float(es.w)};
+      const float ft[4] = {__uint_as_float(et.x), __uint_as_float(et.y), __uint_as_float(et.z), __uint_as_float(et.w)};
+      const float fb[4] = {__uint_as_float(eb.x), __uint_as_float(eb.y), __uint_as_float(eb.z), __uint_as_float(eb.w)};
+      // GEMM1: 16 columns x 7 row tiles
+      f32x4 acc1[FMT];
+#pragma unroll
+      for (int t = 0; t < FMT; ++t) acc1[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < K1; ++kk) {
+        if (kk < nk1) {
+#pragma unroll
+          for (int t = 0; t < FMT; ++t) acc1[t] = mfma(wf[kk], frag_at<T>(sX + t * 16 * F::XROW, F::XROW, kk * KF, lane), acc1[t]);
+        }
+      }
+      if (s + 4 < s_end) fetch(s + 4);                  // next slice's operands, behind this one
+      // epilogue -> wave strip [112][16]
 #pragma unroll
       for (int t = 0; t < FMT; ++t) {
         const int r = t * 16 + (lane & 15);
-        const int hy = r / FH, hx = r - hy * FH;
-        const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
-        const bool inimg = r < FNH && y >= 0 && y < a.H && x >= 0 && x < a.W;
         const float mu = a.ln ? s_mu[r] : 0.f, rs = a.ln ? s_rs[r] : 1.f;
+        const bool inimg = (inimg_mask >> t) & 1u;
         float v[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float z = acc1[t][q];
-          if (a.ln) z = rs * (z - mu * e[col + q]) + e[FNC + col + q];
-          z += e[2 * FNC + col + q];
+          if (a.ln) z = rs * (z - mu * fs[q]) + ft[q];
+          z += fb[q];
           v[q] = inimg ? z : 0.f;
         }
         if constexpr (sizeof(T) == 4) {
-          *reinterpret_cast<float4*>(sH + r * F::HROW + col * 4) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(sHw + r * F::HROW + c4 * 4) = make_float4(v[0], v[1], v[2], v[3]);
         } else {
           typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          *reinterpret_cast<bf16x4*>(sH + r * F::HROW + col * 2) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          *reinterpret_cast<bf16x4*>(sHw + r * F::HROW + c4 * 2) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
         }
       }
-    }
-    if (more) store_vectors(c + 1, vn);   // slot (c+1)&1 was last read before the previous chunk's 2nd barrier
-    __syncthreads();
-    // ---- depthwise 3x3 (+ activation) on the 64 centre pixels ----
-    char* sG = smem + F::OFF_G + (c & 1) * FNO * F::GROW;
-    {
-      constexpr int CPT = MODE == F_GATE ? HC / 4 : FNC / 4;     // channels per thread (8 or 16)
-      const int o = tid >> 2, oy = o >> 3, ox = o & 7;
-      const int cb = (tid & 3) * CPT;
-      float d1[CPT], d2[CPT];
+      // the strip is private to this wave: its LDS ops execute in order, only the compiler's
+      // view of the data dependence through LDS needs a fence
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      // depthwise 3x3 at pixel (oy, ox): 16 channels, wave-uniform tap weights (scalar loads)
+      float d[16];
+      const int wr0 = w1row(s, 0), wr8 = w1row(s, 8);   // rows of channels 0-7 and 8-15
+      f32x8 cw0, cw8;                                   // current tap's weights (SGPRs)
+      {
+        const float* zf = reinterpret_cast<const float*>(g_zero_fused);
+        f32x8 b0, b8;
+        sload2x8(a.dwb ? a.dwb + wr0 : zf, a.dwb ? a.dwb + wr8 : zf, b0, b8);
+        sload2x8(a.dww + wr0, a.dww + wr8, cw0, cw8);
+        sload_wait(b0, b8);
 #pragma unroll
-      for (int i = 0; i < CPT; ++i) {
-        d1[i] = dwv[9 * FNC + cb + i];
-        d2[i] = MODE == F_GATE ? dwv[9 * FNC + HC + cb + i] : 0.f;
+        for (int i = 0; i < 8; ++i) { d[i] = b0[i]; d[8 + i] = b8[i]; }
       }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        const int hr = (oy + tap / 3) * FH + ox + tap % 3;
-        const T* hrow = reinterpret_cast<const T*>(sH + hr * F::HROW);
+        const char* hr = sHw + ((oy + tap / 3) * FH + ox + tap % 3) * F::HROW;
+        float v[16];
 #pragma unroll
-        for (int i0 = 0; i0 < CPT; i0 += VEC) {
-          Vec<T> v; v.load(hrow + cb + i0);
+        for (int c0 = 0; c0 < 16; c0 += VEC) unpack8<T>(*reinterpret_cast<const uint4*>(hr + c0 * ES), v + c0);
+        sload_wait(cw0, cw8);
+        f32x8 nw0, nw8;                                 // next tap's weights in flight
+        if (tap < 8) sload2x8(a.dww + (int64_t)(tap + 1) * a.N1 + wr0, a.dww + (int64_t)(tap + 1) * a.N1 + wr8, nw0, nw8);
 #pragma unroll
-          for (int i = 0; i < VEC; ++i) d1[i0 + i] = fmaf(dwv[tap * FNC + cb + i0 + i], v.v[i], d1[i0 + i]);
-          if constexpr (MODE == F_GATE) {
-            Vec<T> w; w.load(hrow + HC + cb + i0);
-#pragma unroll
-            for (int i = 0; i < VEC; ++i) d2[i0 + i] = fmaf(dwv[tap * FNC + HC + cb + i0 + i], w.v[i], d2[i0 + i]);
-          }
+        for (int i = 0; i < 8; ++i) {
+          d[i] = fmaf(cw0[i], v[i], d[i]);
+          d[8 + i] = fmaf(cw8[i], v[8 + i], d[8 + i]);
         }
-        // pin the accumulators after every tap: otherwise the scheduler runs each channel's 9-tap
-        // chain to completion and keeps every tap's operands live (>250 VGPRs, spills)
+        if (tap < 8) { cw0 = nw0; cw8 = nw8; }
+        // one tap's operands live at a time (else every tap's LDS values stay in VGPRs)
 #pragma unroll
-        for (int i = 0; i < CPT; ++i) {
-          asm volatile("" : "+v"(d1[i]));
-          if constexpr (MODE == F_GATE) asm volatile("" : "+v"(d2[i]));
-        }
+        for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(d[i]));
       }
       if constexpr (MODE == F_DWONLY) {
         const int y = ty0 + oy, x = tx0 + ox;
-        if (y < a.H && x < a.W) {
+        const int ch = s * 16;
+        if (y < a.H && x < a.W && ch < a.N1) {
+          const int di = (a.ndst > 1 && ch >= a.dst[0].cend) ? ((a.ndst > 2 && ch >= a.dst[1].cend) ? 2 : 1) : 0;
+          const FusedDst D = di == 0 ? a.dst[0] : (di == 1 ? a.dst[1] : a.dst[2]);
+          const int cl = ch - D.cbeg;
+          int64_t off;
+          if (D.tok_ws > 0) {
+            const int ws = D.tok_ws, h = a.H / ws, w = a.W / ws;
+            const int p1 = y / h, i = y - p1 * h, p2 = x / w, j = x - p2 * w;
+            off = img * D.tok_stride + ((int64_t)i * w + j) * ((int64_t)ws * ws * D.ccount) +
+                  (int64_t)(p1 * ws + p2) * D.ccount + cl;
+          } else {
+            off = (((int64_t)img * a.H + y) * a.W + x) * D.ld + D.off + cl;
+          }
 #pragma unroll
-          for (int i0 = 0; i0 < CPT; i0 += VEC) {
-            const int ch = c * FNC + cb + i0;
-            if (ch >= a.N1) continue;
-            const int di = (a.ndst > 1 && ch >= a.dst[0].cend) ? ((a.ndst > 2 && ch >= a.dst[1].cend) ? 2 : 1) : 0;
-            const FusedDst D = di == 0 ? a.dst[0] : (di == 1 ? a.dst[1] : a.dst[2]);
-            const int cl = ch - D.cbeg;
-            int64_t off;
-            if (D.tok_ws > 0) {
-              const int ws = D.tok_ws, h = a.H / ws, w = a.W / ws;
-              const int p1 = y / h, i = y - p1 * h, p2 = x / w, j = x - p2 * w;
-              off = img * D.tok_stride + ((int64_t)i * w + j) * ((int64_t)ws * ws * D.ccount) +
-                    (int64_t)(p1 * ws + p2) * D.ccount + cl;
-            } else {
-              off = (((int64_t)img * a.H + y) * a.W + x) * D.ld + D.off + cl;
-            }
+          for (int i0 = 0; i0 < 16; i0 += VEC) {
             Vec<T> ov;
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) ov.v[i] = d1[i0 + i];
-            ov.store(reinterpret_cast<T*>(D.p) + off);
+            for (int i = 0; i < VEC; ++i) ov.v[i] = d[i0 + i];
+            ov.store(reinterpret_cast<T*>(D.p) + off + i0);
           }
         }
       } else {
-        Vec<T> gv;
+        // G columns of this slice within the current pass
+        T* g = reinterpret_cast<T*>(smem + F::OFF_G + lane * F::GROW) + (s * SL) % F::HP;
+        if constexpr (MODE == F_GATE) {
+          Vec<T> gv;
 #pragma unroll
-        for (int i0 = 0; i0 < CPT; i0 += VEC) {
+          for (int i0 = 0; i0 < 8; i0 += VEC) {
 #pragma unroll
-          for (int i = 0; i < VEC; ++i)
-            gv.v[i] = MODE == F_GATE ? gelu_erf(d1[i0 + i]) * d2[i0 + i] : gelu_erf(d1[i0 + i]);
-          gv.store(reinterpret_cast<T*>(sG + o * F::GROW) + cb + i0);
+            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_erf(d[i0 + i]) * d[8 + i0 + i];
+            gv.store(g + i0);
+          }
+        } else {
+#pragma unroll
+          for (int i0 = 0; i0 < 16; i0 += VEC) {
+            Vec<T> gv;
+#pragma unroll
+            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_erf(d[i0 + i]);
+            gv.store(g + i0);
+          }
         }
       }
     }
-    __syncthreads();     // sG complete; sH free for the next chunk's GEMM1
-    if constexpr (MODE != F_DWONLY) {
-      // ---- GEMM2: Y[64 px][N2] += G . W2_chunk^T (sG double-buffered across chunks) ----
-      const int nct = (a.N2 + 15) / 16;
+  };
+
+  if constexpr (MODE == F_DWONLY) {
+    phase_a(0, nslice);
+    return;
+  } else {
+    // ---- passes: phase A over HP hidden channels, then GEMM2 over them ----
+    constexpr int K2 = F::HP / KF;
+    const int nct = a.N2 / 16;                         // output channel tiles (<= 8): wave w owns w, w+4
+    f32x4 acc2[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) acc2[u][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int npass = (hid + F::HP - 1) / F::HP;
+    for (int ps = 0; ps < npass; ++ps) {
+      const int h0 = ps * F::HP, hw = min(F::HP, hid - h0);
+      // W2 fragments of this pass, in flight during phase A
+      FR w2f[2][K2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int kk = 0; kk < K2; ++kk)
+          w2f[u][kk] = frag_glb<T>(W2, hid, (wid + 4 * u) * 16 + (lane & 15), wid + 4 * u < nct, h0 + kk * KF, h0 + hw, lane);
+      if (ps > 0) __syncthreads();                     // previous pass's GEMM2 has read sG
+      phase_a(h0 / SL, (h0 + hw) / SL);
+      __syncthreads();
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (wid + 4 * u >= nct) continue;
 #pragma unroll
-        for (int kk = 0; kk < K2; ++kk)
+        for (int kk = 0; kk < K2; ++kk) {
+          if (kk * KF < hw) {
 #pragma unroll
-          for (int p = 0; p < 4; ++p)
-            acc2[u][p] = mfma(w2f[u][kk], frag_at<T>(sG + p * 16 * F::GROW, F::GROW, kk * KF, lane), acc2[u][p]);
+            for (int p = 0; p < 4; ++p)
+              acc2[u][p] = mfma(w2f[u][kk], frag_at<T>(smem + F::OFF_G + p * 16 * F::GROW, F::GROW, kk * KF, lane), acc2[u][p]);
+          }
+        }
       }
-      if (more) load_w2(c + 1, w2f);
     }
-    if (c + 2 < nchunk) fetch_vectors(c + 2, vn);   // in flight across the barrier and GEMM1
-  }
 
-  if constexpr (MODE != F_DWONLY) {
     // ---- epilogue: + b2, * scale, + residual, store (4 consecutive channels per lane; N2 % 16 == 0).
     // b2 / scale2 come from LDS, all residual loads are issued unconditionally before any use.
-    float* sb = reinterpret_cast<float*>(smem + F::OFF_H);   // sH is free after the last GEMM2
+    float* sb = reinterpret_cast<float*>(smem + F::OFF_H);   // the strips are free after phase A
     __syncthreads();
     if (tid < 128) {
       const float* zf = reinterpret_cast<const float*>(g_zero_fused);
@@ -384,7 +391,6 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
       sb[tid] = bv;
       sb[128 + tid] = a.scale2 ? sv : 1.f;
     }
-    const int nct = a.N2 / 16;
     T* out = reinterpret_cast<T*>(a.out);
     const T* res = reinterpret_cast<const T*>(a.res);
     int64_t pix[4];
@@ -440,15 +446,21 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
   }
 }
 
-template <typename T>
-void launch_fused(const FusedArgs& a, hipStream_t st) {
+template <typename T, int CM>
+static void launch_fused_cm(const FusedArgs& a, hipStream_t st) {
   const int64_t blocks = (int64_t)a.nimg * ((a.H + FT - 1) / FT) * ((a.W + FT - 1) / FT);
   if (a.mode == F_GATE)
-    hipLaunchKernelGGL((fused_kernel<T, F_GATE>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((fused_kernel<T, F_GATE, CM>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   else if (a.mode == F_GELU)
-    hipLaunchKernelGGL((fused_kernel<T, F_GELU>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((fused_kernel<T, F_GELU, CM>), dim3((unsigned)blocks), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((fused_kernel<T, F_DWONLY>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((fused_kernel<T, F_DWONLY, CM>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+}
+
+template <typename T>
+void launch_fused(const FusedArgs& a, hipStream_t st) {
+  if (a.C <= 64) launch_fused_cm<T, 64>(a, st);
+  else launch_fused_cm<T, 128>(a, st);
 }
 
 template void launch_fused<float>(const FusedArgs&, hipStream_t);

@@ -603,6 +603,12 @@ struct Runner {
     tag("fused mode=%d nimg=%d H=%d W=%d C=%d N1=%d N2=%d ln=%d ndst=%d", mode, nimg, H, Wd, C, w1.N, f.N2, f.ln, f.ndst);
     launch(TURTLE_K_FUSED, bytes, flops, [&] { launch_fused<T>(f, st); });
   }
+  // fused.hip handles input widths <= 128 in 16-channel slices and 32-deep GEMM2 K steps
+  bool can_fuse(int c, int mode, int n1, int hidden) const {
+    if (!h->fuse || c > 128 || c % 16) return false;
+    if (mode == F_DWONLY) return n1 % 16 == 0;
+    return hidden % 32 == 0;
+  }
   static FusedDst dst_map(void* p, int64_t ld, int off, int cbeg, int cend) {
     return FusedDst{p, ld, off, cbeg, cend, cend - cbeg, 0, 0};
   }
@@ -660,9 +666,8 @@ struct Runner {
     const int c = b.dim, HW = H * Wd;
     const int64_t P = (int64_t)B * HW;
     const size_t mark = ar.off;
-    const bool fz = h->fuse;
     if (b.attn == TURTLE_ATTN_REDUCED) {
-      if (fz && c <= 128) {
+      if (can_fuse(c, F_GELU, 2 * c, 2 * c)) {
         fused(F_GELU, bw.a_in, bw.a_dw, x, c, 0, c, B, H, Wd, 2 * c, &bw.a_out, x, xalt, {});
         std::swap(x, xalt);
       } else {
@@ -687,7 +692,7 @@ struct Runner {
     // feed-forward
     if (b.ffn == TURTLE_FFN_GFFW) {
       const int hd = b.hidden;
-      if (fz && c <= 128) {
+      if (can_fuse(c, F_GATE, 2 * hd, hd)) {
         fused(F_GATE, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, &bw.f_out, x, xalt, {});
         std::swap(x, xalt);
       } else {
@@ -707,7 +712,7 @@ struct Runner {
 
   // LN(x) -> qkv 1x1 -> qkv_dwconv into `out` [P][3c] (fused, or GEMM + dw)
   void qkv_dw(const BlockW& bw, const T* x, int c, T* out, int nimg, int H, int Wd) {
-    if (h->fuse && c <= 128) {
+    if (can_fuse(c, F_DWONLY, 3 * c, 0)) {
       fused(F_DWONLY, bw.a_in, bw.a_dw, x, c, 0, c, nimg, H, Wd, 3 * c, nullptr, nullptr, nullptr,
             {dst_map(out, 3 * c, 0, 0, 3 * c)});
     } else {
@@ -776,7 +781,7 @@ struct Runner {
     // LN(x) -> [SAB qk | SAB v | FHR qkv] -> their depthwise convs; SAB v goes straight into the new
     // cache's current frame in the dilated token-major layout
     T* vcur = vout + (int64_t)(Tnew - 1) * N * D;
-    if (h->fuse && c <= 128) {
+    if (can_fuse(c, F_DWONLY, 6 * c, 0)) {
       FusedDst dv{vcur, 0, 0, 2 * c, 3 * c, c, ws, (int64_t)Tnew * N * D};
       fused(F_DWONLY, bw.a_in, bw.chm_dw6, x, c, 0, c, B, H, Wd, 6 * c, nullptr, nullptr, nullptr,
             {dst_map(qkd, 2 * c, 0, 0, 2 * c), dv, dst_map(fq, 3 * c, 0, 3 * c, 6 * c)});
@@ -833,7 +838,7 @@ struct Runner {
              2.0 * B * NT * (double)N * 46 * D, [&] { launch_sab_av<T>(va, st); });
     }
     // kv = (W_kv W_po) xs over the B*T aligned frames, then dw3x3 per frame
-    if (h->fuse && c <= 128) {
+    if (can_fuse(c, F_DWONLY, 2 * c, 0)) {
       fused(F_DWONLY, bw.kv, bw.kv_dw, xs, c, 0, c, B * NT, H, Wd, 2 * c, nullptr, nullptr, nullptr,
             {dst_map(kvd, 2 * c, 0, 0, 2 * c)});
     } else {
