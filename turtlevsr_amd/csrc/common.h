@@ -141,6 +141,21 @@ TURTLE_DEV void sload_wait(f32x8& o0, f32x8& o1) {
 #endif
 }
 
+// GELU with erf from Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7): two transcendentals
+// (v_rcp, v_exp) and a 5-term Horner polynomial, against ~25 instructions for erff
+TURTLE_DEV float erf_fast(float x) {
+  const float a = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, a, 1.f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  p *= t;
+  const float e = __builtin_amdgcn_exp2f(-a * a * 1.4426950408889634f);
+  return copysignf(fmaf(-p, e, 1.f), x);
+}
+TURTLE_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+
 TURTLE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
 TURTLE_DEV float wave_sum(float v) {

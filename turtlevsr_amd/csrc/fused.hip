@@ -52,20 +52,6 @@ struct F3 {
   static constexpr int BYTES = OFF_ST + 2 * 112 * 4;
 };
 
-template <typename T> struct Frag;
-template <> struct Frag<bf16> { typedef bf16x8 type; static constexpr int K = 32; };
-template <> struct Frag<float> { typedef float type; static constexpr int K = 4; };
-
-TURTLE_DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
-TURTLE_DEV f32x4 mfma(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
-
-// lane's A/B fragment of one K step from a row-major [row][k] LDS image (row = lane & 15)
-template <typename T>
-TURTLE_DEV typename Frag<T>::type frag_at(const char* row0, int rowbytes, int k0, int lane) {
-  const char* p = row0 + (lane & 15) * rowbytes;
-  if constexpr (sizeof(T) == 2) return *reinterpret_cast<const bf16x8*>(p + (k0 + (lane >> 4) * 8) * 2);
-  else return *reinterpret_cast<const float*>(p + (k0 + (lane >> 4)) * 4);
-}
 // same fragment from global memory (weights); out-of-range rows / k read the zero line
 template <typename T>
 TURTLE_DEV typename Frag<T>::type frag_glb(const T* w, int64_t ld, int row, bool rowok, int k0, int kmax, int lane) {
@@ -181,15 +167,33 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
     }
   }
   __syncthreads();
+  if (a.ln) {
+    // normalise the staged tile in place, once: x^ = (x - mu) * rstd, or x * rstd for the BiasFree
+    // LayerNorm (turtle_t1_arch.py:68-80; packed with ln_s = null) (the LN affine is folded into
+    // W1 / the GEMM1 bias). Out-of-image and padding rows are zero and stay zero. In bf16 this
+    // rounds x^ to bf16 like the reference's autocast LayerNorm output.
+    const int cv = C / VEC;
+    for (int v = tid; v < 112 * cv; v += 256) {
+      const int r = v / cv, k = (v - r * cv) * VEC;
+      T* p = reinterpret_cast<T*>(sX + r * F::XROW) + k;
+      Vec<T> x; x.load(p);
+      const float mu = a.ln_s ? s_mu[r] : 0.f, rs = s_rs[r];   // BiasFree LN: x * rstd, uncentred
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) x.v[i] = (x.v[i] - mu) * rs;
+      x.store(p);
+    }
+    __syncthreads();
+  }
 
-  // per-lane constants of the GEMM1 epilogue: haloed row validity of each M tile
-  unsigned inimg_mask = 0;
+  // per-lane constants of the GEMM1 epilogue: 1 for haloed rows inside the image (the bias is
+  // added there only; the depthwise conv zero-pads its input at the image border)
+  float rowin[FMT];
 #pragma unroll
   for (int t = 0; t < FMT; ++t) {
     const int r = t * 16 + (lane & 15);
     const int hy = r / FH, hx = r - hy * FH;
     const int y = ty0 - 1 + hy, x = tx0 - 1 + hx;
-    if (r < FNH && y >= 0 && y < a.H && x >= 0 && x < a.W) inimg_mask |= 1u << t;
+    rowin[t] = (r < FNH && y >= 0 && y < a.H && x >= 0 && x < a.W) ? 1.f : 0.f;
   }
   // lane = output pixel in the depthwise stage
   const int oy = lane >> 3, ox = lane & 7;
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
     // W1 fragments and the lane's 4 epilogue columns (4(l>>4)..+3) of slice s, fetched one
     // slice ahead so their L2 latency hides behind the previous slice's depthwise stage
     FR wf[K1];
-    uint4 es, et, eb;
+    uint4 et, eb;
     const int c4 = (lane >> 4) * 4;
     auto fetch = [&](int s) {
       const int wr = w1row(s, lane & 15);
@@ -215,15 +219,14 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
       }
       const int er = w1row(s, c4);                      // 4 consecutive W1 rows
       const float* zf = reinterpret_cast<const float*>(g_zero_fused);
-      es = ld16(a.ln_s ? reinterpret_cast<const void*>(a.ln_s + er) : zf);
       et = ld16(a.ln_t ? reinterpret_cast<const void*>(a.ln_t + er) : zf);
       eb = ld16(a.b1 ? reinterpret_cast<const void*>(a.b1 + er) : zf);
     };
     if (s_beg + wid < s_end) fetch(s_beg + wid);
     for (int s = s_beg + wid; s < s_end; s += 4) {
-      const float fs[4] = {__uint_as_float(es.x), __uint_as_float(es.y), __uint_as_float(es.z), __uint_as_float(es.w)};
-      const float ft[4] = {__uint_as_float(et.x), __uint_as_float(et.y), __uint_as_float(et.z), __uint_as_float(et.w)};
-      const float fb[4] = {__uint_as_float(eb.x), __uint_as_float(eb.y), __uint_as_float(eb.z), __uint_as_float(eb.w)};
+      // GEMM1 column bias: LN shift (W.b, 0 without LN) + conv bias
+      const float fe[4] = {__uint_as_float(et.x) + __uint_as_float(eb.x), __uint_as_float(et.y) + __uint_as_float(eb.y),
+                           __uint_as_float(et.z) + __uint_as_float(eb.z), __uint_as_float(et.w) + __uint_as_float(eb.w)};
       // GEMM1: 16 columns x 7 row tiles
       f32x4 acc1[FMT];
 #pragma unroll
@@ -240,16 +243,9 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int t = 0; t < FMT; ++t) {
         const int r = t * 16 + (lane & 15);
-        const float mu = a.ln ? s_mu[r] : 0.f, rs = a.ln ? s_rs[r] : 1.f;
-        const bool inimg = (inimg_mask >> t) & 1u;
         float v[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float z = acc1[t][q];
-          if (a.ln) z = rs * (z - mu * fs[q]) + ft[q];
-          z += fb[q];
-          v[q] = inimg ? z : 0.f;
-        }
+        for (int q = 0; q < 4; ++q) v[q] = fmaf(rowin[t], fe[q], acc1[t][q]);   // rows outside: acc = 0
         if constexpr (sizeof(T) == 4) {
           *reinterpret_cast<float4*>(sHw + r * F::HROW + c4 * 4) = make_float4(v[0], v[1], v[2], v[3]);
         } else {
@@ -261,37 +257,75 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
       // view of the data dependence through LDS needs a fence
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      // depthwise 3x3 at pixel (oy, ox): 16 channels, wave-uniform tap weights (scalar loads)
+      // depthwise 3x3 at pixel (oy, ox): 16 channels, wave-uniform tap weights (scalar loads,
+      // issued one step ahead; uniform offsets computed on the scalar unit)
       float d[16];
-      const int wr0 = w1row(s, 0), wr8 = w1row(s, 8);   // rows of channels 0-7 and 8-15
-      f32x8 cw0, cw8;                                   // current tap's weights (SGPRs)
+      const int wr0 = __builtin_amdgcn_readfirstlane(w1row(s, 0));   // rows of channels 0-7
+      const int wr8 = __builtin_amdgcn_readfirstlane(w1row(s, 8));   //   and 8-15
       {
         const float* zf = reinterpret_cast<const float*>(g_zero_fused);
         f32x8 b0, b8;
         sload2x8(a.dwb ? a.dwb + wr0 : zf, a.dwb ? a.dwb + wr8 : zf, b0, b8);
-        sload2x8(a.dww + wr0, a.dww + wr8, cw0, cw8);
         sload_wait(b0, b8);
 #pragma unroll
         for (int i = 0; i < 8; ++i) { d[i] = b0[i]; d[8 + i] = b8[i]; }
       }
+      if constexpr (sizeof(T) == 2) {
+        // bf16: taps in pairs through v_dot2_f32_bf16 - per channel pair and tap pair, two
+        // v_perm_b32 gather {x_t[c], x_t+1[c]} and two dot2 accumulate (half the VALU work of
+        // unpack + fma); weights are the packed [5][N1] tap-pair table
+        typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+        const float* w2f = reinterpret_cast<const float*>(a.dww2);
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const char* hr = sHw + ((oy + tap / 3) * FH + ox + tap % 3) * F::HROW;
-        float v[16];
+        for (int tp = 0; tp < 5; ++tp) {
+          f32x8 cw0, cw8;                               // scalar-cache hits: loaded per tap pair
+          sload2x8(w2f + tp * a.N1 + wr0, w2f + tp * a.N1 + wr8, cw0, cw8);
+          const int t0 = 2 * tp, t1 = 2 * tp + 1;
+          const char* ha = sHw + ((oy + t0 / 3) * FH + ox + t0 % 3) * F::HROW;
+          const char* hb = sHw + ((oy + t1 / 3) * FH + ox + t1 % 3) * F::HROW;
+          uint32_t A[8], Bv[8];
+          {
+            const uint4 a0 = *reinterpret_cast<const uint4*>(ha), a1 = *reinterpret_cast<const uint4*>(ha + 16);
+            A[0] = a0.x; A[1] = a0.y; A[2] = a0.z; A[3] = a0.w; A[4] = a1.x; A[5] = a1.y; A[6] = a1.z; A[7] = a1.w;
+            if (t1 < 9) {
+              const uint4 b0 = *reinterpret_cast<const uint4*>(hb), b1 = *reinterpret_cast<const uint4*>(hb + 16);
+              Bv[0] = b0.x; Bv[1] = b0.y; Bv[2] = b0.z; Bv[3] = b0.w; Bv[4] = b1.x; Bv[5] = b1.y; Bv[6] = b1.z; Bv[7] = b1.w;
+            } else {
 #pragma unroll
-        for (int c0 = 0; c0 < 16; c0 += VEC) unpack8<T>(*reinterpret_cast<const uint4*>(hr + c0 * ES), v + c0);
-        sload_wait(cw0, cw8);
-        f32x8 nw0, nw8;                                 // next tap's weights in flight
-        if (tap < 8) sload2x8(a.dww + (int64_t)(tap + 1) * a.N1 + wr0, a.dww + (int64_t)(tap + 1) * a.N1 + wr8, nw0, nw8);
+              for (int j = 0; j < 8; ++j) Bv[j] = 0u;
+            }
+          }
+          sload_wait(cw0, cw8);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          d[i] = fmaf(cw0[i], v[i], d[i]);
-          d[8 + i] = fmaf(cw8[i], v[8 + i], d[8 + i]);
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t p0 = __builtin_amdgcn_perm(Bv[j], A[j], 0x05040100u);   // {x_t[2j],   x_t+1[2j]}
+            const uint32_t p1 = __builtin_amdgcn_perm(Bv[j], A[j], 0x07060302u);   // {x_t[2j+1], x_t+1[2j+1]}
+            const float wlo = j < 4 ? cw0[2 * j] : cw8[2 * j - 8], whi = j < 4 ? cw0[2 * j + 1] : cw8[2 * j - 7];
+            d[2 * j] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, p0), __builtin_bit_cast(bf16x2, wlo), d[2 * j], false);
+            d[2 * j + 1] = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, p1), __builtin_bit_cast(bf16x2, whi), d[2 * j + 1], false);
+          }
+#pragma unroll
+          for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(d[i]));
         }
-        if (tap < 8) { cw0 = nw0; cw8 = nw8; }
-        // one tap's operands live at a time (else every tap's LDS values stay in VGPRs)
+      } else {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(d[i]));
+        for (int tap = 0; tap < 9; ++tap) {
+          f32x8 cw0, cw8;                               // scalar-cache hits: loaded per tap
+          sload2x8(a.dww + tap * a.N1 + wr0, a.dww + tap * a.N1 + wr8, cw0, cw8);
+          const char* hr = sHw + ((oy + tap / 3) * FH + ox + tap % 3) * F::HROW;
+          float v[16];
+#pragma unroll
+          for (int c0 = 0; c0 < 16; c0 += VEC) unpack8<T>(*reinterpret_cast<const uint4*>(hr + c0 * ES), v + c0);
+          sload_wait(cw0, cw8);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            d[i] = fmaf(cw0[i], v[i], d[i]);
+            d[8 + i] = fmaf(cw8[i], v[8 + i], d[8 + i]);
+          }
+          // one tap's operands live at a time (else every tap's LDS values stay in VGPRs)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(d[i]));
+        }
       }
       if constexpr (MODE == F_DWONLY) {
         const int y = ty0 + oy, x = tx0 + ox;
@@ -325,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
 #pragma unroll
           for (int i0 = 0; i0 < 8; i0 += VEC) {
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_erf(d[i0 + i]) * d[8 + i0 + i];
+            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_fast(d[i0 + i]) * d[8 + i0 + i];
             gv.store(g + i0);
           }
         } else {
@@ -333,7 +367,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
           for (int i0 = 0; i0 < 16; i0 += VEC) {
             Vec<T> gv;
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_erf(d[i0 + i]);
+            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_fast(d[i0 + i]);
             gv.store(g + i0);
           }
         }

@@ -62,23 +62,33 @@ struct SabScoreArgs {
   int64_t q_bstride;
   const void* k[TURTLE_MAX_T];     // frame t: [N][d] for batch 0
   int64_t k_bstride[TURTLE_MAX_T];
-  int B, T, N, d;
+  int B, T, N, d, th, tw;
+  int nsplit;                      // key range split across blocks (partial top-5 lists)
   const float* tau;                // temperature (device scalar)
-  float* topv;                     // [B][T][N][5]
+  float* topv;                     // [B*T][nsplit][N][5]
   int* topi;
+  float* ballv;                    // [B*T][N][41] scores of the L1-ball keys (|di|+|dj| <= 4)
 };
 template <typename T> void launch_sab_score(const SabScoreArgs& a, hipStream_t st);
+int sab_score_nsplit(int B, int T, int N);
 
-struct SabAvArgs {
-  const void* q; int64_t q_bstride;
-  const void* k[TURTLE_MAX_T]; int64_t k_bstride[TURTLE_MAX_T];
+constexpr int SAB_MAXC = 48;       // candidate slots per query (41 ball + 5 top-k, padded)
+struct SabPrepArgs {               // candidates + clipped softmax per (b, t, query)
+  const float* topv; const int* topi; const float* ballv;
+  int BT, N, th, tw, nsplit;
+  int* cnt;                        // [BT][N] surviving candidates
+  int* ci;                         // [BT][N][SAB_MAXC] key index (padding: the query's own index)
+  float* cw;                       //                   softmax weight (padding: 0)
+};
+void launch_sab_prep(const SabPrepArgs& a, hipStream_t st);
+
+struct SabGatherArgs {             // out = sum_c w_c v[key_c], dilated token -> pixel regroup
   const void* v[TURTLE_MAX_T]; int64_t v_bstride[TURTLE_MAX_T];   // [N][ws*ws*C]
-  int B, T, N, d, th, tw, ws, C;
-  const float* tau;
-  const float* topv; const int* topi;
+  int B, T, N, th, tw, ws, C;
+  const int* cnt; const int* ci; const float* cw;
   void* out;                       // [B*T][Hl][Wl][C] pixel-major
 };
-template <typename T> void launch_sab_av(const SabAvArgs& a, hipStream_t st);
+template <typename T> void launch_sab_gather(const SabGatherArgs& a, hipStream_t st);
 
 #define TURTLE_MAX_SEG 6
 struct GramSeg {                   // ch key columns per head from a pixel-major source
@@ -158,6 +168,7 @@ struct FusedArgs {                 // fused.hip: [LN ->] pw -> dw3x3 -> [act -> 
   const void* w1; int N1;          // [N1][C]
   int ln; const float* ln_s; const float* ln_t; const float* b1;
   const float* dww; const float* dwb;   // [9][N1], [N1]
+  const uint32_t* dww2;            // bf16 tap pairs [5][N1] (bf16 path: v_dot2_f32_bf16)
   int hidden;                      // F_GATE: N1/2, else N1
   int mode;
   const void* w2; int N2;          // [N2][hidden], N2 <= 128

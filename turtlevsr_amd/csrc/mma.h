@@ -61,4 +61,20 @@ TURTLE_DEV void mma_step<float>(const char* sW, const char* sX, int lane, int ks
         acc[tm][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[tn], b[tm], acc[tm][tn], 0, 0, 0);
 }
 
+// single-step MFMA operand fragments (A or B, 16 rows x one K step), per storage type
+template <typename T> struct Frag;
+template <> struct Frag<bf16> { typedef bf16x8 type; static constexpr int K = 32; };
+template <> struct Frag<float> { typedef float type; static constexpr int K = 4; };
+
+TURTLE_DEV f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0); }
+TURTLE_DEV f32x4 mfma(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+
+// lane's fragment of one K step from a row-major [row][k] LDS image (row = lane & 15)
+template <typename T>
+TURTLE_DEV typename Frag<T>::type frag_at(const char* row0, int rowbytes, int k0, int lane) {
+  const char* p = row0 + (lane & 15) * rowbytes;
+  if constexpr (sizeof(T) == 2) return *reinterpret_cast<const bf16x8*>(p + (k0 + (lane >> 4) * 8) * 2);
+  else return *reinterpret_cast<const float*>(p + (k0 + (lane >> 4)) * 4);
+}
+
 }  // namespace turtle

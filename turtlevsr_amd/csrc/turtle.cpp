@@ -199,7 +199,7 @@ static void build_arch(Arch& A) {
 // packed weights
 // ------------------------------------------------------------------------------------------
 struct GemmW { size_t w = NONE, s = NONE, t = NONE, bias = NONE, scale = NONE; int N = 0, K = 0; bool ln = false; };
-struct DwW { size_t w = NONE, bias = NONE; int C = 0; };
+struct DwW { size_t w = NONE, bias = NONE, w2 = NONE; int C = 0; };   // w2: bf16 tap pairs [5][C] (u32)
 struct BlockW {
   GemmW a_in, a_out, q2, k2, kv, f_in, f_out;
   DwW a_dw, sab_qk_dw, sab_v_dw, fhr_dw, kv_dw, f_dw, chm_dw6;
@@ -223,6 +223,29 @@ struct Packer {
     float* p = reinterpret_cast<float*>(host.data() + o);
     for (size_t i = 0; i < v.size(); ++i) p[i] = (float)v[i];
     return o;
+  }
+  size_t u32(const std::vector<uint32_t>& v) {
+    size_t o = align();
+    host.resize(o + v.size() * 4);
+    std::memcpy(host.data() + o, v.data(), v.size() * 4);
+    return o;
+  }
+  static uint16_t bf16_bits(double x) {
+    float f = (float)x;
+    uint32_t u; std::memcpy(&u, &f, 4);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  }
+  // depthwise 3x3 table [9][C] -> bf16 tap pairs [5][C]: lo = tap 2i, hi = tap 2i+1 (0 for tap 9),
+  // the operand layout of v_dot2_f32_bf16 in the fused kernel's depthwise stage
+  size_t dw_pairs(const std::vector<double>& w9, int C) {
+    std::vector<uint32_t> o((size_t)5 * C);
+    for (int i = 0; i < 5; ++i)
+      for (int c = 0; c < C; ++c) {
+        const uint32_t lo = bf16_bits(w9[(size_t)(2 * i) * C + c]);
+        const uint32_t hi = 2 * i + 1 < 9 ? bf16_bits(w9[(size_t)(2 * i + 1) * C + c]) : 0u;
+        o[(size_t)i * C + c] = lo | (hi << 16);
+      }
+    return u32(o);
   }
   // storage-typed matrix; returns offset and writes back the rounded values (for LN rowsums)
   size_t stor(std::vector<double>& v) {
@@ -319,6 +342,7 @@ static DwW pack_dw(TurtleHandle* h, Packer& pk, const std::string& n, int c0, in
   for (int c = 0; c < C; ++c)
     for (int t = 0; t < taps; ++t) o[(size_t)t * C + c] = w[(size_t)(c0 + c) * taps + t];
   DwW d; d.C = C; d.w = pk.f32(o);
+  if (taps == 9) d.w2 = pk.dw_pairs(o, C);
   if (has(h, n + ".bias")) {
     const auto& b = W(h, n + ".bias");
     d.bias = pk.f32(std::vector<double>(b.begin() + c0, b.begin() + c0 + C));
@@ -343,6 +367,7 @@ static DwW pack_dw_cat(TurtleHandle* h, Packer& pk, const std::vector<std::strin
     c0 += cs[i];
   }
   DwW d; d.C = Ct; d.w = pk.f32(o);
+  d.w2 = pk.dw_pairs(o, Ct);
   if (any_bias) d.bias = pk.f32(bias);
   return d;
 }
@@ -584,6 +609,8 @@ struct Runner {
     f.x = x; f.ldx = ldx; f.offx = offx; f.C = C; f.nimg = nimg; f.H = H; f.W = Wd;
     f.w1 = h->ptr(w1.w); f.N1 = w1.N; f.ln = w1.ln; f.ln_s = h->fptr(w1.s); f.ln_t = h->fptr(w1.t); f.b1 = h->fptr(w1.bias);
     f.dww = h->fptr(dwp.w); f.dwb = h->fptr(dwp.bias); f.hidden = hidden; f.mode = mode;
+    f.dww2 = reinterpret_cast<const uint32_t*>(h->ptr(dwp.w2));
+    if (!f.dww2) TFAIL(TURTLE_EINVAL, "fused: depthwise weights without the tap-pair table");
     double px = (double)nimg * H * Wd;
     double bytes = ES * px * C, flops = 2.0 * px * C * w1.N + 18.0 * px * w1.N;
     if (w2) {
@@ -774,8 +801,13 @@ struct Runner {
     T* q2f = buf(P * d2);
     T* k2f = buf(P * d2);
     T* qtok = buf((int64_t)B * N * d2);
-    float* topv = fbuf((int64_t)B * NT * N * 5);
-    int* topi = reinterpret_cast<int*>(fbuf((int64_t)B * NT * N * 5));
+    const int nsplit = sab_score_nsplit(B, NT, N);
+    float* topv = fbuf((int64_t)B * NT * nsplit * N * 5);
+    int* topi = reinterpret_cast<int*>(fbuf((int64_t)B * NT * nsplit * N * 5));
+    float* ballv = fbuf((int64_t)B * NT * N * 41);
+    int* ccnt = reinterpret_cast<int*>(fbuf((int64_t)B * NT * N));
+    int* cidx = reinterpret_cast<int*>(fbuf((int64_t)B * NT * N * SAB_MAXC));
+    float* cwt = fbuf((int64_t)B * NT * N * SAB_MAXC);
     T* xs = buf(P * NT * c);
     T* kvd = buf(P * NT * 2 * c);
     // LN(x) -> [SAB qk | SAB v | FHR qkv] -> their depthwise convs; SAB v goes straight into the new
@@ -817,25 +849,32 @@ struct Runner {
       if (NT > TURTLE_MAX_T) TFAIL(TURTLE_EINVAL, "too many cached frames");
       SabScoreArgs sa{};
       sa.q = qtok; sa.q_bstride = (int64_t)N * d2; sa.B = B; sa.T = NT; sa.N = N; sa.d = d2;
-      sa.tau = h->fptr(bw.sab_tau); sa.topv = topv; sa.topi = topi;
-      SabAvArgs va{};
-      va.q = qtok; va.q_bstride = (int64_t)N * d2; va.B = B; va.T = NT; va.N = N; va.d = d2;
-      va.th = th; va.tw = tw; va.ws = ws; va.C = c; va.tau = sa.tau; va.topv = topv; va.topi = topi; va.out = xs;
+      sa.th = th; sa.tw = tw; sa.nsplit = nsplit;
+      sa.tau = h->fptr(bw.sab_tau); sa.topv = topv; sa.topi = topi; sa.ballv = ballv;
+      SabGatherArgs ga{};
+      ga.B = B; ga.T = NT; ga.N = N; ga.th = th; ga.tw = tw; ga.ws = ws; ga.C = c;
+      ga.cnt = ccnt; ga.ci = cidx; ga.cw = cwt; ga.out = xs;
       for (int t = 0; t < NT; ++t) {
         if (t < Tin) {
           sa.k[t] = kin + (int64_t)t * N * d2; sa.k_bstride[t] = (int64_t)Tin * N * d2;
-          va.v[t] = vin + (int64_t)t * N * D; va.v_bstride[t] = (int64_t)Tin * N * D;
+          ga.v[t] = vin + (int64_t)t * N * D; ga.v_bstride[t] = (int64_t)Tin * N * D;
         } else {
           sa.k[t] = kout + (int64_t)(Tnew - 1) * N * d2; sa.k_bstride[t] = (int64_t)Tnew * N * d2;
-          va.v[t] = vout + (int64_t)(Tnew - 1) * N * D; va.v_bstride[t] = (int64_t)Tnew * N * D;
+          ga.v[t] = vout + (int64_t)(Tnew - 1) * N * D; ga.v_bstride[t] = (int64_t)Tnew * N * D;
         }
-        va.k[t] = sa.k[t]; va.k_bstride[t] = sa.k_bstride[t];
       }
-      launch(TURTLE_K_SAB_SCORE, ES * (double)B * N * d2 * (1 + NT) + 8.0 * B * NT * N * 5,
+      tag("sab_score B=%d T=%d N=%d d=%d nsplit=%d", B, NT, N, d2, nsplit);
+      launch(TURTLE_K_SAB_SCORE, ES * (double)B * N * d2 * (1 + NT) + 8.0 * B * NT * N * (5 * nsplit + 41),
              2.0 * B * NT * (double)N * N * d2, [&] { launch_sab_score<T>(sa, st); });
+      SabPrepArgs pa{};
+      pa.topv = topv; pa.topi = topi; pa.ballv = ballv; pa.BT = B * NT; pa.N = N; pa.th = th; pa.tw = tw;
+      pa.nsplit = nsplit; pa.cnt = ccnt; pa.ci = cidx; pa.cw = cwt;
+      tag("sab_prep BT=%d N=%d", B * NT, N);
+      launch(TURTLE_K_SAB_AV, 4.0 * B * NT * (double)N * (10 * nsplit + 41 + 2 * SAB_MAXC), 0, [&] { launch_sab_prep(pa, st); });
       // <= 46 surviving keys per row (5 top + 41 ball): SURVEY.md §8(a) sparse A.v
-      launch(TURTLE_K_SAB_AV, ES * ((double)B * NT * N * D + (double)B * NT * HW * c) + 8.0 * B * NT * N * 5,
-             2.0 * B * NT * (double)N * 46 * D, [&] { launch_sab_av<T>(va, st); });
+      tag("sab_gather BT=%d N=%d D=%d", B * NT, N, D);
+      launch(TURTLE_K_SAB_AV, ES * ((double)B * NT * N * D + (double)B * NT * HW * c),
+             2.0 * B * NT * (double)N * 46 * D, [&] { launch_sab_gather<T>(ga, st); });
     }
     // kv = (W_kv W_po) xs over the B*T aligned frames, then dw3x3 per frame
     if (can_fuse(c, F_DWONLY, 2 * c, 0)) {
