@@ -123,6 +123,8 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
  *                 the input width is <= 128; 0: separate GEMM + depthwise launches
  *   "panel_gemm"  1 (default): panel GEMM for bf16 plain 1x1 convolutions with K <= 512;
  *                 0: K-loop GEMM everywhere
+ *   "dw_rows"     1 (default): row-sweeping depthwise 3x3 kernel (rolling 3-row window per
+ *                 thread); 0: per-pixel 9-tap gather kernel
  * Unknown names return TURTLE_EINVAL. */
 int turtle_set_option(TurtleHandle* h, const char* name, int value);
 

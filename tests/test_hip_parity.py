@@ -101,12 +101,14 @@ def test_kernel_variants_agree(dtype):
     from turtlevsr_amd.synthetic import synthetic_frames
     _, meta = load("clip_gopro_64")
     clip = synthetic_frames((1, 3, 3, 128, 128), 11)
-    ref = _run(_model(meta, "fp32").set_option("fuse", 0).set_option("panel_gemm", 0), clip)[0]
+    base = {"fuse": 0, "panel_gemm": 0, "dw_rows": 0}
+    ref = _run(_opts(_model(meta, "fp32"), base), clip)[0]
+    variants = [dict(base, fuse=f, panel_gemm=p, dw_rows=d) for f in (0, 1) for p in (0, 1) for d in (0, 1)]
     outs = {}
-    for fuse in (0, 1):
-        for panel in (0, 1):
-            m = _model(meta, dtype).set_option("fuse", fuse).set_option("panel_gemm", panel)
-            outs[(fuse, panel)] = _run(m, clip)[0]
+    for opts in variants:
+        key = tuple(sorted(opts.items()))
+        outs[key] = _run(_opts(_model(meta, dtype), opts), clip)[0]
+    k0 = tuple(sorted(base.items()))
     for key, o in outs.items():
         for j, (a, r) in enumerate(zip(o, ref)):
             if dtype == "fp32":
@@ -114,7 +116,13 @@ def test_kernel_variants_agree(dtype):
                 assert err <= 2e-4, (key, j, err)
             else:
                 assert psnr(a.numpy(), r.numpy()) >= 45.0, (key, j)
-                assert psnr(a.numpy(), outs[(0, 0)][j].numpy()) >= 50.0, (key, j)
+                assert psnr(a.numpy(), outs[k0][j].numpy()) >= 50.0, (key, j)
+
+
+def _opts(m, opts):
+    for k, v in opts.items():
+        m.set_option(k, v)
+    return m
 
 
 def test_set_option_rejects_unknown():

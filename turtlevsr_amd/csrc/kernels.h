@@ -44,6 +44,7 @@ struct DwArgs {
   int mode;
   int tok_ws;                      // > 0: SAB dilated token-major output [img][n][(p1*ws+p2)*C + c]
   int64_t tok_img_stride;          // element stride between images of the token-major output
+  int rows;                        // row-sweeping kernel (default) vs per-pixel gather
 };
 template <typename T> void launch_dw(const DwArgs& a, hipStream_t st);
 

@@ -29,9 +29,142 @@ TURTLE_DEV void unpack16<float>(const uint4& q, float (&v)[4]) {
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_dw[4];
 
+// Row-sweeping depthwise 3x3. A block owns a (32-column strip) x (DW_CC channel vectors) x (band of
+// RB rows) box of one image; thread = (column, channel vector). Walking down the band, each thread
+// keeps the 3x3 neighbourhood of its column as a rolling window of three rows in registers and
+// loads only the next row (3 vectors, the two side ones L1 hits of its neighbours' loads), one row
+// ahead of the math. Every input byte therefore leaves HBM about once (band halo 2/RB) instead of
+// the 3 row re-reads of a per-pixel gather. Tap weights of the block's channels sit in LDS (fp32).
+constexpr int DW_CC = 8;                                  // channel vectors per block
+constexpr int DW_SX = 256 / DW_CC;                        // columns per block
+template <typename T, int MODE>
+__global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstrip, int nchunk, int nband) {
+  constexpr int VEC = Vec<T>::N;
+  constexpr int NH = MODE == DW_GATE ? 2 : 1;             // gate: x1 and x2 halves
+  constexpr int CW = DW_CC * VEC;                         // channels per block
+  __shared__ __attribute__((aligned(16))) float sw[NH][9][CW];
+  const int tid = threadIdx.x;
+  const int CV = a.C / VEC;
+  const int Cw = NH * a.C;
+  int lin = blockIdx.x;
+  {
+    const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
+    lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;   // vertical neighbours share an XCD
+  }
+  const int band = lin % nband;
+  int t = lin / nband;
+  const int strip = t % nstrip;
+  t /= nstrip;
+  const int chunk = t % nchunk;
+  const int64_t img = t / nchunk;
+
+  // tap weights of this chunk -> LDS (zero past C)
+  for (int e = tid; e < NH * 9 * CW; e += 256) {
+    const int hh = e / (9 * CW), r = e - hh * 9 * CW, tap = r / CW, c = r - tap * CW;
+    const int cg = chunk * CW + c;
+    sw[hh][tap][c] = cg < a.C ? a.w[tap * Cw + hh * a.C + cg] : 0.f;
+  }
+  const int cvl = tid % DW_CC, xs = tid / DW_CC;
+  const int x = strip * DW_SX + xs, cv = chunk * DW_CC + cvl;
+  const bool live = x < a.W && cv < CV;
+  const int xc = min(x, a.W - 1), c0 = min(cv, CV - 1) * VEC;
+  const int y0 = band * RB, y1 = min(a.H, y0 + RB);
+  const T* in = reinterpret_cast<const T*>(a.in) + img * a.H * a.W * a.ldi + a.offi + c0;
+  const bool okl = xc > 0, okr = xc + 1 < a.W;
+  // one row of the window: columns x-1, x, x+1 (zero line outside the image)
+  auto load_row = [&](int y, uint4 (&r)[NH][3]) {
+    const bool oky = y >= 0 && y < a.H;
+    const T* p = in + ((int64_t)(oky ? y : 0) * a.W + xc) * a.ldi;
+#pragma unroll
+    for (int hh = 0; hh < NH; ++hh) {
+      const T* q = p + hh * a.C;
+      r[hh][0] = ld16(oky && okl ? reinterpret_cast<const void*>(q - a.ldi) : g_zero_dw);
+      r[hh][1] = ld16(oky ? reinterpret_cast<const void*>(q) : g_zero_dw);
+      r[hh][2] = ld16(oky && okr ? reinterpret_cast<const void*>(q + a.ldi) : g_zero_dw);
+    }
+  };
+  float bias[NH][VEC];
+  {
+    const float* zb = reinterpret_cast<const float*>(g_zero_dw);
+#pragma unroll
+    for (int hh = 0; hh < NH; ++hh) {
+      const float* b = a.bias ? a.bias + hh * a.C + c0 : zb;
+#pragma unroll
+      for (int i0 = 0; i0 < VEC; i0 += 4) {
+        const uint4 u = ld16(b + i0);
+        bias[hh][i0] = __uint_as_float(u.x); bias[hh][i0 + 1] = __uint_as_float(u.y);
+        bias[hh][i0 + 2] = __uint_as_float(u.z); bias[hh][i0 + 3] = __uint_as_float(u.w);
+      }
+    }
+  }
+  uint4 w0[NH][3], w1[NH][3], w2[NH][3], nx[NH][3];
+  load_row(y0 - 1, w0);
+  load_row(y0, w1);
+  load_row(y0 + 1, w2);
+  __syncthreads();
+  const int wc = cvl * VEC;
+  for (int y = y0; y < y1; ++y) {
+    if (y + 1 < y1) load_row(y + 2, nx);                  // next row in flight during the math
+    // re-read the tap weights from LDS every row (opaque offset): hoisted, they would hold
+    // 72-144 VGPRs for the whole sweep
+    int wcy = wc;
+    asm volatile("" : "+v"(wcy));
+    float acc[NH][VEC];
+#pragma unroll
+    for (int hh = 0; hh < NH; ++hh) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) acc[hh][i] = bias[hh][i];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const uint4 q = tap < 3 ? w0[hh][tap] : tap < 6 ? w1[hh][tap - 3] : w2[hh][tap - 6];
+        float v[VEC];
+        unpack16<T>(q, v);
+        const float* wt = &sw[hh][tap][wcy];
+#pragma unroll
+        for (int i0 = 0; i0 < VEC; i0 += 4) {
+          const float4 ww = *reinterpret_cast<const float4*>(wt + i0);
+          acc[hh][i0] = fmaf(ww.x, v[i0], acc[hh][i0]);
+          acc[hh][i0 + 1] = fmaf(ww.y, v[i0 + 1], acc[hh][i0 + 1]);
+          acc[hh][i0 + 2] = fmaf(ww.z, v[i0 + 2], acc[hh][i0 + 2]);
+          acc[hh][i0 + 3] = fmaf(ww.w, v[i0 + 3], acc[hh][i0 + 3]);
+        }
+        // one tap's weights / unpacked values live at a time (the scheduler would otherwise
+        // hoist all 9 taps' LDS reads and unpacks: 200+ VGPRs, one wave per SIMD)
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) asm volatile("" : "+v"(acc[hh][i]));
+      }
+    }
+    if (live) {
+      Vec<T> o;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        float r = acc[0][i];
+        if (MODE == DW_GELU) r = gelu_erf(r);
+        else if (MODE == DW_GATE) r = gelu_erf(r) * acc[NH - 1][i];
+        o.v[i] = r;
+      }
+      const int64_t pix = (img * a.H + y) * a.W + x;
+      int64_t dst;
+      if (a.tok_ws > 0) {
+        const int ws = a.tok_ws, h = a.H / ws, w = a.W / ws;
+        const int p1 = y / h, i = y - p1 * h, p2 = x / w, j = x - p2 * w;
+        dst = img * a.tok_img_stride + ((int64_t)i * w + j) * ((int64_t)ws * ws * a.C) + (int64_t)(p1 * ws + p2) * a.C + c0;
+      } else {
+        dst = pix * a.ldo + a.offo + c0;
+      }
+      o.store(reinterpret_cast<T*>(a.out) + dst);
+    }
+#pragma unroll
+    for (int hh = 0; hh < NH; ++hh)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { w0[hh][k] = w1[hh][k]; w1[hh][k] = w2[hh][k]; w2[hh][k] = nx[hh][k]; }
+  }
+}
+
 // one thread = one pixel x VEC channels; the 9 (18 for the gate) neighbour vectors are loaded
 // unconditionally (out-of-image taps read a zero line), so all of them are in flight together.
 // Block ids are remapped so each XCD sweeps a contiguous band of rows (vertical reuse in its L2).
+// Kept as the reference variant behind turtle_set_option("dw_rows", 0).
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
   constexpr int VEC = Vec<T>::N;
@@ -111,6 +244,20 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
 
 template <typename T>
 void launch_dw(const DwArgs& a, hipStream_t st) {
+  if (a.rows) {
+    const int CV = a.C / Vec<T>::N;
+    const int nstrip = (a.W + DW_SX - 1) / DW_SX, nchunk = (CV + DW_CC - 1) / DW_CC;
+    // band height: tall bands (halo 2/RB) while the grid still has >= ~8 blocks per CU
+    int RB = 32;
+    auto nblk = [&](int rb) { return (int64_t)a.nimg * nchunk * nstrip * ((a.H + rb - 1) / rb); };
+    while (RB > 4 && nblk(RB) < 2048) RB /= 2;
+    const int nband = (a.H + RB - 1) / RB;
+    const dim3 grid((unsigned)nblk(RB));
+    if (a.mode == DW_GATE) hipLaunchKernelGGL((dw_rows_kernel<T, DW_GATE>), grid, dim3(256), 0, st, a, RB, nstrip, nchunk, nband);
+    else if (a.mode == DW_GELU) hipLaunchKernelGGL((dw_rows_kernel<T, DW_GELU>), grid, dim3(256), 0, st, a, RB, nstrip, nchunk, nband);
+    else hipLaunchKernelGGL((dw_rows_kernel<T, DW_PLAIN>), grid, dim3(256), 0, st, a, RB, nstrip, nchunk, nband);
+    return;
+  }
   const int64_t total = (int64_t)a.nimg * a.H * a.W * (a.C / Vec<T>::N);
   const int64_t blocks = (total + 255) / 256;
   if (a.mode == DW_GATE) hipLaunchKernelGGL((dw_kernel<T, DW_GATE>), dim3((unsigned)blocks), dim3(256), 0, st, a);

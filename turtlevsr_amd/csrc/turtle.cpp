@@ -286,6 +286,7 @@ struct TurtleHandle {
   bool loaded = false;
   bool fuse = getenv("TURTLE_NO_FUSE") == nullptr;   // block-level fused kernels (fused.hip)
   bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
+  bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
   const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
   const float* fptr(size_t off) const { return reinterpret_cast<const float*>(ptr(off)); }
@@ -595,7 +596,7 @@ struct Runner {
     a.in = in; a.ldi = ldi; a.offi = offi; a.out = out; a.ldo = ldo; a.offo = offo;
     a.w = h->fptr(w.w); a.bias = h->fptr(w.bias);
     a.nimg = nimg; a.H = H; a.W = Wd; a.C = mode == DW_GATE ? w.C / 2 : w.C; a.mode = mode;
-    a.tok_ws = tok_ws; a.tok_img_stride = tok_stride;
+    a.tok_ws = tok_ws; a.tok_img_stride = tok_stride; a.rows = h->dw_rows;
     const double px = (double)nimg * H * Wd, cin = mode == DW_GATE ? 2.0 * a.C : a.C;
     tag("dw nimg=%d H=%d W=%d C=%d mode=%d tok=%d", nimg, H, Wd, a.C, mode, tok_ws);
     launch(TURTLE_K_DW, ES * px * (cin + a.C), 18.0 * px * cin, [&] { launch_dw<T>(a, st); });
@@ -1061,6 +1062,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     const std::string n = name;
     if (n == "fuse") h->fuse = value != 0;
     else if (n == "panel_gemm") h->panel = value != 0;
+    else if (n == "dw_rows") h->dw_rows = value != 0;
     else TFAIL(TURTLE_EINVAL, "unknown option '" + n + "'");
   });
 }
