@@ -123,6 +123,8 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
  *                 the input width is <= 128; 0: separate GEMM + depthwise launches
  *   "panel_gemm"  1 (default): panel GEMM for bf16 plain 1x1 convolutions with K <= 512;
  *                 0: K-loop GEMM everywhere
+ *   "gemm_lds"    1 (default): LDS-pipelined bf16 GEMM (global_load_lds double buffering)
+ *                 wherever its alignment rules hold; 0: panel / K-loop GEMMs
  *   "dw_rows"     1 (default): row-sweeping depthwise 3x3 kernel (rolling 3-row window per
  *                 thread); 0: per-pixel 9-tap gather kernel
  * Unknown names return TURTLE_EINVAL. */

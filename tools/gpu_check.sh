@@ -12,4 +12,10 @@ rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/t.log
 rm -f gpurun_out/launches.tsv
 TURTLE_PROF_DUMP=gpurun_out/launches.tsv timeout -k 10 200 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-psnr > gpurun_out/b2.log 2>&1 || exit $?
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b.log 2>&1
-rc=$?; tail -1 gpurun_out/b.log; exit $rc
+rc=$?; tail -1 gpurun_out/b.log; [ $rc -ne 0 ] && exit $rc
+# (optional) kernel-trace summary of a short run: GPU_CHECK_PROF=1
+if [ -n "$GPU_CHECK_PROF" ]; then
+  rm -rf gpurun_out/prof
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-psnr > gpurun_out/p.log 2>&1
+  echo "prof rc=$?"
+fi

@@ -3,8 +3,9 @@
 //
 //   1. gram:      split over pixels, per (batch, head): G = q^T [k_seg0 | k_seg1 | ...] and the
 //                 per-channel sums of squares (for F.normalize over HW), fp32 MFMA 16x16x4.
-//   2. finalize:  reduce the pixel splits, logits = G / (|q_i| |k_j|) * temperature, row softmax
-//                 (over all cached + current key rows of the head), 1/|k_cur| for the FHR cache.
+//   2. rows:      reduce the pixel-chunk partials (deterministic order), logits =
+//                 G / (|q_i| |k_j|) * temperature, row softmax (over all cached + current key
+//                 rows of the head), 1/|k_cur| for the FHR cache.
 //   3. weff:      fold attention into the projection: W_eff = project_out . blockdiag(A_h), so
 //                 project_out(A v) becomes ONE pointwise GEMM over the K-concatenated value
 //                 sources (current v, cached v rows, CHM history frames) with the residual add
@@ -17,9 +18,7 @@ namespace turtle {
 #ifndef TURTLE_GRAM_TR
 #define TURTLE_GRAM_TR 1
 #endif
-template <typename T> constexpr int gram_gp() { return sizeof(T) == 2 ? 32 : 16; }  // pixels per step
 constexpr int GMAXT = 24;        // max 16x16 accumulator tiles per wave (ch=64, 6 segments)
-constexpr int GMAXV = 7;         // max 16-byte staging vectors per thread per step
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_gram[4];
 
@@ -27,10 +26,15 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_gram[4];
 // LDS holds [pixel][channel] tiles exactly as they sit in HBM (16-byte row chunks); the MFMA
 // operands need 8 consecutive pixels of one channel per lane, which ds_read_b64_tr_b16 delivers
 // (two 4-row transposed reads), so nothing is transposed in registers.
-template <typename T>
+// Staging: thread t owns channel vector cv = t % CVt of pixel rows t / CVt + PS u (PS = 256 / CVt
+// rows per pass, up to GNU passes), so its sum of squares is a single VEC accumulator; a step of
+// GP pixels keeps ~16-32 KB per block in flight. MT = accumulator tiles per wave (compile time,
+// so the accumulators of a 1-segment Gram do not cost the registers of a 6-segment one).
+constexpr int GNU = 8;
+template <typename T, int GP, int MT>
 __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
-  constexpr int VEC = Vec<T>::N, ES = sizeof(T), GP = gram_gp<T>();
+  constexpr int VEC = Vec<T>::N, ES = sizeof(T);
   const int ch = a.ch, ncol = a.nseg * ch;
   const int RQ = ch * ES + 16, RK = ncol * ES + 16;          // LDS row strides (bytes)
   char* sq = gsm;                                            // [GP][RQ]
@@ -42,69 +46,69 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
   const int p_beg = chunk * a.chunk, p_end = min(a.HW, p_beg + a.chunk);
   const int tj_n = ncol / 16, TT = (ch / 16) * tj_n;
   const int qv = ch / VEC, CVt = (ch + ncol) / VEC;          // vectors per pixel
-  const int NV = GP * CVt;
+  const int PS = 256 / CVt;                                  // pixel rows per pass
+  const int cv = tid % CVt, pg = tid / CVt;
+  const bool tact = pg < PS;
 
   for (int i = tid; i < ch + ncol; i += 256) nrm[i] = 0.f;
 
-  // per-thread staging geometry (fixed across steps)
-  const T* src[GMAXV];
-  int64_t pstride[GMAXV];
-  int lds_off[GMAXV], vpx[GMAXV];
+  const T* src;
+  int64_t pst;
+  char* lrow;
+  int lstride;
+  if (cv < qv) {
+    src = reinterpret_cast<const T*>(a.q) + (int64_t)b * a.HW * a.ldq + a.qoff + h * ch + cv * VEC;
+    pst = a.ldq;
+    lrow = sq + cv * VEC * ES;
+    lstride = RQ;
+  } else {
+    const int kc = (cv - qv) * VEC, s = kc / ch, jj = kc - s * ch;
+    GramSeg g = a.seg[0];
 #pragma unroll
-  for (int j = 0; j < GMAXV; ++j) {
-    const int v = tid + 256 * j;
-    const int px = v / CVt, cv = v % CVt;
-    vpx[j] = v < NV ? px : -1;
-    if (cv < qv) {
-      src[j] = reinterpret_cast<const T*>(a.q) + (int64_t)b * a.HW * a.ldq + a.qoff + h * ch + cv * VEC;
-      pstride[j] = a.ldq;
-      lds_off[j] = px * RQ + cv * VEC * ES;
-    } else {
-      const int kc = (cv - qv) * VEC, s = kc / ch, jj = kc - s * ch;
-      const GramSeg& g = a.seg[s < a.nseg ? s : 0];
-      src[j] = reinterpret_cast<const T*>(g.base) + ((int64_t)b * g.img_mul + g.img_add) * a.HW * g.ld + g.off +
-               (int64_t)h * g.hstride + jj;
-      pstride[j] = g.ld;
-      lds_off[j] = GP * RQ + px * RK + kc * ES;
-    }
+    for (int q = 1; q < TURTLE_MAX_SEG; ++q)
+      if (s == q) g = a.seg[q];
+    src = reinterpret_cast<const T*>(g.base) + ((int64_t)b * g.img_mul + g.img_add) * a.HW * g.ld + g.off +
+          (int64_t)h * g.hstride + jj;
+    pst = g.ld;
+    lrow = sk + kc * ES;
+    lstride = RK;
   }
 
-  f32x4 acc[GMAXT];
+  f32x4 acc[MT];
 #pragma unroll
-  for (int t = 0; t < GMAXT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float sqs[GMAXV][VEC];
+  for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float sqs[VEC];
 #pragma unroll
-  for (int j = 0; j < GMAXV; ++j)
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) sqs[j][e] = 0.f;
+  for (int e = 0; e < VEC; ++e) sqs[e] = 0.f;
 
-  uint4 stg[GMAXV];
+  uint4 stg[GNU];
   auto load = [&](int p0) {
 #pragma unroll
-    for (int j = 0; j < GMAXV; ++j) {
-      const int p = p0 + vpx[j];
-      const bool ok = vpx[j] >= 0 && p < p_end;
-      stg[j] = ld16(ok ? reinterpret_cast<const void*>(src[j] + (int64_t)p * pstride[j]) : g_zero_gram);
+    for (int u = 0; u < GNU; ++u) {
+      const int px = pg + PS * u, p = p0 + px;
+      const bool ok = tact && px < GP && p < p_end;
+      stg[u] = ld16(ok ? reinterpret_cast<const void*>(src + (int64_t)p * pst) : g_zero_gram);
     }
   };
 
   load(p_beg);
   for (int p0 = p_beg; p0 < p_end; p0 += GP) {
 #pragma unroll
-    for (int j = 0; j < GMAXV; ++j) {
-      if (vpx[j] < 0) continue;
-      *reinterpret_cast<uint4*>(gsm + lds_off[j]) = stg[j];
+    for (int u = 0; u < GNU; ++u) {
+      const int px = pg + PS * u;
+      if (!tact || px >= GP) continue;
+      *reinterpret_cast<uint4*>(lrow + px * lstride) = stg[u];
       float x[VEC];
       if constexpr (sizeof(T) == 2) {
-        const uint32_t w[4] = {stg[j].x, stg[j].y, stg[j].z, stg[j].w};
+        const uint32_t w[4] = {stg[u].x, stg[u].y, stg[u].z, stg[u].w};
 #pragma unroll
         for (int i = 0; i < 4; ++i) { x[2 * i] = __uint_as_float(w[i] << 16); x[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
       } else {
-        x[0] = __uint_as_float(stg[j].x); x[1] = __uint_as_float(stg[j].y);
-        x[2] = __uint_as_float(stg[j].z); x[3] = __uint_as_float(stg[j].w);
+        x[0] = __uint_as_float(stg[u].x); x[1] = __uint_as_float(stg[u].y);
+        x[2] = __uint_as_float(stg[u].z); x[3] = __uint_as_float(stg[u].w);
       }
 #pragma unroll
-      for (int e = 0; e < VEC; ++e) sqs[j][e] = fmaf(x[e], x[e], sqs[j][e]);
+      for (int e = 0; e < VEC; ++e) sqs[e] = fmaf(x[e], x[e], sqs[e]);
     }
     __syncthreads();
     if (p0 + GP < p_end) load(p0 + GP);
@@ -114,20 +118,23 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
       typedef short v4s __attribute__((ext_vector_type(4)));
       typedef __attribute__((address_space(3))) v4s lds_v4s;
 #pragma unroll
-      for (int t = 0; t < GMAXT; ++t) {
+      for (int t = 0; t < MT; ++t) {
         const int tile = wid + 4 * t;
         if (tile < TT) {
           const int it = tile / tj_n, jt = tile - it * tj_n;
-          const char* qa = sq + (8 * g16 + qq) * RQ + (it * 16 + 4 * pp) * 2;
-          const char* ka = sk + (8 * g16 + qq) * RK + (jt * 16 + 4 * pp) * 2;
-          const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)qa);
-          const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(qa + 4 * RQ));
-          const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)ka);
-          const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(ka + 4 * RK));
-          typedef short v8s __attribute__((ext_vector_type(8)));
-          const bf16x8 af = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
-          const bf16x8 bfr = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[t], 0, 0, 0);
+#pragma unroll
+          for (int ss = 0; ss < GP / 32; ++ss) {
+            const char* qa = sq + (32 * ss + 8 * g16 + qq) * RQ + (it * 16 + 4 * pp) * 2;
+            const char* ka = sk + (32 * ss + 8 * g16 + qq) * RK + (jt * 16 + 4 * pp) * 2;
+            const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)qa);
+            const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(qa + 4 * RQ));
+            const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)ka);
+            const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(ka + 4 * RK));
+            typedef short v8s __attribute__((ext_vector_type(8)));
+            const bf16x8 af = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7));
+            const bf16x8 bfr = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr, acc[t], 0, 0, 0);
+          }
         }
       }
     } else {
@@ -135,7 +142,7 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
       for (int kk = 0; kk < GP; kk += 4) {
         const int pr = kk + (lane >> 4);
 #pragma unroll
-        for (int t = 0; t < GMAXT; ++t) {
+        for (int t = 0; t < MT; ++t) {
           const int tile = wid + 4 * t;
           if (tile < TT) {
             const int it = tile / tj_n, jt = tile - it * tj_n;
@@ -148,19 +155,16 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
     }
     __syncthreads();
   }
-  // column sums of squares: per-thread partials -> LDS atomics
+  // column sums of squares: PS threads per channel vector -> LDS atomics
+  if (tact) {
 #pragma unroll
-  for (int j = 0; j < GMAXV; ++j) {
-    if (vpx[j] < 0) continue;
-    const int cv = (tid + 256 * j) % CVt;
-#pragma unroll
-    for (int e = 0; e < VEC; ++e) atomicAdd(&nrm[cv * VEC + e], sqs[j][e]);
+    for (int e = 0; e < VEC; ++e) atomicAdd(&nrm[cv * VEC + e], sqs[e]);
   }
   __syncthreads();
   const int stride = ch * ncol + ch + ncol;
   float* out = a.part + ((int64_t)bh * a.nchunk + chunk) * stride;
 #pragma unroll
-  for (int t = 0; t < GMAXT; ++t) {
+  for (int t = 0; t < MT; ++t) {
     const int tile = wid + 4 * t;
     if (tile < TT) {
       const int it = tile / tj_n, jt = tile % tj_n;
@@ -172,120 +176,169 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
   for (int i = tid; i < ch + ncol; i += 256) out[ch * ncol + i] = nrm[i];   // [nq (ch) | nk (ncol)]
 }
 
+template <typename T, int GP, int MT>
+static void launch_gram_cfg(const GramArgs& a, hipStream_t st) {
+  const int ncol = a.nseg * a.ch;
+  const size_t lds = (size_t)GP * ((a.ch + ncol) * sizeof(T) + 32) + (a.ch + ncol) * sizeof(float);
+  hipLaunchKernelGGL((gram_kernel<T, GP, MT>), dim3((unsigned)(a.B * a.heads * a.nchunk)), dim3(256), lds, st, a);
+}
+
+template <typename T, int GP>
+static void launch_gram_gp(const GramArgs& a, hipStream_t st) {
+  const int tt = (a.ch / 16) * (a.nseg * a.ch / 16), mt = (tt + 3) / 4;
+  if (mt <= 4) launch_gram_cfg<T, GP, 4>(a, st);
+  else if (mt <= 8) launch_gram_cfg<T, GP, 8>(a, st);
+  else if (mt <= 16) launch_gram_cfg<T, GP, 16>(a, st);
+  else launch_gram_cfg<T, GP, GMAXT>(a, st);
+}
+
 template <typename T>
 void launch_gram(const GramArgs& a, hipStream_t st) {
-  const int ncol = a.nseg * a.ch;
-  const size_t lds = (size_t)gram_gp<T>() * ((a.ch + ncol) * sizeof(T) + 32) + (a.ch + ncol) * sizeof(float);
-  hipLaunchKernelGGL(gram_kernel<T>, dim3((unsigned)(a.B * a.heads * a.nchunk)), dim3(256), lds, st, a);
+  const int cvt = (a.ch + a.nseg * a.ch) / Vec<T>::N;
+  const int ps = 256 / cvt, rows = ps * GNU;                  // pixel rows GNU passes can stage
+  if constexpr (sizeof(T) == 2) {
+    if (rows >= 128) launch_gram_gp<T, 128>(a, st);
+    else if (rows >= 64) launch_gram_gp<T, 64>(a, st);
+    else launch_gram_gp<T, 32>(a, st);
+  } else {
+    launch_gram_gp<T, 16>(a, st);
+  }
 }
 
-// reduce the pixel splits in two deterministic levels: this kernel sums the chunks of split g
-// (c = g, g + S, ...) into red[bh][g][e]; the softmax kernel adds the S partial sums it reads
-__global__ __launch_bounds__(256) void gram_reduce_kernel(const float* part, float* red, int nchunk, int stride, int S) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= stride) return;
-  const int bh = blockIdx.y, g = blockIdx.z;
-  const float* p = part + ((int64_t)bh * nchunk + g) * stride + e;
-  const int64_t step = (int64_t)S * stride;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int c = g;
-  for (; c + 3 * S < nchunk; c += 4 * S, p += 4 * step) {
-    s0 += p[0]; s1 += p[step]; s2 += p[2 * step]; s3 += p[3 * step];
+// Reduce the per-chunk Gram partials: red[bh][e] = sum_c part[bh][c][e]. Block = 64 consecutive
+// entries x 4 chunk groups; each lane keeps 8 loads in flight, the 4 group sums meet in LDS
+// (fixed order: deterministic).
+__global__ __launch_bounds__(256) void gram_sum_kernel(const float* part, float* red, int nchunk, int stride) {
+  __shared__ float ps[4][64];
+  const int lane = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane, bh = blockIdx.y;
+  const int ec = min(e, stride - 1);
+  const float* p = part + (int64_t)bh * nchunk * stride + ec;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int c = grp;
+  for (; c + 28 < nchunk; c += 32) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += p[(int64_t)(c + 4 * u) * stride];
   }
-  for (; c < nchunk; c += S, p += step) s0 += p[0];
-  red[((int64_t)bh * S + g) * stride + e] = (s0 + s1) + (s2 + s3);
-}
-
-// one wave per query row i of (b, h): logits over all key columns (sum of the S partials),
-// softmax, and 1/|k_cur| for the FHR cache (turtle_t1_arch.py:357-366, 598-600)
-constexpr int SM_MAXC = 512 / 64;
-__global__ __launch_bounds__(256) void attn_softmax_kernel(AttnFinArgs a) {
-  const int ch = a.ch, ncol = a.nseg * ch, stride = ch * ncol + ch + ncol, S = a.nsplit;
-  const int bh = blockIdx.x, b = bh / a.heads, h = bh % a.heads;
-  const float* R = a.red + (int64_t)bh * S * stride;
-  auto sum_s = [&](int e) {
-    float v = 0.f;
-    for (int g = 0; g < S; ++g) v += R[(int64_t)g * stride + e];
-    return v;
-  };
-  __shared__ float kinv_s[512];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  for (int j = tid; j < ncol; j += 256) {
-    const int s = j / ch;
-    kinv_s[j] = ((a.norm_mask >> s) & 1) ? 1.f / fmaxf(sqrtf(sum_s(ch * ncol + ch + j)), 1e-12f) : 1.f;
-  }
+  for (; c < nchunk; c += 4) s[0] += p[(int64_t)c * stride];
+  ps[grp][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
   __syncthreads();
-  if (blockIdx.y == 0 && a.kinv && a.cur_seg >= 0)
-    for (int j = tid; j < ch; j += 256) a.kinv[(int64_t)b * a.heads * ch + h * ch + j] = kinv_s[a.cur_seg * ch + j];
-  const int i = blockIdx.y * 4 + wid;
+  if (grp == 0 && e < stride) red[(int64_t)bh * stride + e] = (ps[0][lane] + ps[1][lane]) + (ps[2][lane] + ps[3][lane]);
+}
+
+// Row softmax of the channel-attention logits, one wave per (query row i, b*h):
+//   A[i][j] = softmax_j( G[i][j] * tau_h / (|q_i| |k_j|) )   over all ncol key columns
+// (turtle_t1_arch.py:357-366, 686-692). Row 0 also writes 1/|k_cur| for the FHR cache.
+constexpr int AR_KC = 8;             // ncol <= 512 = 8 x 64 lanes
+__global__ __launch_bounds__(256) void attn_row_kernel(AttnFinArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6), bh = blockIdx.y, b = bh / a.heads, h = bh % a.heads;
+  const int ch = a.ch, ncol = a.nseg * ch, stride = ch * ncol + ch + ncol;
   if (i >= ch) return;
-  const float qi = a.tau[h] / fmaxf(sqrtf(sum_s(ch * ncol + i)), 1e-12f);
-  float lg[SM_MAXC];
+  const float* R = a.red + (int64_t)bh * stride;
+  float G[AR_KC], N[AR_KC];
+#pragma unroll
+  for (int k = 0; k < AR_KC; ++k) {
+    const int jc = min(lane + 64 * k, ncol - 1);
+    G[k] = R[i * ncol + jc];
+    N[k] = R[ch * ncol + ch + jc];
+  }
+  const float qn = a.tau[h] / fmaxf(sqrtf(R[ch * ncol + i]), 1e-12f);
+  float lg[AR_KC], kv[AR_KC];
   float mx = -INFINITY;
 #pragma unroll
-  for (int k = 0; k < SM_MAXC; ++k) {
+  for (int k = 0; k < AR_KC; ++k) {
     const int j = lane + 64 * k;
-    lg[k] = j < ncol ? sum_s(i * ncol + j) * qi * kinv_s[j] : -INFINITY;
+    const int sgm = min(j, ncol - 1) / ch;
+    kv[k] = ((a.norm_mask >> sgm) & 1) ? 1.f / fmaxf(sqrtf(N[k]), 1e-12f) : 1.f;
+    lg[k] = j < ncol ? G[k] * qn * kv[k] : -INFINITY;
     mx = fmaxf(mx, lg[k]);
   }
   mx = wave_max(mx);
   float sum = 0.f;
 #pragma unroll
-  for (int k = 0; k < SM_MAXC; ++k) {
+  for (int k = 0; k < AR_KC; ++k) {
     lg[k] = lane + 64 * k < ncol ? expf(lg[k] - mx) : 0.f;
     sum += lg[k];
   }
   const float inv = 1.f / wave_sum(sum);
   float* A = a.attn + ((int64_t)bh * ch + i) * ncol;
 #pragma unroll
-  for (int k = 0; k < SM_MAXC; ++k)
+  for (int k = 0; k < AR_KC; ++k)
     if (lane + 64 * k < ncol) A[lane + 64 * k] = lg[k] * inv;
+  if (i == 0 && a.kinv && a.cur_seg >= 0) {
+#pragma unroll
+    for (int k = 0; k < AR_KC; ++k) {
+      const int j = lane + 64 * k;
+      if (j >= a.cur_seg * ch && j < (a.cur_seg + 1) * ch)
+        a.kinv[(int64_t)b * a.heads * ch + h * ch + (j - a.cur_seg * ch)] = kv[k];
+    }
+  }
 }
 
-int attn_nsplit(int nchunk) { return nchunk < 32 ? nchunk : 32; }
+int attn_nsplit(int nchunk) { return 1; }
 
 void launch_attn_finalize(const AttnFinArgs& a, hipStream_t st) {
   const int ncol = a.nseg * a.ch, stride = a.ch * ncol + a.ch + ncol, nbh = a.B * a.heads;
-  hipLaunchKernelGGL(gram_reduce_kernel, dim3((unsigned)((stride + 255) / 256), (unsigned)nbh, (unsigned)a.nsplit),
-                     dim3(256), 0, st, a.part, a.red, a.nchunk, stride, a.nsplit);
-  hipLaunchKernelGGL(attn_softmax_kernel, dim3((unsigned)nbh, (unsigned)((a.ch + 3) / 4)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(gram_sum_kernel, dim3((unsigned)((stride + 63) / 64), (unsigned)nbh), dim3(256), 0, st, a.part, a.red,
+                     a.nchunk, stride);
+  hipLaunchKernelGGL(attn_row_kernel, dim3((unsigned)((a.ch + 3) / 4), (unsigned)nbh), dim3(256), 0, st, a);
 }
 
-// W_eff[b][o][seg_col[s] + h*seg_hstride[s] + j] = sum_i Wp[o][h*ch + i] * A[b,h][i][s*ch + j]
-// block = (4 output channels, b*h); threads stride the key columns, so A rows load coalesced and
-// the Wp operands are wave-uniform (scalar loads)
-constexpr int WE_OT = 4;
+// Fold the attention into the projection, one block per (32 output channels, 64 key columns,
+// b*h): W_eff[b][o][col(j)] = sum_i Wp[o][h*ch + i] * A[i][j] (A and Wp slabs staged in LDS by
+// coalesced loads), so project_out(A v) becomes one GEMM over the K-concatenated value sources.
+constexpr int WF_MAXCH = 128;
 template <typename T>
-__global__ __launch_bounds__(256) void weff_kernel(WeffArgs a) {
+__global__ __launch_bounds__(256) void attn_weff_kernel(WeffArgs a) {
+  __shared__ __attribute__((aligned(16))) float sA[WF_MAXCH][64];
+  __shared__ __attribute__((aligned(16))) float sW[WF_MAXCH][32];    // [i][o]
   const int ch = a.ch, ncol = a.nseg * ch;
-  const int o0 = blockIdx.x * WE_OT, bh = blockIdx.y, b = bh / a.heads, h = bh % a.heads;
-  T* W = reinterpret_cast<T*>(a.weff);
+  const int o0 = blockIdx.x * 32, j0 = blockIdx.y * 64, bh = blockIdx.z;
+  const int b = bh / a.heads, h = bh % a.heads;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float* A = a.attn + (int64_t)bh * ch * ncol;
-  for (int col = threadIdx.x; col < ncol; col += 256) {
-    float acc[WE_OT];
-#pragma unroll
-    for (int t = 0; t < WE_OT; ++t) acc[t] = 0.f;
-    for (int i = 0; i < ch; ++i) {
-      const float av = A[(int64_t)i * ncol + col];
-#pragma unroll
-      for (int t = 0; t < WE_OT; ++t)
-        if (o0 + t < a.C) acc[t] = fmaf(a.wp[(int64_t)(o0 + t) * a.C + h * ch + i], av, acc[t]);
-    }
-    const int sg = col / ch, jj = col - sg * ch;
-    int64_t scol = a.seg_col[0];
-    int shs = a.seg_hstride[0];
-#pragma unroll
-    for (int q = 1; q < TURTLE_MAX_SEG; ++q)
-      if (sg == q) { scol = a.seg_col[q]; shs = a.seg_hstride[q]; }
-#pragma unroll
-    for (int t = 0; t < WE_OT; ++t)
-      if (o0 + t < a.C) W[((int64_t)b * a.C + o0 + t) * a.Keff + scol + (int64_t)h * shs + jj] = from_f<T>(acc[t]);
+  for (int e = tid; e < ch * 64; e += 256) {
+    const int i = e >> 6, jj = e & 63;
+    sA[i][jj] = j0 + jj < ncol ? A[i * ncol + j0 + jj] : 0.f;
   }
+  for (int e = tid; e < 32 * ch; e += 256) {
+    const int oo = e / ch, i = e - oo * ch;
+    sW[i][oo] = o0 + oo < a.C ? a.wp[(int64_t)(o0 + oo) * a.C + h * ch + i] : 0.f;
+  }
+  __syncthreads();
+  const int jj = lane, og = wid * 8;
+  float acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = 0.f;
+  for (int i = 0; i < ch; ++i) {
+    const float av = sA[i][jj];
+    const float4 w0 = *reinterpret_cast<const float4*>(&sW[i][og]);
+    const float4 w1 = *reinterpret_cast<const float4*>(&sW[i][og + 4]);
+    acc[0] = fmaf(w0.x, av, acc[0]); acc[1] = fmaf(w0.y, av, acc[1]);
+    acc[2] = fmaf(w0.z, av, acc[2]); acc[3] = fmaf(w0.w, av, acc[3]);
+    acc[4] = fmaf(w1.x, av, acc[4]); acc[5] = fmaf(w1.y, av, acc[5]);
+    acc[6] = fmaf(w1.z, av, acc[6]); acc[7] = fmaf(w1.w, av, acc[7]);
+  }
+  const int col = j0 + jj;
+  if (col >= ncol) return;
+  const int sg = col / ch, j = col - sg * ch;
+  int64_t scol = a.seg_col[0];
+  int shs = a.seg_hstride[0];
+#pragma unroll
+  for (int q = 1; q < TURTLE_MAX_SEG; ++q)
+    if (sg == q) { scol = a.seg_col[q]; shs = a.seg_hstride[q]; }
+  T* W = reinterpret_cast<T*>(a.weff) + (int64_t)b * a.C * a.Keff + scol + (int64_t)h * shs + j;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (o0 + og + u < a.C) W[(int64_t)(o0 + og + u) * a.Keff] = from_f<T>(acc[u]);
 }
 
 template <typename T>
 void launch_weff(const WeffArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(weff_kernel<T>, dim3((unsigned)((a.C + WE_OT - 1) / WE_OT), (unsigned)(a.B * a.heads)), dim3(256), 0, st, a);
+  const int ncol = a.nseg * a.ch;
+  hipLaunchKernelGGL(attn_weff_kernel<T>, dim3((unsigned)((a.C + 31) / 32), (unsigned)((ncol + 63) / 64), (unsigned)(a.B * a.heads)),
+                     dim3(256), 0, st, a);
 }
 
 template void launch_gram<float>(const GramArgs&, hipStream_t);

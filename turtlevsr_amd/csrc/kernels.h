@@ -31,8 +31,11 @@ struct GemmArgs {
   const float* zeros;              // >= 16384 zero floats / 8192 ones (absent vectors, residual)
   const float* ones;
   int allow_panel;                 // panel kernel permitted (turtle_set_option "panel_gemm")
+  int allow_lds;                   // LDS-pipelined kernel permitted (turtle_set_option "gemm_lds")
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
+bool gemm_lds_ok(const GemmArgs& g);                              // gemm2.hip (bf16)
+void launch_gemm_lds(const GemmArgs& g, hipStream_t st);
 
 enum DwMode { DW_PLAIN = 0, DW_GELU = 1, DW_GATE = 2 };
 struct DwArgs {
@@ -103,22 +106,22 @@ struct GramArgs {
 };
 template <typename T> void launch_gram(const GramArgs& a, hipStream_t st);
 
-struct AttnFinArgs {
+struct AttnFinArgs {               // per-row Gram reduction + softmax
   const float* part; int nchunk;
-  int nsplit;                      // first-level reduction splits (attn_nsplit(nchunk))
   int B, heads, ch, nseg;
   unsigned norm_mask;              // bit s: segment s is L2-normalised over HW
   const float* tau;                // [heads]
-  float* red;                      // scratch [B*heads][nsplit][ch*ncol + ch + ncol]
-  float* attn;                     // [B*heads][ch][ncol]
   float* kinv;                     // [B][heads*ch] 1/max(|k_cur|,eps) of segment `cur_seg`, or null
   int cur_seg;
+  float* red;                      // scratch [B*heads][ch*ncol + ch + ncol] summed partials
+  float* attn;                     // [B*heads][ch][ncol]
 };
 void launch_attn_finalize(const AttnFinArgs& a, hipStream_t st);
 int attn_nsplit(int nchunk);
 
 struct WeffArgs {                  // W_eff[b][o][col] = sum_i Wp[o][h*ch+i] * A[b][h][i][seg*ch+j]
-  const float* attn; const float* wp;   // wp fp32 [C][C]
+  const float* attn;               // softmaxed attention [B*heads][ch][ncol]
+  const float* wp;                 // wp fp32 [C][C]
   int B, heads, ch, nseg, C;
   int64_t seg_col[TURTLE_MAX_SEG]; // column of (seg, h=0, j=0) in W_eff
   int seg_hstride[TURTLE_MAX_SEG]; // column step per head

@@ -287,6 +287,7 @@ struct TurtleHandle {
   bool fuse = getenv("TURTLE_NO_FUSE") == nullptr;   // block-level fused kernels (fused.hip)
   bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
+  bool gemm_lds = true;                               // LDS-pipelined bf16 GEMM (gemm2.hip)
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
   const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
   const float* fptr(size_t off) const { return reinterpret_cast<const float*>(ptr(off)); }
@@ -578,7 +579,7 @@ struct Runner {
     g.bias = bias ? bias : h->fptr(w.bias); g.scale = h->fptr(w.scale); g.gelu = gelu;
     g.res = res; g.ldr = ldr; g.offr = offr;
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store;
-    g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel;
+    g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel; g.allow_lds = h->gemm_lds;
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
     // algorithmic traffic: A once (a 3x3 reads each input pixel once), W per weight set, out
     // (+ residual) once
@@ -648,18 +649,19 @@ struct Runner {
                  const SrcList& vsrc, int HW, int Wimg, T* x, float* kinv, int cur_seg) {
     const int c = b.dim, ch = c / b.heads, nseg = (int)segs.size(), ncol = nseg * ch;
     if (ncol > 512 || nseg > TURTLE_MAX_SEG) TFAIL(TURTLE_EINVAL, "channel attention: more than 512 key columns");
-    // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each
+    // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each, whole
+    // 128-pixel steps of the bf16 Gram
     int nchunk = std::max(1, std::min((HW + 255) / 256, std::max(1, 1024 / (B * b.heads))));
     int chunk = (HW + nchunk - 1) / nchunk;
-    chunk = (chunk + 31) / 32 * 32;
+    chunk = (chunk + 127) / 128 * 128;
     nchunk = (HW + chunk - 1) / chunk;
     const int stride = ch * ncol + ch + ncol;
     float* part = fbuf((int64_t)B * b.heads * nchunk * stride);
-    const int nsplit = attn_nsplit(nchunk);
-    float* red = fbuf((int64_t)B * b.heads * nsplit * stride);
+    float* red = fbuf((int64_t)B * b.heads * stride);
     float* attn = fbuf((int64_t)B * b.heads * ch * ncol);
     T* weff = buf((int64_t)B * c * vsrc.Ktot);
     if (dry()) return;
+    if (ch > 128) TFAIL(TURTLE_EINVAL, "channel attention: more than 128 channels per head");
     GramArgs g{};
     g.q = q; g.ldq = ldq; g.qoff = qoff; g.nseg = nseg;
     unsigned mask = 0;
@@ -672,16 +674,16 @@ struct Runner {
     launch(TURTLE_K_ATTN, ES * (double)B * HW * c * (1 + nseg), 2.0 * B * b.heads * ch * ncol * (double)HW,
            [&] { launch_gram<T>(g, st); });
     AttnFinArgs f{};
-    f.part = part; f.nchunk = nchunk; f.nsplit = nsplit; f.B = B; f.heads = b.heads; f.ch = ch; f.nseg = nseg; f.norm_mask = mask;
-    f.tau = h->fptr(bw.tau); f.red = red; f.attn = attn; f.kinv = kinv; f.cur_seg = cur_seg;
-    tag("attn_finalize nbh=%d ch=%d ncol=%d nchunk=%d", B * b.heads, ch, ncol, nchunk);
+    f.part = part; f.nchunk = nchunk; f.B = B; f.heads = b.heads; f.ch = ch; f.nseg = nseg;
+    f.norm_mask = mask; f.tau = h->fptr(bw.tau); f.kinv = kinv; f.cur_seg = cur_seg; f.red = red; f.attn = attn;
+    tag("attn_rows nbh=%d ch=%d ncol=%d nchunk=%d", B * b.heads, ch, ncol, nchunk);
     launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride, 0, [&] { launch_attn_finalize(f, st); });
     WeffArgs we{};
     we.attn = attn; we.wp = h->fptr(bw.wp); we.B = B; we.heads = b.heads; we.ch = ch; we.nseg = nseg; we.C = c;
     for (int s = 0; s < nseg; ++s) { we.seg_col[s] = segs[s].col; we.seg_hstride[s] = segs[s].colh; }
     we.Keff = vsrc.Ktot; we.weff = weff;
     tag("weff B=%d C=%d heads=%d ncol=%d", B, c, b.heads, ncol);
-    launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot, 2.0 * B * c * (double)b.heads * ncol * ch,
+    launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot + 4.0 * B * b.heads * ch * ncol, 2.0 * B * c * (double)b.heads * ncol * ch,
            [&] { launch_weff<T>(we, st); });
     GemmW pw; pw.N = c; pw.K = vsrc.Ktot;
     gemm(pw, vsrc, (int64_t)B * HW, HW, Wimg, x, c, 0, x, c, 0, 0, STORE_NHWC, weff, (int64_t)c * vsrc.Ktot, 1, c,
@@ -1063,6 +1065,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     if (n == "fuse") h->fuse = value != 0;
     else if (n == "panel_gemm") h->panel = value != 0;
     else if (n == "dw_rows") h->dw_rows = value != 0;
+    else if (n == "gemm_lds") h->gemm_lds = value != 0;
     else TFAIL(TURTLE_EINVAL, "unknown option '" + n + "'");
   });
 }
