@@ -125,6 +125,8 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
  *                 0: K-loop GEMM everywhere
  *   "gemm_lds"    1 (default): LDS-pipelined bf16 GEMM (global_load_lds double buffering)
  *                 wherever its alignment rules hold; 0: panel / K-loop GEMMs
+ *   "pwdw"        0 (default; 1 = on): pointwise GEMM -> depthwise 3x3 (-> gate) in one kernel for bf16
+ *                 input widths that are multiples of 64 not covered by "fuse"; 0: GEMM + depthwise
  *   "dw_rows"     1 (default): row-sweeping depthwise 3x3 kernel (rolling 3-row window per
  *                 thread); 0: per-pixel 9-tap gather kernel
  * Unknown names return TURTLE_EINVAL. */

@@ -212,10 +212,11 @@ __global__ __launch_bounds__(256, 2) void gemm_lds_kernel(GemmArgs g) {
       // zero-filled. Sums and sums of squares by v_dot2_f32_bf16 (x . 1 and x . x per pair).
       typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
       const bf16x2 one2 = __builtin_bit_cast(bf16x2, 0x3F803F80u);
-      const char* row = sA + lr * 128 + lh * 64;
+      const char* row = sA + lr * 128;
+      const int sw = (lr >> 1) & 7;
 #pragma unroll
       for (int pc = 0; pc < 4; ++pc) {
-        const uint4 x = *reinterpret_cast<const uint4*>(row + pc * 16);
+        const uint4 x = *reinterpret_cast<const uint4*>(row + (((lh * 4 + pc) ^ sw) << 4));   // swizzled: no conflicts
         const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {

@@ -183,6 +183,18 @@ struct FusedArgs {                 // fused.hip: [LN ->] pw -> dw3x3 -> [act -> 
 };
 template <typename T> void launch_fused(const FusedArgs& a, hipStream_t st);
 
+struct PwdwArgs {                  // pwdw.hip: [LN ->] pw (C -> N1) -> dw3x3 [-> gelu(x1)*x2], bf16
+  const void* x; int64_t ldx; int offx; int C;   // input pixel-major [nimg][H][W][ldx]
+  int nimg, H, W;
+  const void* w1; int N1;          // [N1][C] (LN affine folded)
+  int ln; const float* ln_s; const float* ln_t; const float* b1;
+  const float* dww; const float* dwb;   // [9][N1] fp32, [N1]
+  int gate;                        // 0: out = dw (N1 channels); 1: gelu(dw[:h]) * dw[h:] (h = N1/2)
+  void* out; int64_t ldo; int offo;
+};
+bool pwdw_ok(const PwdwArgs& a);
+void launch_pwdw(const PwdwArgs& a, hipStream_t st);
+
 void launch_cast_f32(const float* src, void* dst, int64_t n, int to_bf16, hipStream_t st);
 
 }  // namespace turtle

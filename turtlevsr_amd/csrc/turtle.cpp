@@ -288,6 +288,7 @@ struct TurtleHandle {
   bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
   bool gemm_lds = true;                               // LDS-pipelined bf16 GEMM (gemm2.hip)
+  bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
   const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
   const float* fptr(size_t off) const { return reinterpret_cast<const float*>(ptr(off)); }
@@ -638,6 +639,25 @@ struct Runner {
     if (mode == F_DWONLY) return n1 % 16 == 0;
     return hidden % 32 == 0;
   }
+  // [LN ->] pw -> dw3x3 [-> gelu(x1)*x2] in one kernel, bf16, input widths multiple of 64 (pwdw.hip)
+  bool can_pwdw(int c, int n1, bool gate) const {
+    if (!h->pwdw || ES != 2 || c % 64) return false;
+    const int hid = gate ? n1 / 2 : n1;
+    return gate ? hid % 64 == 0 : hid % 128 == 0;
+  }
+  void pwdw(const GemmW& w1, const DwW& dwp, const T* x, int64_t ldx, int offx, int C, int nimg, int H, int Wd, int gate,
+            T* out, int64_t ldo, int offo) {
+    if (dry()) return;
+    if (dwp.C != w1.N) TFAIL(TURTLE_EINVAL, "pwdw: dw width != pointwise width");
+    PwdwArgs p{};
+    p.x = x; p.ldx = ldx; p.offx = offx; p.C = C; p.nimg = nimg; p.H = H; p.W = Wd;
+    p.w1 = h->ptr(w1.w); p.N1 = w1.N; p.ln = w1.ln; p.ln_s = h->fptr(w1.s); p.ln_t = h->fptr(w1.t); p.b1 = h->fptr(w1.bias);
+    p.dww = h->fptr(dwp.w); p.dwb = h->fptr(dwp.bias); p.gate = gate; p.out = out; p.ldo = ldo; p.offo = offo;
+    if (!pwdw_ok(p)) TFAIL(TURTLE_EINVAL, "pwdw: unsupported shape");
+    const double px = (double)nimg * H * Wd, hid = gate ? w1.N / 2 : w1.N;
+    tag("pwdw gate=%d nimg=%d H=%d W=%d C=%d N1=%d", gate, nimg, H, Wd, C, w1.N);
+    launch(TURTLE_K_FUSED, ES * px * (C + hid), 2.0 * px * C * w1.N + 18.0 * px * w1.N, [&] { launch_pwdw(p, st); });
+  }
   static FusedDst dst_map(void* p, int64_t ld, int off, int cbeg, int cend) {
     return FusedDst{p, ld, off, cbeg, cend, cend - cbeg, 0, 0};
   }
@@ -725,6 +745,10 @@ struct Runner {
       if (can_fuse(c, F_GATE, 2 * hd, hd)) {
         fused(F_GATE, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, &bw.f_out, x, xalt, {});
         std::swap(x, xalt);
+      } else if (can_pwdw(c, 2 * hd, true)) {
+        T* t2 = buf(P * hd);
+        pwdw(bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, 1, t2, hd, 0);
+        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
       } else {
         T* t1 = buf(P * 2 * hd);
         T* t2 = buf(P * hd);
@@ -745,6 +769,8 @@ struct Runner {
     if (can_fuse(c, F_DWONLY, 3 * c, 0)) {
       fused(F_DWONLY, bw.a_in, bw.a_dw, x, c, 0, c, nimg, H, Wd, 3 * c, nullptr, nullptr, nullptr,
             {dst_map(out, 3 * c, 0, 0, 3 * c)});
+    } else if (can_pwdw(c, 3 * c, false)) {
+      pwdw(bw.a_in, bw.a_dw, x, c, 0, c, nimg, H, Wd, 0, out, 3 * c, 0);
     } else {
       const int64_t P = (int64_t)nimg * H * Wd;
       T* t1 = buf(P * 3 * c);
@@ -883,6 +909,8 @@ struct Runner {
     if (can_fuse(c, F_DWONLY, 2 * c, 0)) {
       fused(F_DWONLY, bw.kv, bw.kv_dw, xs, c, 0, c, B * NT, H, Wd, 2 * c, nullptr, nullptr, nullptr,
             {dst_map(kvd, 2 * c, 0, 0, 2 * c)});
+    } else if (can_pwdw(c, 2 * c, false)) {
+      pwdw(bw.kv, bw.kv_dw, xs, c, 0, c, B * NT, H, Wd, 0, kvd, 2 * c, 0);
     } else {
       T* kv = buf(P * NT * 2 * c);
       gemm(bw.kv, src1(xs, c, 0, c), P * NT, HW, Wd, kv, 2 * c, 0);
@@ -1066,6 +1094,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "panel_gemm") h->panel = value != 0;
     else if (n == "dw_rows") h->dw_rows = value != 0;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
+    else if (n == "pwdw") h->pwdw = value != 0;
     else TFAIL(TURTLE_EINVAL, "unknown option '" + n + "'");
   });
 }
