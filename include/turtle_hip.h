@@ -127,6 +127,10 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
  *                 wherever its alignment rules hold; 0: panel / K-loop GEMMs
  *   "pwdw"        0 (default; 1 = on): pointwise GEMM -> depthwise 3x3 (-> gate) in one kernel for bf16
  *                 input widths that are multiples of 64 not covered by "fuse"; 0: GEMM + depthwise
+ *   "sab_mfma"    1 (default): SAB sparse A.v on the matrix cores (bf16): per 8x8 query tile the
+ *                 ball part is a dense [64 x 256] x [256 x D] product, top-k tail added per query
+ *   "sab_tile"    0 (default; 1 = on, when sab_mfma is off or fp32): VALU A.v over 8x8 query
+ *                 tiles with the ball key rows staged in LDS; 0: one wave per query
  *   "dw_rows"     1 (default): row-sweeping depthwise 3x3 kernel (rolling 3-row window per
  *                 thread); 0: per-pixel 9-tap gather kernel
  * Unknown names return TURTLE_EINVAL. */

@@ -80,9 +80,10 @@ constexpr int SAB_MAXC = 48;       // candidate slots per query (41 ball + 5 top
 struct SabPrepArgs {               // candidates + clipped softmax per (b, t, query)
   const float* topv; const int* topi; const float* ballv;
   int BT, N, th, tw, nsplit;
-  int* cnt;                        // [BT][N] surviving candidates
+  int* cnt;                        // [BT][N] surviving candidates | (ball candidates, listed first) << 16
   int* ci;                         // [BT][N][SAB_MAXC] key index (padding: the query's own index)
   float* cw;                       //                   softmax weight (padding: 0)
+  float* ballw;                    // [BT][N][41] dense ball weights (may alias ballv)
 };
 void launch_sab_prep(const SabPrepArgs& a, hipStream_t st);
 
@@ -90,9 +91,13 @@ struct SabGatherArgs {             // out = sum_c w_c v[key_c], dilated token ->
   const void* v[TURTLE_MAX_T]; int64_t v_bstride[TURTLE_MAX_T];   // [N][ws*ws*C]
   int B, T, N, th, tw, ws, C;
   const int* cnt; const int* ci; const float* cw;
+  const float* ballw;              // [B*T][N][41] dense ball weights (matrix-core A.v)
   void* out;                       // [B*T][Hl][Wl][C] pixel-major
 };
+bool sab_av_mfma_ok(const SabGatherArgs& a);
+void launch_sab_av_mfma(const SabGatherArgs& a, hipStream_t st);   // bf16
 template <typename T> void launch_sab_gather(const SabGatherArgs& a, hipStream_t st);
+template <typename T> void launch_sab_gather_tile(const SabGatherArgs& a, hipStream_t st);
 
 #define TURTLE_MAX_SEG 6
 struct GramSeg {                   // ch key columns per head from a pixel-major source

@@ -312,8 +312,12 @@ __global__ __launch_bounds__(256) void sab_prep_kernel(SabPrepArgs a) {
   const int cnt = __popcll(bal);
   const int64_t o = qi * SAB_MAXC;
   if (ok) { a.ci[o + slot] = m; a.cw[o + slot] = wgt; }
+  // dense ball weights (0 = excluded / outside the grid) for the matrix-core A.v (in place of the
+  // ball scores this lane read above)
+  if (lane < BALL) a.ballw[((int64_t)bt * a.N + n) * BALL + lane] = ok ? wgt : 0.f;
   if (lane >= cnt && lane < SAB_MAXC) { a.ci[o + lane] = n; a.cw[o + lane] = 0.f; }
-  if (lane == 0) a.cnt[qi] = cnt;
+  const int nball = __popcll(bal & ((1ull << BALL) - 1));     // ball candidates come first
+  if (lane == 0) a.cnt[qi] = cnt | (nball << 16);
 }
 
 void launch_sab_prep(const SabPrepArgs& a, hipStream_t st) {
@@ -350,7 +354,7 @@ __global__ __launch_bounds__(256) void sab_gather_kernel(SabGatherArgs a) {
   const int e_l = chunk * CH + lane * VEC;
   const bool lok = e_l < D;                        // D need not be a multiple of the chunk
   const int e0 = lok ? e_l : 0;
-  const int cnt = a.cnt[qi];
+  const int cnt = a.cnt[qi] & 0xffff;
   const int* ci = a.ci + qi * SAB_MAXC;
   const float* cw = a.cw + qi * SAB_MAXC;
   float acc[VEC];
@@ -392,9 +396,373 @@ void launch_sab_gather(const SabGatherArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(sab_gather_kernel<T>, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, a);
 }
 
+// ------------------------------------------------------------------------------------------
+// sparse A.v, query-tiled: block = 8 x 8 query tokens x a 128-element chunk of D x one (b, t).
+// The 41 L1-ball keys of every query of the tile lie in the 16 x 16 token square around it, so
+// that square's value rows (16 x 16 x 256 B = 64 KB) are staged in LDS once by LDS-DMA and the
+// ball candidates (listed first by sab_prep) are read from there; only the <= 5 top-k keys outside
+// the ball come from L2. Against one wave per query this cuts the L2 traffic ~6x (each value row
+// was re-read by ~41 queries). 16 lanes (8 elements each) per query; writes the inverse dilated
+// regroup (turtle_t1_arch.py:602-604) straight into the pixel-major aligned frame.
+// ------------------------------------------------------------------------------------------
+constexpr int SG_T = 8;                      // query tile side (tokens)
+constexpr int SG_S = SG_T + 8;               // staged key square side (ball radius 4)
+constexpr int SG_CH = 128;                   // D elements per block
+
+template <typename T>
+__global__ __launch_bounds__(256) void sab_gather_tile_kernel(SabGatherArgs a) {
+  constexpr int VEC = Vec<T>::N, ES = sizeof(T);
+  constexpr int LPQ = SG_CH / VEC;           // lanes per query (16 bf16, 32 fp32 -> 2 queries / 32 lanes)
+  constexpr int ROWB = SG_CH * ES;           // staged row bytes
+  extern __shared__ __attribute__((aligned(16))) char sv[];   // [SG_S * SG_S][ROWB]
+  const int D = a.ws * a.ws * a.C;
+  const int nch = (D + SG_CH - 1) / SG_CH;
+  const int tty = (a.th + SG_T - 1) / SG_T, ttx = (a.tw + SG_T - 1) / SG_T;
+  int lin = blockIdx.x;
+  {
+    const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
+    lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;
+  }
+  const int tile = lin % (tty * ttx);
+  int rest = lin / (tty * ttx);
+  const int bt = rest % (a.B * a.T);
+  const int chunk = rest / (a.B * a.T);
+  const int ti0 = (tile / ttx) * SG_T, tj0 = (tile % ttx) * SG_T;
+  const int t = bt % a.T, b = bt / a.T;
+  const T* v = reinterpret_cast<const T*>(a.v[0]);
+  int64_t vbs = a.v_bstride[0];
+#pragma unroll
+  for (int j = 1; j < TURTLE_MAX_T; ++j)
+    if (t == j) { v = reinterpret_cast<const T*>(a.v[j]); vbs = a.v_bstride[j]; }
+  v += (int64_t)b * vbs;
+  const int e_base = chunk * SG_CH;
+  const int tid = threadIdx.x;
+
+  // ---- stage the key square: 256 rows x ROWB, 16-byte pieces, rows outside the grid -> zeros ----
+  {
+    constexpr int PPR = ROWB / 16;            // pieces per row
+    constexpr int NP = SG_S * SG_S * PPR / 256;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int pc = tid + 256 * i, r = pc / PPR, k = pc - r * PPR;
+      const int ki = ti0 - 4 + r / SG_S, kj = tj0 - 4 + r % SG_S;
+      const int e = e_base + k * (16 / ES);
+      const bool ok = ki >= 0 && ki < a.th && kj >= 0 && kj < a.tw && e < D;
+      const uint4 q = ld16(ok ? reinterpret_cast<const void*>(v + (int64_t)(ki * a.tw + kj) * D + e) : g_zero_sab);
+      *reinterpret_cast<uint4*>(sv + r * ROWB + k * 16) = q;
+    }
+  }
+  __syncthreads();
+
+  // ---- per query: LPQ lanes x VEC elements ----
+  const int lq = tid % LPQ, qslot = tid / LPQ;                 // 256 / LPQ query slots per pass
+  constexpr int QPP = 256 / LPQ;
+  const int e0 = e_base + lq * VEC;
+  const bool eok = e0 < D;
+  const int e0c = eok ? e0 : 0;
+  const int Hl = a.th * a.ws, Wl = a.tw * a.ws;
+  T* out = reinterpret_cast<T*>(a.out) + (int64_t)bt * Hl * Wl * a.C;
+  for (int qb = 0; qb < SG_T * SG_T; qb += QPP) {
+    const int ql = qb + qslot;
+    const int ti = ti0 + ql / SG_T, tj = tj0 + ql % SG_T;
+    const bool qok = ti < a.th && tj < a.tw;
+    const int n = qok ? ti * a.tw + tj : 0;
+    const int64_t qi = (int64_t)bt * a.N + n;
+    const int cw_all = qok ? a.cnt[qi] : 0;
+    const int cnt = cw_all & 0xffff, nb = cw_all >> 16;
+    // candidate lists: the query's LPQ lanes hold its <= 48 (key, weight) pairs, broadcast per step
+    const int* ci = a.ci + qi * SAB_MAXC;
+    const float* cw = a.cw + qi * SAB_MAXC;
+    constexpr int NR = (SAB_MAXC + LPQ - 1) / LPQ;
+    int rci[NR];
+    float rcw[NR];
+#pragma unroll
+    for (int k = 0; k < NR; ++k) {
+      const int c = min(lq + LPQ * k, SAB_MAXC - 1);
+      rci[k] = ci[c];
+      rcw[k] = cw[c];
+    }
+    int cmax = cnt;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
+    float acc[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
+    const int qbase = (tid & 63) & ~(LPQ - 1);
+    for (int c = 0; c < cmax; ++c) {
+      const int k = c / LPQ, src = qbase + (c - k * LPQ);
+      int mk = rci[0];
+      float wk = rcw[0];
+#pragma unroll
+      for (int u = 1; u < NR; ++u) { mk = k == u ? rci[u] : mk; wk = k == u ? rcw[u] : wk; }
+      const int m = __shfl(mk, src, 64);
+      const float w = __shfl(wk, src, 64);
+      if (c < nb) {
+        // ball key (ki, kj) -> row of the staged square
+        const int ki = m / a.tw, kj = m - ki * a.tw;
+        const int r = (ki - ti0 + 4) * SG_S + (kj - tj0 + 4);
+        Vec<T> x;
+        x.load(reinterpret_cast<const T*>(sv + r * ROWB + lq * 16));
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc[i] = fmaf(w, x.v[i], acc[i]);
+      } else if (c < cnt) {
+        // top-k key outside the ball: from L2
+        Vec<T> x;
+        x.from_raw(ld16(v + (int64_t)m * D + e0c));
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) acc[i] = fmaf(w, x.v[i], acc[i]);
+      }
+    }
+    if (qok && eok) {
+      const int sub = e0 / a.C, c0 = e0 - sub * a.C;
+      const int p1 = sub / a.ws, p2 = sub - p1 * a.ws;
+      Vec<T> o;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) o.v[i] = acc[i];
+      o.store(out + ((int64_t)(p1 * a.th + ti) * Wl + p2 * a.tw + tj) * a.C + c0);
+    }
+  }
+}
+
+template <typename T>
+void launch_sab_gather_tile(const SabGatherArgs& a, hipStream_t st) {
+  const int D = a.ws * a.ws * a.C;
+  const int nch = (D + SG_CH - 1) / SG_CH;
+  const int64_t blocks = (int64_t)nch * a.B * a.T * ((a.th + SG_T - 1) / SG_T) * ((a.tw + SG_T - 1) / SG_T);
+  const size_t lds = (size_t)SG_S * SG_S * SG_CH * sizeof(T);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_gather_tile_kernel<T>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(sab_gather_tile_kernel<T>, dim3((unsigned)blocks), dim3(256), lds, st, a);
+}
+
+// ------------------------------------------------------------------------------------------
+// sparse A.v on the matrix cores. The 41 L1-ball keys of the 8 x 8 query tokens of a tile all lie
+// in the 16 x 16 token square around it, so the ball part of A.v for the tile is a dense product
+//   O[64 q][e] = W'[64 q][256 square keys] . V[256 keys][e]          (41 non-zeros per W' row)
+// (bf16 MFMA 16x16x32, fp32 accumulation). W' is built once per block from the dense ball
+// weights sab_prep leaves in `ballw` and kept in registers as MFMA A fragments; the block then
+// walks its range of 64-element chunks of D: V chunk [256][64] staged in LDS (register double
+// buffer, padded rows, transposed ds_read_b64_tr_b16 B fragments), MFMA, then the <= 5 top-k
+// keys outside the ball are added per query from L2 and the result is written with the inverse
+// dilated regroup (turtle_t1_arch.py:602-604) into the pixel-major aligned frame.
+// ------------------------------------------------------------------------------------------
+constexpr int SM_T = 8, SM_S = 16;                 // query tile / key square side (tokens)
+constexpr int SM_E = 64;                           // D elements per chunk
+constexpr int SM_RV = SM_E * 2 + 16;               // staged V row bytes (padded)
+constexpr int SM_RO = SM_E + 4;                    // output staging row (floats)
+constexpr int SM_LDS = 2 * 256 * SM_RV + 64 * SM_RO * 4 + 64 * SAB_K * 8;
+
+__global__ __launch_bounds__(256, 1) void sab_av_mfma_kernel(SabGatherArgs a, int nsplit) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  char* sV = sm;                                   // [2][256][SM_RV]
+  float* sO = reinterpret_cast<float*>(sm + 2 * 256 * SM_RV);   // [64][SM_RO]
+  int* sTi = reinterpret_cast<int*>(sO + 64 * SM_RO);           // [64][5] tail keys
+  float* sTw = reinterpret_cast<float*>(sTi + 64 * SAB_K);      // [64][5] tail weights
+  const int D = a.ws * a.ws * a.C, nch = D / SM_E;
+  const int tty = (a.th + SM_T - 1) / SM_T, ttx = (a.tw + SM_T - 1) / SM_T;
+  int lin = blockIdx.x;
+  {
+    const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
+    lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;
+  }
+  const int split = lin % nsplit;
+  int rest = lin / nsplit;
+  const int tile = rest % (tty * ttx);
+  const int bt = rest / (tty * ttx);
+  const int ch_beg = split * nch / nsplit, ch_end = (split + 1) * nch / nsplit;
+  const int ti0 = (tile / ttx) * SM_T, tj0 = (tile % ttx) * SM_T;
+  const int t = bt % a.T, b = bt / a.T;
+  const bf16* v = reinterpret_cast<const bf16*>(a.v[0]);
+  int64_t vbs = a.v_bstride[0];
+#pragma unroll
+  for (int j = 1; j < TURTLE_MAX_T; ++j)
+    if (t == j) { v = reinterpret_cast<const bf16*>(a.v[j]); vbs = a.v_bstride[j]; }
+  v += (int64_t)b * vbs;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  // ---- tail lists (top-k keys outside the ball), 64 queries x <= 5 ----
+  for (int e = tid; e < 64 * SAB_K; e += 256) {
+    const int ql = e / SAB_K, x = e - ql * SAB_K;
+    const int ti = ti0 + ql / SM_T, tj = tj0 + ql % SM_T;
+    int m = 0;
+    float w = 0.f;
+    if (ti < a.th && tj < a.tw) {
+      const int64_t qi = (int64_t)bt * a.N + ti * a.tw + tj;
+      const int cc = a.cnt[qi], cnt = cc & 0xffff, nb = cc >> 16;
+      if (nb + x < cnt) { m = a.ci[qi * SAB_MAXC + nb + x]; w = a.cw[qi * SAB_MAXC + nb + x]; }
+    }
+    sTi[e] = m;
+    sTw[e] = w;
+  }
+
+  // dense ball weights of the 64 queries -> LDS (in the output staging area, free until the loop)
+  float* sB = sO;
+  for (int e = tid; e < 64 * BALL; e += 256) {
+    const int ql = e / BALL, s = e - ql * BALL;
+    const int ti = ti0 + ql / SM_T, tj = tj0 + ql % SM_T;
+    sB[e] = (ti < a.th && tj < a.tw) ? a.ballw[((int64_t)bt * a.N + ti * a.tw + tj) * BALL + s] : 0.f;
+  }
+  __syncthreads();
+  // ---- W' A fragments in registers: q-tile qt (16 queries), K-step ks (32 square keys) ----
+  // lane: query row qt*16 + (l & 15), keys 32 ks + 8 (l >> 4) + j
+  bf16x8 wf[4][8];
+  {
+    const int ql_lo = lane & 15, kg = lane >> 4;
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+      const int ql = qt * 16 + ql_lo;
+      const int qy = ql / SM_T, qx = ql % SM_T;                 // query offset in the tile
+      const float* bw = sB + ql * BALL;
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        bf16x8 f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int k = ks * 32 + kg * 8 + j;                   // square key: row k / 16, col k % 16
+          const int di = k / SM_S - 4 - qy, dj = k % SM_S - 4 - qx;
+          const int ad = (di < 0 ? -di : di) + (dj < 0 ? -dj : dj);
+          float w = 0.f;
+          if (ad <= 4) w = bw[ball_slot(di, dj)];
+          f[j] = (bf16)w;
+        }
+        wf[qt][ks] = f;
+      }
+    }
+  }
+
+  // ---- V chunk staging: 256 rows x 64 elements, 8 x 16 B per thread ----
+  uint4 stg[8];
+  auto load_v = [&](int chn) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int pc = tid + 256 * i, r = pc >> 3, k = pc & 7;
+      const int ki = ti0 - 4 + r / SM_S, kj = tj0 - 4 + r % SM_S;
+      const bool ok = ki >= 0 && ki < a.th && kj >= 0 && kj < a.tw;
+      stg[i] = ld16(ok ? reinterpret_cast<const void*>(v + (int64_t)(ki * a.tw + kj) * D + chn * SM_E + k * 8) : g_zero_sab);
+    }
+  };
+  auto store_v = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int pc = tid + 256 * i, r = pc >> 3, k = pc & 7;
+      *reinterpret_cast<uint4*>(sV + (buf * 256 + r) * SM_RV + k * 16) = stg[i];
+    }
+  };
+  const int Hl = a.th * a.ws, Wl = a.tw * a.ws;
+  bf16* out = reinterpret_cast<bf16*>(a.out) + (int64_t)bt * Hl * Wl * a.C;
+  const int g16 = lane >> 4, li = lane & 15, qq = li >> 2, pp = li & 3;
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  typedef __attribute__((address_space(3))) v4s lds_v4s;
+  typedef short v8s __attribute__((ext_vector_type(8)));
+
+  __syncthreads();                                 // sB reads done before sO is reused
+  // tail rows of this thread's query / element group, fetched one chunk ahead (their L2 latency
+  // was the critical path of a chunk)
+  const int tq = tid >> 2, teg = (tid & 3) * 16;
+  uint4 tcur[2 * SAB_K], tnext[2 * SAB_K];
+  auto load_tail = [&](int chn, uint4 (&r)[2 * SAB_K]) {
+#pragma unroll
+    for (int x = 0; x < SAB_K; ++x) {
+      const bf16* src = v + (int64_t)sTi[tq * SAB_K + x] * D + chn * SM_E + teg;
+      r[2 * x] = ld16(src);
+      r[2 * x + 1] = ld16(src + 8);
+    }
+  };
+  if (ch_beg < ch_end) {
+    load_v(ch_beg);
+    load_tail(ch_beg, tcur);
+    store_v(0);
+  }
+  __syncthreads();
+  for (int chn = ch_beg; chn < ch_end; ++chn) {
+    const int buf = (chn - ch_beg) & 1;
+    if (chn + 1 < ch_end) {
+      load_v(chn + 1);
+      load_tail(chn + 1, tnext);
+    }
+    // MFMA: wave w owns elements w*16 .. +15 of the chunk, all 64 queries
+    f32x4 acc[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) acc[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* vb = sV + buf * 256 * SM_RV;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const char* va = vb + (ks * 32 + 8 * g16 + qq) * SM_RV + (wid * 16 + 4 * pp) * 2;
+      const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)va);
+      const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(va + 4 * SM_RV));
+      const bf16x8 bfr = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int qt = 0; qt < 4; ++qt) acc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[qt][ks], bfr, acc[qt], 0, 0, 0);
+    }
+    // C: column (l & 15) = element wid*16 + (l & 15), rows 4 (l >> 4) + i = query
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sO[(qt * 16 + g16 * 4 + i) * SM_RO + wid * 16 + li] = acc[qt][i];
+    __syncthreads();
+    // tail + store: thread = (query tid / 4, 16 elements (tid % 4) * 16)
+    {
+      const int ql = tq, eg = teg;
+      const int ti = ti0 + ql / SM_T, tj = tj0 + ql % SM_T;
+      float o[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[e] = sO[ql * SM_RO + eg + e];
+      const int e0 = chn * SM_E + eg;
+#pragma unroll
+      for (int x = 0; x < SAB_K; ++x) {
+        const float w = sTw[ql * SAB_K + x];
+        Vec<bf16> v0, v1;
+        v0.from_raw(tcur[2 * x]);
+        v1.from_raw(tcur[2 * x + 1]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { o[e] = fmaf(w, v0.v[e], o[e]); o[8 + e] = fmaf(w, v1.v[e], o[8 + e]); }
+      }
+      if (ti < a.th && tj < a.tw) {
+        const int sub = e0 / a.C, c0 = e0 - sub * a.C;
+        const int p1 = sub / a.ws, p2 = sub - p1 * a.ws;
+        bf16* dst = out + ((int64_t)(p1 * a.th + ti) * Wl + p2 * a.tw + tj) * a.C + c0;
+        Vec<bf16> s0, s1;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s0.v[e] = o[e]; s1.v[e] = o[8 + e]; }
+        s0.store(dst);
+        s1.store(dst + 8);
+      }
+    }
+    if (chn + 1 < ch_end) {
+      store_v(buf ^ 1);
+#pragma unroll
+      for (int x = 0; x < 2 * SAB_K; ++x) tcur[x] = tnext[x];
+    }
+    __syncthreads();
+  }
+}
+
+bool sab_av_mfma_ok(const SabGatherArgs& a) {
+  const int D = a.ws * a.ws * a.C;
+  return a.ballw != nullptr && D % SM_E == 0 && a.C % 16 == 0;
+}
+
+void launch_sab_av_mfma(const SabGatherArgs& a, hipStream_t st) {
+  const int D = a.ws * a.ws * a.C, nch = D / SM_E;
+  const int tiles = ((a.th + SM_T - 1) / SM_T) * ((a.tw + SM_T - 1) / SM_T) * a.B * a.T;
+  // split each tile's chunk range so the grid reaches ~4 blocks per CU
+  const int nsplit = std::max(1, std::min(nch, (1024 + tiles - 1) / tiles));
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_av_mfma_kernel), hipFuncAttributeMaxDynamicSharedMemorySize, SM_LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(sab_av_mfma_kernel, dim3((unsigned)(tiles * nsplit)), dim3(256), SM_LDS, st, a, nsplit);
+}
+
 template void launch_sab_score<float>(const SabScoreArgs&, hipStream_t);
 template void launch_sab_score<bf16>(const SabScoreArgs&, hipStream_t);
 template void launch_sab_gather<float>(const SabGatherArgs&, hipStream_t);
 template void launch_sab_gather<bf16>(const SabGatherArgs&, hipStream_t);
+template void launch_sab_gather_tile<float>(const SabGatherArgs&, hipStream_t);
+template void launch_sab_gather_tile<bf16>(const SabGatherArgs&, hipStream_t);
 
 }  // namespace turtle

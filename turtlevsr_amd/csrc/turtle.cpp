@@ -288,6 +288,8 @@ struct TurtleHandle {
   bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
   bool gemm_lds = true;                               // LDS-pipelined bf16 GEMM (gemm2.hip)
+  bool sab_tile = false;                              // query-tiled VALU SAB gather (sab.hip)
+  bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
   const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
@@ -882,7 +884,7 @@ struct Runner {
       sa.tau = h->fptr(bw.sab_tau); sa.topv = topv; sa.topi = topi; sa.ballv = ballv;
       SabGatherArgs ga{};
       ga.B = B; ga.T = NT; ga.N = N; ga.th = th; ga.tw = tw; ga.ws = ws; ga.C = c;
-      ga.cnt = ccnt; ga.ci = cidx; ga.cw = cwt; ga.out = xs;
+      ga.cnt = ccnt; ga.ci = cidx; ga.cw = cwt; ga.ballw = ballv; ga.out = xs;
       for (int t = 0; t < NT; ++t) {
         if (t < Tin) {
           sa.k[t] = kin + (int64_t)t * N * d2; sa.k_bstride[t] = (int64_t)Tin * N * d2;
@@ -897,13 +899,17 @@ struct Runner {
              2.0 * B * NT * (double)N * N * d2, [&] { launch_sab_score<T>(sa, st); });
       SabPrepArgs pa{};
       pa.topv = topv; pa.topi = topi; pa.ballv = ballv; pa.BT = B * NT; pa.N = N; pa.th = th; pa.tw = tw;
-      pa.nsplit = nsplit; pa.cnt = ccnt; pa.ci = cidx; pa.cw = cwt;
+      pa.nsplit = nsplit; pa.cnt = ccnt; pa.ci = cidx; pa.cw = cwt; pa.ballw = ballv;
       tag("sab_prep BT=%d N=%d", B * NT, N);
       launch(TURTLE_K_SAB_AV, 4.0 * B * NT * (double)N * (10 * nsplit + 41 + 2 * SAB_MAXC), 0, [&] { launch_sab_prep(pa, st); });
       // <= 46 surviving keys per row (5 top + 41 ball): SURVEY.md §8(a) sparse A.v
       tag("sab_gather BT=%d N=%d D=%d", B * NT, N, D);
       launch(TURTLE_K_SAB_AV, ES * ((double)B * NT * N * D + (double)B * NT * HW * c),
-             2.0 * B * NT * (double)N * 46 * D, [&] { launch_sab_gather<T>(ga, st); });
+             2.0 * B * NT * (double)N * 46 * D, [&] {
+               if (h->sab_mfma && ES == 2 && sab_av_mfma_ok(ga)) launch_sab_av_mfma(ga, st);
+               else if (h->sab_tile) launch_sab_gather_tile<T>(ga, st);
+               else launch_sab_gather<T>(ga, st);
+             });
     }
     // kv = (W_kv W_po) xs over the B*T aligned frames, then dw3x3 per frame
     if (can_fuse(c, F_DWONLY, 2 * c, 0)) {
@@ -1095,6 +1101,8 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "dw_rows") h->dw_rows = value != 0;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
     else if (n == "pwdw") h->pwdw = value != 0;
+    else if (n == "sab_tile") h->sab_tile = value != 0;
+    else if (n == "sab_mfma") h->sab_mfma = value != 0;
     else TFAIL(TURTLE_EINVAL, "unknown option '" + n + "'");
   });
 }
