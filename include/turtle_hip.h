@@ -127,6 +127,8 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
  *                 wherever its alignment rules hold; 0: panel / K-loop GEMMs
  *   "pwdw"        0 (default; 1 = on): pointwise GEMM -> depthwise 3x3 (-> gate) in one kernel for bf16
  *                 input widths that are multiples of 64 not covered by "fuse"; 0: GEMM + depthwise
+ *   "stem_mfma"   1 (default): input_projection / ending 3x3 convolutions on the matrix cores (bf16,
+ *                 dim 64); 0: VALU kernels
  *   "sab_mfma"    1 (default): SAB sparse A.v on the matrix cores (bf16): per 8x8 query tile the
  *                 ball part is a dense [64 x 256] x [256 x D] product, top-k tail added per query
  *   "sab_tile"    0 (default; 1 = on, when sab_mfma is off or fp32): VALU A.v over 8x8 query

@@ -158,6 +158,19 @@ TURTLE_DEV float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.7
 
 TURTLE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
+// tanh-form GELU, x * sigmoid(1.5957691 (x + 0.044715 x^3)): |diff| to the erf form <= 5e-4,
+// below the bf16 rounding step of any GELU output above 0.13; one exp2 + one rcp + 4 VALU
+TURTLE_DEV float gelu_tanh(float x) {
+  const float u = x * fmaf(-0.10294324f, x * x, -2.3022082f);   // -log2(e) * 1.5957691 (x + 0.044715 x^3)
+  return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u));
+}
+// GELU of a kernel computing in storage type T: tanh form for bf16 storage, erf form for fp32
+template <typename T>
+TURTLE_DEV float gelu_t(float x) {
+  if constexpr (sizeof(T) == 2) return gelu_tanh(x);
+  else return gelu_erf(x);
+}
+
 TURTLE_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -359,7 +359,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
 #pragma unroll
           for (int i0 = 0; i0 < 8; i0 += VEC) {
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_fast(d[i0 + i]) * d[8 + i0 + i];
+            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_t<T>(d[i0 + i]) * d[8 + i0 + i];
             gv.store(g + i0);
           }
         } else {
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
           for (int i0 = 0; i0 < 16; i0 += VEC) {
             Vec<T> gv;
 #pragma unroll
-            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_fast(d[i0 + i]);
+            for (int i = 0; i < VEC; ++i) gv.v[i] = gelu_t<T>(d[i0 + i]);
             gv.store(g + i0);
           }
         }

@@ -166,6 +166,9 @@ struct EndArgs {                   // ending 3x3 Cin->Cimg + bias + current fram
   float* out;                      // [B][Cimg][Hout][Wout]
 };
 template <typename T> void launch_ending(const EndArgs& a, hipStream_t st);
+bool stem_end_mfma_ok(int cin_end, int cin_stem, int cout_stem);   // bf16 matrix-core stem / ending
+void launch_ending_mfma(const EndArgs& a, hipStream_t st);
+void launch_stem_mfma(const StemArgs& a, hipStream_t st);
 
 enum FusedMode { F_DWONLY = 0, F_GELU = 1, F_GATE = 2 };
 struct FusedDst {                  // F_DWONLY output for channels [cbeg, cend)

@@ -43,6 +43,7 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
   constexpr int NH = MODE == DW_GATE ? 2 : 1;             // gate: x1 and x2 halves
   constexpr int CW = DW_CC * VEC;                         // channels per block
   __shared__ __attribute__((aligned(16))) float sw[NH][9][CW];
+  __shared__ __attribute__((aligned(16))) float sbias[NH][CW];
   const int tid = threadIdx.x;
   const int CV = a.C / VEC;
   const int Cw = NH * a.C;
@@ -64,6 +65,11 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
     const int cg = chunk * CW + c;
     sw[hh][tap][c] = cg < a.C ? a.w[tap * Cw + hh * a.C + cg] : 0.f;
   }
+  // bias in LDS too (read per row: registers are the occupancy limit of the gate variant)
+  for (int e = tid; e < NH * CW; e += 256) {
+    const int hh = e / CW, c = e - hh * CW, cg = chunk * CW + c;
+    sbias[hh][c] = a.bias && cg < a.C ? a.bias[hh * a.C + cg] : 0.f;
+  }
   const int cvl = tid % DW_CC, xs = tid / DW_CC;
   const int x = strip * DW_SX + xs, cv = chunk * DW_CC + cvl;
   const bool live = x < a.W && cv < CV;
@@ -83,20 +89,6 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
       r[hh][2] = ld16(oky && okr ? reinterpret_cast<const void*>(q + a.ldi) : g_zero_dw);
     }
   };
-  float bias[NH][VEC];
-  {
-    const float* zb = reinterpret_cast<const float*>(g_zero_dw);
-#pragma unroll
-    for (int hh = 0; hh < NH; ++hh) {
-      const float* b = a.bias ? a.bias + hh * a.C + c0 : zb;
-#pragma unroll
-      for (int i0 = 0; i0 < VEC; i0 += 4) {
-        const uint4 u = ld16(b + i0);
-        bias[hh][i0] = __uint_as_float(u.x); bias[hh][i0 + 1] = __uint_as_float(u.y);
-        bias[hh][i0 + 2] = __uint_as_float(u.z); bias[hh][i0 + 3] = __uint_as_float(u.w);
-      }
-    }
-  }
   uint4 w0[NH][3], w1[NH][3], w2[NH][3], nx[NH][3];
   load_row(y0 - 1, w0);
   load_row(y0, w1);
@@ -113,7 +105,10 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh) {
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) acc[hh][i] = bias[hh][i];
+      for (int i0 = 0; i0 < VEC; i0 += 4) {
+        const float4 bb = *reinterpret_cast<const float4*>(&sbias[hh][wcy + i0]);
+        acc[hh][i0] = bb.x; acc[hh][i0 + 1] = bb.y; acc[hh][i0 + 2] = bb.z; acc[hh][i0 + 3] = bb.w;
+      }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const uint4 q = tap < 3 ? w0[hh][tap] : tap < 6 ? w1[hh][tap - 3] : w2[hh][tap - 6];
@@ -139,8 +134,8 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
         float r = acc[0][i];
-        if (MODE == DW_GELU) r = gelu_erf(r);
-        else if (MODE == DW_GATE) r = gelu_erf(r) * acc[NH - 1][i];
+        if (MODE == DW_GELU) r = gelu_t<T>(r);
+        else if (MODE == DW_GATE) r = gelu_t<T>(r) * acc[NH - 1][i];
         o.v[i] = r;
       }
       const int64_t pix = (img * a.H + y) * a.W + x;
@@ -227,8 +222,8 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
 #pragma unroll
   for (int i = 0; i < VEC; ++i) {
     float r = acc1[i];
-    if (MODE == DW_GELU) r = gelu_erf(r);
-    else if (MODE == DW_GATE) r = gelu_erf(r) * acc2[i];
+    if (MODE == DW_GELU) r = gelu_t<T>(r);
+    else if (MODE == DW_GATE) r = gelu_t<T>(r) * acc2[i];
     o.v[i] = r;
   }
   int64_t dst;
@@ -514,8 +509,47 @@ __global__ __launch_bounds__(256) void fhr_cache_kernel(FhrCacheArgs a) {
   }
 }
 
+// same, 16 bytes per thread: with R, Rnew, ch and the shift multiples of the vector width every
+// output vector comes whole from the old cache or from the current (rescaled) rows
+template <typename T>
+__global__ __launch_bounds__(256) void fhr_cache_vec_kernel(FhrCacheArgs a) {
+  constexpr int VEC = Vec<T>::N;
+  const int nv = a.Rnew / VEC;
+  const int64_t total = (int64_t)a.B * a.P * a.heads * nv;
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const T* old = reinterpret_cast<const T*>(a.old);
+  const T* cur = reinterpret_cast<const T*>(a.cur);
+  const int shift = a.R + a.ch - a.Rnew;
+  const int rv = (int)(idx % nv);
+  const int64_t t = idx / nv;
+  const int h = (int)(t % a.heads);
+  const int64_t bp = t / a.heads;
+  const int r = rv * VEC + shift;
+  Vec<T> v;
+  if (r < a.R) {
+    v.load(old + (bp * a.heads + h) * a.R + r);
+  } else {
+    const int j = r - a.R, b = (int)(bp / a.P);
+    v.load(cur + bp * a.ldc + a.coff + h * a.ch + j);
+    if (a.kinv) {
+      const float* kv = a.kinv + (int64_t)b * a.heads * a.ch + h * a.ch + j;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) v.v[i] *= kv[i];
+    }
+  }
+  v.store(reinterpret_cast<T*>(a.out) + (bp * a.heads + h) * a.Rnew + rv * VEC);
+}
+
 template <typename T>
 void launch_fhr_cache(const FhrCacheArgs& a, hipStream_t st) {
+  constexpr int VEC = Vec<T>::N;
+  const int shift = a.R + a.ch - a.Rnew;
+  if (a.R % VEC == 0 && a.Rnew % VEC == 0 && a.ch % VEC == 0 && shift % VEC == 0 && a.ldc % VEC == 0 && a.coff % VEC == 0) {
+    const int64_t total = (int64_t)a.B * a.P * a.heads * (a.Rnew / VEC);
+    hipLaunchKernelGGL(fhr_cache_vec_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
+    return;
+  }
   const int64_t total = (int64_t)a.B * a.P * a.heads * a.Rnew;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 65536) blocks = 65536;
@@ -533,6 +567,146 @@ void launch_cast_f32(const float* src, void* dst, int64_t n, int to_bf16, hipStr
   if (blocks > 65536) blocks = 65536;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(cast_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, n, to_bf16);
+}
+
+// ------------------------------------------------------------------------------------------
+// bf16 stem / ending on the matrix cores. One wave = a 16-pixel run of a padded row:
+//   ending: C[co][px] = W[co][tap*Cin + c] . X[tap*Cin + c][px]   (K = 9 Cin, co < Cimg padded to 16)
+//   stem:   C[co][px] = W[co][ci*9 + tap] . F[ci*9 + tap][px]     (K = 9 Cimg padded to 32, 64 co)
+// A = weights as register fragments built once per wave, B = the 16 pixels' operands: for the ending
+// 16-byte channel vectors straight from the pixel-major map, for the stem 8 gathered frame samples
+// (zero pad / SR bilinear, frame_px) per lane. Per-wave work loops over runs (grid-stride).
+// ------------------------------------------------------------------------------------------
+template <int CIN>
+__global__ __launch_bounds__(256) void ending_mfma_kernel(EndArgs a) {
+  constexpr int KS = 9 * CIN / 32;
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15;
+  const int wv = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  bf16x8 wf[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    bf16x8 f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = s * 32 + g * 8 + j, tap = k / CIN, c = k - tap * CIN;
+      f[j] = (bf16)(li < a.Cimg ? a.w[(li * CIN + c) * 9 + tap] : 0.f);
+    }
+    wf[s] = f;
+  }
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = i < a.Cimg ? a.bias[i] : 0.f;
+  StemArgs s{};
+  s.inp = a.inp; s.in_bstride = a.in_bstride; s.in_fstride = a.in_fstride;
+  s.Cimg = a.Cimg; s.Hin = a.Hin; s.Win = a.Win; s.sr = a.sr;
+  const bf16* X = reinterpret_cast<const bf16*>(a.x);
+  const int tpr = (a.Wp + 15) / 16, nt = a.B * a.Hp * tpr;
+  for (int t = wv; t < nt; t += nw) {
+    const int tx = t % tpr, row = t / tpr, y = row % a.Hp, b = row / a.Hp;
+    const int x = tx * 16 + li;
+    uint4 xv[KS];
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int k0 = st * 32 + g * 8, tap = k0 / CIN, c = k0 - tap * CIN;
+      const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+      const bool ok = yy >= 0 && yy < a.Hp && xx >= 0 && xx < a.Wp;
+      xv[st] = ld16(ok ? reinterpret_cast<const void*>(X + (((int64_t)b * a.Hp + yy) * a.Wp + xx) * CIN + c) : g_zero_end);
+    }
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < KS; ++st) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[st], __builtin_bit_cast(bf16x8, xv[st]), acc, 0, 0, 0);
+    // C: column li = pixel, rows 4 g + i = output channel (only g == 0 holds co < 4)
+    if (g == 0 && y < a.Hout && x < a.Wout) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (i < a.Cimg)
+          a.out[(((int64_t)b * a.Cimg + i) * a.Hout + y) * a.Wout + x] = acc[i] + bias[i] + frame_px(s, b, 1, i, y, x);
+    }
+  }
+}
+
+template <int CIN>   // frame channels (Cimg, or 2 Cimg with use_both_input); K = 9 CIN padded to 32 KS
+__global__ __launch_bounds__(256) void stem_mfma_kernel(StemArgs a) {
+  constexpr int KS = (9 * CIN + 31) / 32;
+  __shared__ __attribute__((aligned(16))) char stile[4][16 * 144];    // per wave: 16 px x 64 co bf16
+  const int lane = threadIdx.x & 63, g = lane >> 4, li = lane & 15, wid = threadIdx.x >> 6;
+  const int wv = blockIdx.x * 4 + wid, nw = gridDim.x * 4;
+  // A fragments: W[co][ci][tap] (fp32 [64][CIN][3][3]), co = 16 ct + li, k = ci*9 + tap
+  bf16x8 wf[4][KS];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      bf16x8 f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = st * 32 + g * 8 + j, co = ct * 16 + li;
+        f[j] = (bf16)(k < 9 * CIN && co < a.Cout ? a.w[co * 9 * CIN + k] : 0.f);
+      }
+      wf[ct][st] = f;
+    }
+  const int tpr = (a.Wp + 15) / 16, nt = a.B * a.Hp * tpr;
+  char* sw = stile[wid];
+  for (int t = wv; t < nt; t += nw) {
+    const int tx = t % tpr, row = t / tpr, y = row % a.Hp, b = row / a.Hp;
+    const int x = tx * 16 + li;
+    bf16x8 xf[KS];
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = st * 32 + g * 8 + j;
+        const int ci = k / 9, tap = k - ci * 9;
+        const int yy = y + tap / 3 - 1, xx = x + tap % 3 - 1;
+        const int f = a.use_both ? (ci < a.Cimg ? 0 : 1) : 1, c = a.use_both ? ci % a.Cimg : ci;
+        const bool inpad = k < 9 * CIN && yy >= 0 && yy < a.Hp && xx >= 0 && xx < a.Wp;
+        const float val = frame_px(a, b, f, min(c, a.Cimg - 1), yy, xx);
+        xf[st][j] = (bf16)(inpad ? val : 0.f);
+      }
+    }
+    f32x4 acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < KS; ++st) acc[ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ct][st], xf[st], acc[ct], 0, 0, 0);
+    }
+    // C: column li = pixel, rows 4 g + i = channel 16 ct + 4 g + i -> LDS [px][co], then 16-byte rows
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { const int co = ct * 16 + g * 4 + i; v[i] = acc[ct][i] + (a.bias ? a.bias[co] : 0.f); }
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<bf16x4*>(sw + li * 144 + (ct * 16 + g * 4) * 2) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    bf16* o = reinterpret_cast<bf16*>(a.out);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pc = lane + 64 * h, px = pc >> 3, k = pc & 7;
+      const uint4 q = *reinterpret_cast<const uint4*>(sw + px * 144 + k * 16);
+      const int xo = tx * 16 + px;
+      if (xo < a.Wp) *reinterpret_cast<uint4*>(o + (((int64_t)b * a.Hp + y) * a.Wp + xo) * 64 + k * 8) = q;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+bool stem_end_mfma_ok(int cin_end, int cin_stem, int cout_stem) {
+  return cin_end == 64 && cout_stem == 64 && (cin_stem == 3 || cin_stem == 6);
+}
+
+void launch_ending_mfma(const EndArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(ending_mfma_kernel<64>, dim3(2048), dim3(256), 0, st, a);
+}
+
+void launch_stem_mfma(const StemArgs& a, hipStream_t st) {
+  const int cin = a.use_both ? 2 * a.Cimg : a.Cimg;
+  if (cin == 3) hipLaunchKernelGGL(stem_mfma_kernel<3>, dim3(2048), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(stem_mfma_kernel<6>, dim3(2048), dim3(256), 0, st, a);
 }
 
 #define INST(T)                                                          \

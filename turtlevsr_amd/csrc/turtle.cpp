@@ -289,6 +289,7 @@ struct TurtleHandle {
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
   bool gemm_lds = true;                               // LDS-pipelined bf16 GEMM (gemm2.hip)
   bool sab_tile = false;                              // query-tiled VALU SAB gather (sab.hip)
+  bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
@@ -972,7 +973,10 @@ struct Runner {
       s.w = h->fptr(h->mw.stem_w); s.bias = h->fptr(h->mw.stem_b); s.Cout = d; s.out = e1;
       tag("stem %dx%d", Hp, Wp);
       launch(TURTLE_K_OTHER, 4.0 * B * A.in_ch * Hin * Win + ES * (double)P1 * d, 18.0 * P1 * d * A.in_ch,
-             [&] { launch_stem<T>(s, st); });
+             [&] {
+               if (h->stem_mfma && ES == 2 && stem_end_mfma_ok(d, A.in_ch, d)) launch_stem_mfma(s, st);
+               else launch_stem<T>(s, st);
+             });
     }
     int H = Hp, Wd = Wp;
     e1 = level(0, e1, a1, H, Wd);
@@ -1013,7 +1017,10 @@ struct Runner {
       e.sr = A.cfg.super_resolution; e.out = out;
       tag("ending %dx%d", Hout, Wout);
       launch(TURTLE_K_OTHER, ES * (double)P1 * d + 8.0 * B * A.out_ch * Hout * Wout, 18.0 * P1 * d * A.out_ch,
-             [&] { launch_ending<T>(e, st); });
+             [&] {
+               if (h->stem_mfma && ES == 2 && stem_end_mfma_ok(d, A.in_ch, d)) launch_ending_mfma(e, st);
+               else launch_ending<T>(e, st);
+             });
     }
   }
 };
@@ -1103,6 +1110,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "pwdw") h->pwdw = value != 0;
     else if (n == "sab_tile") h->sab_tile = value != 0;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
+    else if (n == "stem_mfma") h->stem_mfma = value != 0;
     else TFAIL(TURTLE_EINVAL, "unknown option '" + n + "'");
   });
 }
