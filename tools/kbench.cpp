@@ -31,6 +31,7 @@ struct Shape { int64_t M; int N, K; int ln, res, gelu; const char* tag; int nsrc
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
+  const int dbg = argc > 2 ? atoi(argv[2]) : 0;     // pn ablation bits: 1 no stores, 2 no W refills, 4 no LDS reads
   const Shape shapes[] = {
       {130560, 1280, 256, 1, 0, 0, "L3 GFFW project_in"},
       {130560, 768, 256, 1, 0, 0, "L3 qkv"},
@@ -57,19 +58,23 @@ int main(int argc, char** argv) {
   std::vector<uint16_t> h(std::max(maxA, maxO));
   srand(1);
   for (auto& x : h) x = f2bf((rand() / (float)RAND_MAX - 0.5f));
-  void *A, *Wt, *R, *O1, *O2;
+  void *A, *Wt, *R, *O1, *O2, *O3;
   float *vec, *zeros, *ones;
   CK(hipMalloc(&A, maxA * 2));
   CK(hipMalloc(&Wt, maxW * 2));
   CK(hipMalloc(&R, maxO * 2));
   CK(hipMalloc(&O1, maxO * 2));
   CK(hipMalloc(&O2, maxO * 2));
+  CK(hipMalloc(&O3, maxO * 2));
   CK(hipMemcpy(A, h.data(), maxA * 2, hipMemcpyHostToDevice));
   CK(hipMemcpy(R, h.data(), maxO * 2, hipMemcpyHostToDevice));
   for (size_t i = 0; i < maxW; ++i) h[i] = f2bf((rand() / (float)RAND_MAX - 0.5f) * 0.1f);
   CK(hipMemcpy(Wt, h.data(), maxW * 2, hipMemcpyHostToDevice));
   std::vector<float> hv(16384);
   for (auto& x : hv) x = rand() / (float)RAND_MAX - 0.5f;
+  // vec[0..4095] = ln_s: row sums of W (N <= 4096 used with LN), as the model's folded LayerNorm
+  std::vector<uint16_t> hw(maxW);
+  CK(hipMemcpy(hw.data(), Wt, maxW * 2, hipMemcpyDeviceToHost));
   CK(hipMalloc(&vec, 16384 * 4));
   CK(hipMemcpy(vec, hv.data(), 16384 * 4, hipMemcpyHostToDevice));
   std::vector<float> z(16384, 0.f), o(16384, 1.f);
@@ -77,12 +82,14 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&ones, 16384 * 4));
   CK(hipMemcpy(zeros, z.data(), 16384 * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(ones, o.data(), 16384 * 4, hipMemcpyHostToDevice));
+  unsigned long long* stamps = nullptr;
+  CK(hipMalloc(&stamps, 2 * 8 * 256 * 8));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   std::vector<uint16_t> r1(maxO), r2(maxO);
-  printf("%-24s %8s %5s %5s | %9s %7s %6s | %9s %7s %6s | %s\n", "shape", "M", "N", "K", "new us", "TF/s", "GB/s",
-         "old us", "TF/s", "GB/s", "max|d|");
+  printf("%-24s %8s %5s %5s | %9s %7s %6s | %9s %7s %6s | %9s %7s %6s | %s\n", "shape", "M", "N", "K", "pn us", "TF/s", "GB/s",
+         "lds us", "TF/s", "GB/s", "panel us", "TF/s", "GB/s", "max|d| pn,panel vs lds");
   for (auto& s : shapes) {
     GemmArgs g{};
     g.a.n = s.nsrc; g.a.Ktot = s.K;
@@ -91,16 +98,24 @@ int main(int argc, char** argv) {
     g.M = s.M; g.N = s.N; g.HW = (int)s.M; g.Wimg = s.Wimg;
     g.conv3 = s.conv3; g.cin = kin; g.store_mode = s.store;
     g.w = Wt; g.ldw = s.K; g.wdiv = 1;
+    if (s.ln) {
+      std::vector<float> rs(s.N, 0.f);
+      for (int n = 0; n < s.N; ++n)
+        for (int k = 0; k < s.K; ++k) rs[n] += bf2f(hw[(size_t)n * s.K + k]);
+      CK(hipMemcpy(vec, rs.data(), s.N * 4, hipMemcpyHostToDevice));
+    }
     g.ln = s.ln; g.ln_s = s.ln ? vec : nullptr; g.ln_t = s.ln ? vec + 4096 : nullptr;
     g.bias = vec + 8192; g.scale = nullptr; g.gelu = s.gelu;
     g.res = s.res ? R : nullptr; g.ldr = s.N; g.offr = 0;
     g.ldo = s.store == STORE_UNSHUFFLE ? s.N * 4 : (s.store == STORE_SHUFFLE ? s.N / 4 : s.N); g.offo = 0;
-    g.zeros = zeros; g.ones = ones;
-    double us[2];
-    for (int v = 0; v < 2; ++v) {
-      g.allow_lds = v == 0;
-      g.allow_panel = v == 1;          // variant 0: LDS kernel forced; 1: panel / K-loop
-      g.out = v == 0 ? O1 : O2;
+    g.zeros = zeros; g.ones = ones; g.dbg = dbg;
+    double us[3];
+    for (int v = 0; v < 3; ++v) {
+      g.allow_pn = v == 0;             // variant 0: resident-panel kernel (if eligible); 1: LDS kernel; 2: panel / K-loop
+      g.allow_lds = v == 1;
+      g.allow_panel = v == 2;
+      g.out = v == 0 ? O1 : (v == 1 ? O2 : O3);
+      g.stamps = (v == 0 && (dbg & 8) && &s == &shapes[0]) ? stamps : nullptr;
       launch_gemm<bf16>(g, 0);
       CK(hipDeviceSynchronize());
       CK(hipEventRecord(e0, 0));
@@ -111,14 +126,28 @@ int main(int argc, char** argv) {
       CK(hipEventElapsedTime(&ms, e0, e1));
       us[v] = ms * 1e3 / reps;
     }
+    if ((dbg & 8) && &s == &shapes[0]) {       // s_memtime stamps of block 0, waves 0 and 4 (last launch)
+      std::vector<unsigned long long> hs(2 * 8 * 256);
+      CK(hipMemcpy(hs.data(), stamps, hs.size() * 8, hipMemcpyDeviceToHost));
+      for (int w : {0, 4}) {
+        printf("stamps block 0 wave %d (cycles from first):", w);
+        const unsigned long long* b = hs.data() + w * 256;
+        for (int i = 1; i < 64 && b[i] > b[0] && b[i] - b[0] < (1ull << 32); ++i) printf(" %llu", b[i] - b[i - 1]);
+        printf("\n");
+      }
+      CK(hipMemset(stamps, 0, 2 * 8 * 256 * 8));
+    }
     const size_t n = (size_t)s.M * s.N;
     CK(hipMemcpy(r1.data(), O1, n * 2, hipMemcpyDeviceToHost));
     CK(hipMemcpy(r2.data(), O2, n * 2, hipMemcpyDeviceToHost));
-    double md = 0;
+    double md = 0, md3 = 0;
     for (size_t i = 0; i < n; ++i) md = std::max(md, (double)fabsf(bf2f(r1[i]) - bf2f(r2[i])));
+    CK(hipMemcpy(r1.data(), O3, n * 2, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; ++i) md3 = std::max(md3, (double)fabsf(bf2f(r1[i]) - bf2f(r2[i])));
     const double fl = 2.0 * s.M * s.N * s.K, by = 2.0 * ((double)s.M * s.K + (double)s.M * s.N * (s.res ? 2 : 1));
-    printf("%-24s %8lld %5d %5d | %9.1f %7.0f %6.0f | %9.1f %7.0f %6.0f | %.3g\n", s.tag, (long long)s.M, s.N, s.K, us[0],
-           fl / us[0] / 1e6, by / us[0] / 1e3, us[1], fl / us[1] / 1e6, by / us[1] / 1e3, md);
+    printf("%-24s %8lld %5d %5d | %9.1f %7.0f %6.0f | %9.1f %7.0f %6.0f | %9.1f %7.0f %6.0f | %.3g %.3g%s\n", s.tag, (long long)s.M,
+           s.N, s.K, us[0], fl / us[0] / 1e6, by / us[0] / 1e3, us[1], fl / us[1] / 1e6, by / us[1] / 1e3, us[2],
+           fl / us[2] / 1e6, by / us[2] / 1e3, md, md3, gemm_pn_ok((g.allow_pn = 1, g)) ? "" : "  (pn n/a)");
   }
   return 0;
 }

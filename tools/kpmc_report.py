@@ -42,6 +42,13 @@ def main():
                   "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS"):
             if c in vals:
                 out.append(f"{c[8:] if c.startswith('SQ_INSTS') else c[3:]}/w={vals[c] / w:.0f}")
+        for c in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CU_CYCLES", "SQ_WAIT_INST_LDS", "SQ_VMEM_WR_TA_DATA_FIFO_FULL",
+                  "SQ_VMEM_TA_ADDR_FIFO_FULL", "SQ_INST_LEVEL_VMEM"):
+            if c in vals and cyc:
+                out.append(f"{c[3:]}/wcyc={vals[c] / cyc:.3f}")
+        ns = [v for k, v in ent.items() if k.startswith("_ns_")]
+        if ns:
+            out.append(f"us={sorted(ns)[len(ns) // 2] / 1e3:.1f}")
         if "FETCH_SIZE" in vals:
             out.append(f"fetchMB={2 * vals['FETCH_SIZE'] / 1024:.1f}")
         if "WRITE_SIZE" in vals:

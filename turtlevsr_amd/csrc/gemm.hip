@@ -556,6 +556,7 @@ static void launch_cfg(const GemmArgs& g, hipStream_t st) {
 template <typename T>
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
+    if (gemm_pn_ok(g)) { launch_gemm_pn(g, st); return; }
     if (gemm_lds_ok(g)) { launch_gemm_lds(g, st); return; }
     if (panel_ok(g)) { launch_panel_any(g, st); return; }
   }

@@ -32,10 +32,15 @@ struct GemmArgs {
   const float* ones;
   int allow_panel;                 // panel kernel permitted (turtle_set_option "panel_gemm")
   int allow_lds;                   // LDS-pipelined kernel permitted (turtle_set_option "gemm_lds")
+  int allow_pn;                    // resident-panel kernel permitted (turtle_set_option "gemm_pn")
+  int dbg;                         // tools/kbench ablations of the pn kernel (0 in the product path)
+  unsigned long long* stamps;      // tools/kbench s_memtime stamps of the pn kernel (null in the product path)
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
 bool gemm_lds_ok(const GemmArgs& g);                              // gemm2.hip (bf16)
 void launch_gemm_lds(const GemmArgs& g, hipStream_t st);
+bool gemm_pn_ok(const GemmArgs& g);                               // gemm3.hip (bf16)
+void launch_gemm_pn(const GemmArgs& g, hipStream_t st);
 
 enum DwMode { DW_PLAIN = 0, DW_GELU = 1, DW_GATE = 2 };
 struct DwArgs {

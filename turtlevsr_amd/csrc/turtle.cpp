@@ -288,6 +288,7 @@ struct TurtleHandle {
   bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
   bool gemm_lds = true;                               // LDS-pipelined bf16 GEMM (gemm2.hip)
+  bool gemm_pn = true;                                // resident-panel bf16 GEMM, K <= 512 (gemm3.hip)
   bool sab_tile = false;                              // query-tiled VALU SAB gather (sab.hip)
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
@@ -583,7 +584,7 @@ struct Runner {
     g.bias = bias ? bias : h->fptr(w.bias); g.scale = h->fptr(w.scale); g.gelu = gelu;
     g.res = res; g.ldr = ldr; g.offr = offr;
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store;
-    g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel; g.allow_lds = h->gemm_lds;
+    g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel; g.allow_lds = h->gemm_lds; g.allow_pn = h->gemm_pn;
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
     // algorithmic traffic: A once (a 3x3 reads each input pixel once), W per weight set, out
     // (+ residual) once
@@ -1107,6 +1108,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "panel_gemm") h->panel = value != 0;
     else if (n == "dw_rows") h->dw_rows = value != 0;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
+    else if (n == "gemm_pn") h->gemm_pn = value != 0;
     else if (n == "pwdw") h->pwdw = value != 0;
     else if (n == "sab_tile") h->sab_tile = value != 0;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
