@@ -28,6 +28,8 @@
 #include "kernels.h"
 #include "mma.h"
 
+#include <type_traits>
+
 namespace turtle {
 
 constexpr int FT = 8;                 // output tile side
@@ -144,6 +146,34 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
     for (int v = tid; v < 112 * per; v += 256) {
       const int r = v / per, k = C + (v - r * per) * VEC;
       *reinterpret_cast<uint4*>(sX + r * F::XROW + k * ES) = uint4{0u, 0u, 0u, 0u};
+    }
+  }
+  // residual of the output tile, requested now: its HBM latency hides behind the whole tile
+  typedef typename std::conditional<sizeof(T) == 2, uint2, uint4>::type RawRes;
+  RawRes rraw[2][4];
+  int64_t pix[4];
+  bool okp[4];
+  if constexpr (MODE != F_DWONLY) {
+    const T* res = reinterpret_cast<const T*>(a.res);
+    const int nct0 = a.N2 / 16;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int o = p * 16 + (lane & 15);
+      const int y = ty0 + (o >> 3), x = tx0 + (o & 7);
+      okp[p] = y < a.H && x < a.W;
+      pix[p] = ((int64_t)img * a.H + (okp[p] ? y : 0)) * a.W + (okp[p] ? x : 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int n = (wid + 4 * u) * 16 + (lane >> 4) * 4;
+      const bool okc = wid + 4 * u < nct0 && res != nullptr;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const void* ra = okc ? reinterpret_cast<const void*>(res + pix[p] * a.ldr + a.offr + n)
+                             : reinterpret_cast<const void*>(g_zero_fused);
+        if constexpr (sizeof(T) == 2) rraw[u][p] = ld8(ra);
+        else rraw[u][p] = ld16(ra);
+      }
     }
   }
   __syncthreads();
@@ -426,36 +456,21 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
       sb[128 + tid] = a.scale2 ? sv : 1.f;
     }
     T* out = reinterpret_cast<T*>(a.out);
-    const T* res = reinterpret_cast<const T*>(a.res);
-    int64_t pix[4];
-    bool okp[4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const int o = p * 16 + (lane & 15);
-      const int y = ty0 + (o >> 3), x = tx0 + (o & 7);
-      okp[p] = y < a.H && x < a.W;
-      pix[p] = ((int64_t)img * a.H + (okp[p] ? y : 0)) * a.W + (okp[p] ? x : 0);
-    }
     typedef __attribute__((ext_vector_type(4))) float f4;
     f4 rv[2][4];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int n = (wid + 4 * u) * 16 + (lane >> 4) * 4;
-      const bool okc = wid + 4 * u < nct && res != nullptr;
+    for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int p = 0; p < 4; ++p) {
-        const void* ra = okc ? reinterpret_cast<const void*>(res + pix[p] * a.ldr + a.offr + n)
-                             : reinterpret_cast<const void*>(g_zero_fused);
         if constexpr (sizeof(T) == 4) {
-          const uint4 q = ld16(ra);
+          const uint4 q = rraw[u][p];
           rv[u][p] = f4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
         } else {
-          const uint2 q = ld8(ra);
+          const uint2 q = rraw[u][p];
           rv[u][p] = f4{__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
                         __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u)};
         }
       }
-    }
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
