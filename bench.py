@@ -12,8 +12,9 @@ an independent clip replica ("replicas only", scaling weak); value = frames of a
 rank time.
 
 The JSON line also carries
-* roofline: the dominant kernel class (most GPU time in the timed region, measured with HIP
-  events on the forward's stream) priced with its algorithmic bytes or FLOPs per launch;
+* roofline: the dominant kernel launch shape (most GPU time in the timed region, measured with
+  HIP events on the forward's stream) priced with its algorithmic bytes or FLOPs per launch;
+  traffic = its PMC HBM bytes per launch from the committed profiles/r01_pmc_traffic.json;
 * cpu_baseline: the CPU oracle (oracle/turtle_ref.py, fp32 PyTorch CPU restatement of the
   reference) on a bounded 256x256 steady-state sample, scaled to 1080p frames/s by the
   algorithmic FLOP ratio (BASELINE.md §3);
@@ -37,6 +38,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from turtlevsr_amd.model import TurtleHIP  # noqa: E402
+from turtlevsr_amd.replicas import clip_seed, replica_throughput  # noqa: E402
 from turtlevsr_amd.synthetic import synthetic_frames, synthetic_state_dict  # noqa: E402
 
 RES = {"1080p": (1080, 1920), "540p": (540, 960), "256": (256, 256), "128": (128, 128)}
@@ -87,6 +89,64 @@ def cpu_baseline(opt, threads):
     return dt
 
 
+def launch_groups(dump):
+    """Per kernel launch shape (the library's launch tag) of the timed region: summed ms, launches,
+    algorithmic bytes and FLOPs, from the TURTLE_PROF_DUMP per-launch records."""
+    groups = {}
+    if not os.path.exists(dump):
+        return groups
+    with open(dump) as f:
+        for line in f:
+            parts = line.rstrip("\n").split("\t")
+            if len(parts) < 5:
+                continue
+            g = groups.setdefault(parts[4], dict(ms=0.0, launches=0, bytes=0.0, flops=0.0))
+            g["ms"] += float(parts[1]); g["launches"] += 1
+            g["bytes"] += float(parts[2]); g["flops"] += float(parts[3])
+    return groups
+
+
+def pmc_traffic():
+    """HBM bytes per launch by launch tag, from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes (tools/pmc_traffic.py; FETCH_SIZE doubled for the gfx950 wide-read undercount)."""
+    path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f).get("per_tag", {})
+
+
+def roofline(prof, dump, steps, dtype):
+    """Roofline of the dominant kernel: the launch shape with the most GPU time in the timed region,
+    its algorithmic bytes (or FLOPs) per launch over its average launch duration (HIP events on the
+    forward's stream); traffic = PMC HBM bytes per launch of that shape, when profiled."""
+    groups = launch_groups(dump)
+    if not groups:
+        return None
+    tag = max(groups, key=lambda k: groups[k]["ms"])
+    g = groups[tag]
+    n = max(g["launches"], 1)
+    avg_s = g["ms"] * 1e-3 / n
+    bpl, fpl = g["bytes"] / n, g["flops"] / n
+    ridge = MFMA_PEAK[dtype] * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if fpl / max(bpl, 1.0) < ridge:
+        ach = bpl / avg_s / 1e9
+        roof = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4))
+    else:
+        ach = fpl / avg_s / 1e12
+        roof = dict(bound="mfma", achieved=round(ach, 2), peak=MFMA_PEAK[dtype], unit="TFLOP/s",
+                    frac=round(ach / MFMA_PEAK[dtype], 4))
+    tr = pmc_traffic().get(tag)
+    roof.update(traffic=round(tr["hbm_bytes_per_launch"]) if tr else None, kernel=tag,
+                launches_per_step=g["launches"] / steps, avg_launch_us=round(avg_s * 1e6, 2),
+                algorithmic_bytes_per_launch=round(bpl), algorithmic_flops_per_launch=round(fpl),
+                mfma_tflops=round(fpl / avg_s / 1e12, 2), hbm_gbs=round(bpl / avg_s / 1e9, 1),
+                class_ms_per_step={k: round(v["ms"] / steps, 3) for k, v in prof.items()},
+                top_launch_shapes_ms_per_step={k: round(groups[k]["ms"] / steps, 3)
+                                               for k in sorted(groups, key=lambda k: -groups[k]["ms"])[:6]})
+    return roof
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,7 +170,7 @@ def main():
     opt = load_opt()
 
     model = build_model(opt, args.dtype, dev)
-    frames = clip_frames(h, w, 100 + rank, dev)
+    frames = clip_frames(h, w, clip_seed(rank), dev)
     kc = vc = None
     j = 0
 
@@ -128,6 +188,10 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
+        dump = os.path.join("/tmp", f"turtle_bench_launches_{os.getpid()}.tsv")
+        if os.path.exists(dump):
+            os.remove(dump)
+        os.environ["TURTLE_PROF_DUMP"] = dump        # per-launch records of the timed region
         model.profile_begin("all")
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -138,31 +202,13 @@ def main():
             dist.barrier()
         elapsed = time.perf_counter() - t0
         prof = model.profile_end()
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    tmax = float(t.item())
-    frames_total = args.steps * world
-    fps = frames_total / tmax
+        os.environ.pop("TURTLE_PROF_DUMP", None)
+    rep = replica_throughput(elapsed, args.steps, dev)
+    tmax, fps = rep.t_max, rep.value
 
-    # dominant kernel class in the timed region
-    dom = max(prof, key=lambda k: prof[k]["ms"])
-    pd = prof[dom]
-    per_launch_ms = pd["ms"] / max(pd["launches"], 1)
-    gbs = pd["bytes"] / (pd["ms"] * 1e-3) / 1e9 if pd["ms"] > 0 else 0.0
-    tfs = pd["flops"] / (pd["ms"] * 1e-3) / 1e12 if pd["ms"] > 0 else 0.0
-    # bound: arithmetic intensity of the class vs the MFMA ridge
-    ridge = MFMA_PEAK[args.dtype] * 1e12 / (HBM_PEAK_GBS * 1e9)
-    ai = pd["flops"] / max(pd["bytes"], 1.0)
-    if ai < ridge:
-        roof = dict(bound="hbm", achieved=round(gbs, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(gbs / HBM_PEAK_GBS, 4))
-    else:
-        roof = dict(bound="mfma", achieved=round(tfs, 2), peak=MFMA_PEAK[args.dtype], unit="TFLOP/s",
-                    frac=round(tfs / MFMA_PEAK[args.dtype], 4))
-    roof.update(kernel=dom, launches_per_step=pd["launches"] / args.steps, avg_launch_us=round(per_launch_ms * 1e3, 2),
-                algorithmic_bytes_per_launch=pd["bytes"] / max(pd["launches"], 1),
-                algorithmic_flops_per_launch=pd["flops"] / max(pd["launches"], 1), traffic=None,
-                class_ms_per_step={k: round(v["ms"] / args.steps, 3) for k, v in prof.items()})
+    roof = roofline(prof, dump, args.steps, args.dtype)
+    if os.path.exists(dump):
+        os.remove(dump)
 
     psnr = None
     if not args.no_psnr and rank == 0 and args.dtype == "bf16":
