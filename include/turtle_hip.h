@@ -123,6 +123,9 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
  *                 the input width is <= 128; 0: separate GEMM + depthwise launches
  *   "panel_gemm"  1 (default): panel GEMM for bf16 plain 1x1 convolutions with K <= 512;
  *                 0: K-loop GEMM everywhere
+ *   "gemm_pn"     1 (default): persistent resident-panel bf16 GEMM for 1x1 convolutions with
+ *                 K in {64, 128, 256, 384, 512} and N % 64 == 0 (LayerNorm applied to the LDS
+ *                 panel in place); 0: the kernels below
  *   "gemm_lds"    1 (default): LDS-pipelined bf16 GEMM (global_load_lds double buffering)
  *                 wherever its alignment rules hold; 0: panel / K-loop GEMMs
  *   "pwdw"        0 (default; 1 = on): pointwise GEMM -> depthwise 3x3 (-> gate) in one kernel for bf16

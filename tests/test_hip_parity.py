@@ -132,3 +132,20 @@ def test_set_option_rejects_unknown():
     m = _model(meta, "fp32")
     with pytest.raises(RuntimeError):
         m.set_option("no_such_switch", 1)
+
+
+def test_biasfree_layernorm_gemm_variants():
+    """BiasFree LayerNorm (x * rstd, uncentred: turtle_t1_arch.py:68-80) at GoPro widths, where the
+    resident-panel GEMM applies the LayerNorm to its LDS panel: bf16 with gemm_pn on vs off agree
+    (>= 50 dB) and both stay >= 45 dB from the fp32 build (golden tiny clips are too narrow to
+    reach that kernel)."""
+    from turtlevsr_amd.synthetic import synthetic_frames
+    _, meta = load("clip_gopro_64")
+    meta = dict(meta, opt=dict(meta["opt"], LayerNorm_type="BiasFree"))
+    clip = synthetic_frames((1, 3, 3, 128, 128), 5)
+    ref = _run(_model(meta, "fp32"), clip)[0]
+    on = _run(_opts(_model(meta, "bf16"), {"gemm_pn": 1}), clip)[0]
+    off = _run(_opts(_model(meta, "bf16"), {"gemm_pn": 0}), clip)[0]
+    for j in range(len(ref)):
+        assert psnr(on[j].numpy(), off[j].numpy()) >= 50.0, j
+        assert psnr(on[j].numpy(), ref[j].numpy()) >= 45.0, j

@@ -242,7 +242,8 @@ __global__ __launch_bounds__(512, 1) void gemm_pn_kernel(GemmArgs g, int npanel)
       }
 #pragma unroll
       for (int o = 1; o < TPR; o <<= 1) { ls += __shfl_xor(ls, o, 64); lq += __shfl_xor(lq, o, 64); }
-      const float mu = ls / KP, rs = rsqrtf(fmaxf(lq / KP - mu * mu, 0.f) + 1e-5f), nm = -mu * rs;
+      // BiasFree LayerNorm (packed with ln_s = null): x * rstd, uncentred (turtle_t1_arch.py:68-80)
+      const float mu = ls / KP, rs = rsqrtf(fmaxf(lq / KP - mu * mu, 0.f) + 1e-5f), nm = g.ln_s ? -mu * rs : 0.f;
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
         const uint32_t w[4] = {xs[j].x, xs[j].y, xs[j].z, xs[j].w};
