@@ -66,6 +66,8 @@ int main(int argc, char** argv) {
   for (auto& v : h2) v = (uint32_t)f2bf((rand() / (float)RAND_MAX - 0.5f) * 0.3f) | ((uint32_t)f2bf((rand() / (float)RAND_MAX - 0.5f) * 0.3f) << 16);
   CK(hipMalloc(&dww2, 5 * 640 * 4));
   CK(hipMemcpy(dww2, h2.data(), 5 * 640 * 4, hipMemcpyHostToDevice));
+  unsigned long long* stamps = nullptr;
+  CK(hipMalloc(&stamps, 3 * 4 * 64 * 8));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
@@ -82,7 +84,7 @@ int main(int argc, char** argv) {
     a.w2 = W2; a.N2 = s.N2; a.b2 = vec + 12288; a.scale2 = vec + 13312;
     a.res = R; a.ldr = s.N2; a.offr = 0;
     a.out = O; a.ldo = s.N2; a.offo = 0;
-    a.ndst = 0; a.dbg = dbg;
+    a.ndst = 0; a.dbg = dbg; a.stamps = (dbg & 64) ? stamps : nullptr;
     launch_fused<bf16>(a, 0);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0, 0));
@@ -92,6 +94,18 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / reps;
+    if (dbg & 64) {           // stamps of the last launch: blocks 0, 1, 16000, waves 0-3 (cycles between stamps)
+      std::vector<unsigned long long> hs(3 * 4 * 64);
+      CK(hipMemcpy(hs.data(), stamps, hs.size() * 8, hipMemcpyDeviceToHost));
+      for (int b = 0; b < 3; ++b)
+        for (int w = 0; w < 4; w += 3) {
+          const unsigned long long* q = hs.data() + (b * 4 + w) * 64;
+          printf("  stamps blk %d wave %d:", b, w);
+          for (int i = 1; i < 64 && q[i] > q[i - 1] && q[i] - q[0] < (1ull << 32); ++i) printf(" %llu", q[i] - q[i - 1]);
+          printf("\n");
+        }
+      CK(hipMemset(stamps, 0, hs.size() * 8));
+    }
     const double px = (double)s.H * s.W;
     const double by = px * 2.0 * (s.C + 2.0 * s.N2);          // x in, residual in, out
     const double fl = px * 2.0 * ((double)s.C * s.N1 + (double)a.hidden * s.N2);

@@ -79,6 +79,16 @@ TURTLE_DEV void unpack8(const uint4& q, float* v) {
   }
 }
 
+// s_memtime stamp into a tools/fbench buffer (blocks 0, 1 and 16000; null in the product path)
+TURTLE_DEV void f_stamp(unsigned long long* buf, int& si) {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  if (buf && si < 63) {
+    asm volatile("global_store_dwordx2 %0, %1, off" : : "v"(buf + si), "v"(t) : "memory");
+    ++si;
+  }
+}
+
 template <typename T, int MODE, int CM>
 __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
   using F = F3<T, MODE, CM>;
@@ -95,6 +105,11 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
   // derived from it then compile to scalar loads
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* sHw = smem + F::OFF_H + wid * 112 * F::HROW;   // this wave's private strip
+  const int sblk = blockIdx.x == 0 ? 0 : (blockIdx.x == 1 ? 1 : (blockIdx.x == 16000 ? 2 : -1));
+  unsigned long long* sbuf = a.stamps && sblk >= 0 && lane == 0 ? a.stamps + (sblk * 4 + wid) * 64 : nullptr;
+  int si = 0;
+#define FST() do { if (a.stamps) f_stamp(sbuf, si); } while (0)
+  FST();
   // ---- tile of this block (XCD-aware: neighbouring tiles share an L2) ----
   const int tx_n = (a.W + FT - 1) / FT, ty_n = (a.H + FT - 1) / FT;
   int lin = blockIdx.x;
@@ -177,6 +192,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
     }
   }
   __syncthreads();
+  FST();
   if (a.ln && tid < 224) {
     // LayerNorm statistics of the 112 staged rows: 2 threads per row, shifted sums
     const int lr = tid >> 1, lh = tid & 1;
@@ -215,6 +231,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
     __syncthreads();
   }
 
+  FST();
   // per-lane constants of the GEMM1 epilogue: 1 for haloed rows inside the image (the bias is
   // added there only; the depthwise conv zero-pads its input at the image border)
   float rowin[FMT];
@@ -268,6 +285,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
           for (int t = 0; t < FMT; ++t) acc1[t] = mfma(wf[kk], frag_at<T>(sX + t * 16 * F::XROW, F::XROW, kk * KF, lane), acc1[t]);
         }
       }
+      FST();
       if (s + 4 < s_end) fetch(s + 4);                  // next slice's operands, behind this one
       // epilogue -> wave strip [112][16]
 #pragma unroll
@@ -287,6 +305,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
       // view of the data dependence through LDS needs a fence
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
+      FST();
       // depthwise 3x3 at pixel (oy, ox): 16 channels, wave-uniform tap weights (scalar loads,
       // issued one step ahead; uniform offsets computed on the scalar unit)
       float d[16];
@@ -357,6 +376,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
           for (int i = 0; i < 16; ++i) asm volatile("" : "+v"(d[i]));
         }
       }
+      FST();
       if constexpr (MODE == F_DWONLY) {
         const int y = ty0 + oy, x = tx0 + ox;
         const int ch = s * 16;
@@ -430,6 +450,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
       if (ps > 0) __syncthreads();                     // previous pass's GEMM2 has read sG
       phase_a(h0 / SL, (h0 + hw) / SL);
       __syncthreads();
+      FST();
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (wid + 4 * u >= nct) continue;
@@ -444,6 +465,7 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
       }
     }
 
+    FST();
     // ---- epilogue: + b2, * scale, + residual, store (4 consecutive channels per lane; N2 % 16 == 0).
     // b2 / scale2 come from LDS, all residual loads are issued unconditionally before any use.
     float* sb = reinterpret_cast<float*>(smem + F::OFF_H);   // the strips are free after phase A
@@ -493,6 +515,8 @@ __global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
       }
     }
   }
+  FST();
+#undef FST
 }
 
 template <typename T, int CM>

@@ -194,6 +194,7 @@ struct FusedArgs {                 // fused.hip: [LN ->] pw -> dw3x3 -> [act -> 
   void* out; int64_t ldo; int offo;
   FusedDst dst[3]; int ndst;
   int dbg;                         // tools/fbench ablations (0 in the product path)
+  unsigned long long* stamps;      // tools/fbench s_memtime stamps (null in the product path)
 };
 template <typename T> void launch_fused(const FusedArgs& a, hipStream_t st);
 

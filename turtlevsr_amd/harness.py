@@ -1,0 +1,191 @@
+"""Evaluation harness around the frame path: whole-frame and tiled causal
+inference over a video, uint8 PSNR / SSIM — the protocol the reference's published numbers use.
+
+Restates basicsr/inference.py:
+* `run_inference_patched` (172-246): reflect-pad right/bottom to a multiple of 8, tiles of side
+  `min(tile, h, w)` at stride `tile - tile_overlap` (last tile flush with the border), one history
+  cache per tile position carried to the next frame, overlapping outputs averaged, clamp to [0, 1];
+  SR ("SR" model type) feeds each tile bicubic-downsampled by 4;
+* `run_inference` (260-350): frame 0 is its own previous frame; outputs cropped to the GT size;
+  PSNR on `tensor2img` uint8 images (or the BT.601 Y channel), SSIM with a Gaussian window;
+* `calc_PSNR` (52-61), `ssim_calculate` (31-50), `bgr2ycbcr` (63-84), `tensor2img`
+  (basicsr/utils/img_util.py:42-104, 3-D RGB case).
+`model` is any callable `model(x[B, 2, C, H, W], k_cached, v_cached) -> (out, k, v)`: the HIP module
+(turtlevsr_amd.model / basicsr.models.archs.turtle_t1_arch) in production; tests also drive the
+oracle through it. Caches stay on the model's device (the reference round-trips them through host
+memory per tile; `cache_device="cpu"` reproduces that)."""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def tile_starts(size: int, tile: int, stride: int) -> list[int]:
+    """Tile origins along one axis (inference.py:198-199): every `stride` below `size - tile`, then
+    `size - tile` itself."""
+    return list(range(0, size - tile, stride)) + [size - tile]
+
+
+def pad_to_multiple(x: torch.Tensor, multiple: int = 8) -> torch.Tensor:
+    """Reflect-pad right/bottom to a multiple (inference.py:185-190; no pad when already a multiple)."""
+    h, w = x.shape[-2], x.shape[-1]
+    H = ((h + multiple) // multiple) * multiple
+    W = ((w + multiple) // multiple) * multiple
+    padh = H - h if h % multiple != 0 else 0
+    padw = W - w if w % multiple != 0 else 0
+    if padh == 0 and padw == 0:
+        return x
+    return F.pad(x, (0, padw, 0, padh), "reflect")
+
+
+def _to(lst, dev):
+    return None if lst is None else [None if t is None else t.to(dev) for t in lst]
+
+
+def run_inference_patched(img_lq_prev: torch.Tensor, img_lq_curr: torch.Tensor, model, tile: int, tile_overlap: int,
+                          prev_patch_dict_k: dict | None = None, prev_patch_dict_v: dict | None = None,
+                          img_multiple_of: int = 8, model_type: str = "t1", cache_device=None):
+    """One frame, tile by tile (inference.py:172-246). Inputs [B, C, H, W] on the model's device.
+    Returns (restored [B, C, Hpad, Wpad] in [0, 1], patch_dict_k, patch_dict_v)."""
+    img_lq_curr = pad_to_multiple(img_lq_curr, img_multiple_of)
+    img_lq_prev = pad_to_multiple(img_lq_prev, img_multiple_of)
+    b, c, h, w = img_lq_curr.shape
+    tile = min(tile, h, w)
+    if tile % 8 != 0:
+        raise ValueError("tile size should be multiple of 8")
+    stride = tile - tile_overlap
+    E = torch.zeros(b, c, h, w, dtype=torch.float32, device=img_lq_curr.device)
+    Wt = torch.zeros_like(E)
+    patch_dict_k, patch_dict_v = {}, {}
+    for h_idx in tile_starts(h, tile, stride):
+        for w_idx in tile_starts(w, tile, stride):
+            cur = img_lq_curr[..., h_idx:h_idx + tile, w_idx:w_idx + tile]
+            prev = img_lq_prev[..., h_idx:h_idx + tile, w_idx:w_idx + tile]
+            if model_type == "SR":
+                prev = F.interpolate(prev, scale_factor=1 / 4, mode="bicubic")
+                cur = F.interpolate(cur, scale_factor=1 / 4, mode="bicubic")
+            x = torch.stack((prev, cur), dim=1).float().contiguous()
+            key = f"{h_idx}-{w_idx}"
+            k_old = _to(prev_patch_dict_k[key], x.device) if prev_patch_dict_k is not None else None
+            v_old = _to(prev_patch_dict_v[key], x.device) if prev_patch_dict_v is not None else None
+            out_patch, k_c, v_c = model(x, k_old, v_old)
+            patch_dict_k[key] = _to(k_c, cache_device) if cache_device is not None else k_c
+            patch_dict_v[key] = _to(v_c, cache_device) if cache_device is not None else v_c
+            E[..., h_idx:h_idx + tile, w_idx:w_idx + tile] += out_patch.float()
+            Wt[..., h_idx:h_idx + tile, w_idx:w_idx + tile] += 1.0
+    restored = torch.clamp(E / Wt, 0, 1)
+    return restored, patch_dict_k, patch_dict_v
+
+
+def tensor2img(t: torch.Tensor) -> np.ndarray:
+    """[C, H, W] (or [1, C, H, W]) in [0, 1] -> uint8 HWC, rounded (img_util.py:73-100, RGB kept)."""
+    x = t.squeeze(0).float().detach().cpu().clamp(0, 1).numpy().transpose(1, 2, 0)
+    if x.shape[2] == 1:
+        x = x[:, :, 0]
+    return (x * 255.0).round().astype(np.uint8)
+
+
+def calc_PSNR(img1: np.ndarray, img2: np.ndarray) -> float:
+    """PSNR of two [0, 255] images (inference.py:52-61)."""
+    mse = np.mean((img1.astype(np.float64) - img2.astype(np.float64)) ** 2)
+    if mse == 0:
+        return float("inf")
+    return 20 * math.log10(255.0 / math.sqrt(mse))
+
+
+def bgr2ycbcr(img: np.ndarray, only_y: bool = True) -> np.ndarray:
+    """BT.601 Y (or YCbCr) of a BGR image, uint8 or float [0, 1] (inference.py:63-84)."""
+    in_type = img.dtype
+    x = img.astype(np.float64)
+    if in_type != np.uint8:
+        x = x * 255.0
+    if only_y:
+        r = np.dot(x, [24.966, 128.553, 65.481]) / 255.0 + 16.0
+    else:
+        r = np.matmul(x, [[24.966, 112.0, -18.214], [128.553, -74.203, -93.786], [65.481, -37.797, 112.0]]) / 255.0 + [16, 128, 128]
+    if in_type == np.uint8:
+        r = r.round()
+    else:
+        r = r / 255.0
+    return r.astype(in_type)
+
+
+def ssim_calculate(img1: np.ndarray, img2: np.ndarray, sd: float = 1.5, C1: float = 0.01 ** 2, C2: float = 0.03 ** 2) -> float:
+    """Gaussian-window SSIM of two [0, 255] images (inference.py:31-50; the window runs over every
+    axis of the array, channels included, as scipy.ndimage.gaussian_filter does there)."""
+    from scipy.ndimage import gaussian_filter
+    a = np.asarray(img1, dtype=np.float32) / 255
+    b = np.asarray(img2, dtype=np.float32) / 255
+    mu1, mu2 = gaussian_filter(a, sd), gaussian_filter(b, sd)
+    s1 = gaussian_filter(a * a, sd) - mu1 * mu1
+    s2 = gaussian_filter(b * b, sd) - mu2 * mu2
+    s12 = gaussian_filter(a * b, sd) - mu1 * mu2
+    num = (2 * mu1 * mu2 + C1) * (2 * s12 + C2)
+    den = (mu1 * mu1 + mu2 * mu2 + C1) * (s1 + s2 + C2)
+    return float(np.mean(num / den))
+
+
+@dataclass
+class VideoScores:
+    psnr: list = field(default_factory=list)
+    ssim: list = field(default_factory=list)
+    outputs: list = field(default_factory=list)
+
+    @property
+    def mean_psnr(self) -> float:
+        return float(np.mean(self.psnr)) if self.psnr else float("nan")
+
+
+def run_video(frames_lq, frames_gt, model, tile: int | None = None, tile_overlap: int = 0, y_channel_PSNR: bool = False,
+              model_type: str = "t1", keep_outputs: bool = False, cache_device=None) -> VideoScores:
+    """Causal restoration of one video and its per-frame PSNR / SSIM (inference.py:260-350).
+    `frames_lq` / `frames_gt`: sequences of [C, H, W] tensors in [0, 1] (LQ on the model's device);
+    `tile=None` runs whole frames."""
+    res = VideoScores()
+    prev = None
+    k_cache = v_cache = None
+    for cur, gt in zip(frames_lq, frames_gt):
+        if prev is None:
+            prev = cur
+        c, h, w = gt.shape
+        if tile is not None:
+            out, k_cache, v_cache = run_inference_patched(prev.unsqueeze(0), cur.unsqueeze(0), model, tile, tile_overlap,
+                                                          k_cache, v_cache, model_type=model_type, cache_device=cache_device)
+        else:
+            p, q = prev.unsqueeze(0), cur.unsqueeze(0)
+            if model_type == "SR":
+                p = F.interpolate(p, scale_factor=1 / 4, mode="bicubic")
+                q = F.interpolate(q, scale_factor=1 / 4, mode="bicubic")
+            x = torch.stack((p, q), dim=1).float().contiguous()
+            out, k_cache, v_cache = model(x, k_cache, v_cache)
+        out = out.squeeze(0)[:, :h, :w]
+        if y_channel_PSNR:
+            gy = bgr2ycbcr(tensor2img(gt)[:, :, ::-1])
+            oy = bgr2ycbcr(tensor2img(out)[:, :, ::-1])
+            res.psnr.append(calc_PSNR(oy, gy))
+            res.ssim.append(ssim_calculate(oy, gy))
+        else:
+            o8, g8 = tensor2img(out), tensor2img(gt)
+            res.psnr.append(calc_PSNR(o8, g8))
+            res.ssim.append(ssim_calculate(o8, g8))
+        if keep_outputs:
+            res.outputs.append(out.detach().float().cpu())
+        prev = cur
+    return res
+
+
+def load_checkpoint(model: torch.nn.Module, path: str, key: str = "params", strict: bool = True):
+    """Trained weights from a reference checkpoint (inference.py:248-255,
+    base_model.py:261-286): `torch.load(path)[key]` with a leading `module.` (DataParallel /
+    DistributedDataParallel) stripped, loaded strictly into the model (633 keys for Turtle_t1).
+    Loaded with weights_only=True: a checkpoint is data, never executed."""
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    sd = ckpt[key] if isinstance(ckpt, dict) and key in ckpt else ckpt
+    if not isinstance(sd, dict):
+        raise ValueError(f"{path}: no state dict under '{key}'")
+    sd = {(k[7:] if k.startswith("module.") else k): v for k, v in sd.items()}
+    return model.load_state_dict(sd, strict=strict)
