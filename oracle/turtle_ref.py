@@ -44,6 +44,7 @@ class Block:
     heads: int
     ntc: int               # num_frames_tocache
     ws: int                # SAB window size = 2 * Scale_patchsize
+    t0: bool = False       # "Turtle" (turtle_arch.py) StateAlignBlock instead of Turtle_t1's
 
 
 @dataclass
@@ -90,14 +91,22 @@ def arch_from_opt(opt: dict) -> dict:
         "refinement": level("refinement", dim, opt.get("num_refinement_blocks", 1), o["refinement_attn_type1"], o["refinement_attn_type2"], o["refinement_ffw_type"], heads[0], ntc, 1),
     }
     known = {"ReducedAttn", "Channel", "FHR", "CHM", "NoAttn"}
+    t0 = is_t0(opt)
     for lv in levels.values():
         for b in lv.blocks:
+            b.t0 = t0
             if b.attn not in known:
                 raise ValueError(f"attention type {b.attn!r} not defined")
             if b.ffn not in ("FFW", "GFFW"):
                 raise ValueError(f"FFW type {b.ffn!r} not defined")
     return dict(levels=levels, dim=dim, ffe=ffe, use_both=bool(opt["use_both_input"]),
-                ln_type=opt.get("LayerNorm_type", "WithBias"), ntc=ntc)
+                ln_type=opt.get("LayerNorm_type", "WithBias"), ntc=ntc, t0=t0)
+
+
+def is_t0(opt: dict) -> bool:
+    """The option file's `model` selects the arch module (video_restoration_model.py:18-21):
+    Turtle_arch -> the t0 network (turtle_arch.py), otherwise Turtle_t1 / TurtleSuper_t1."""
+    return str(opt.get("model", "")).lower() in ("turtle_arch", "turtle")
 
 
 # ----------------------------------------------------------------------------------------------
@@ -227,11 +236,63 @@ def state_align(sd: SD, p: str, x: Tensor, ws: int, ntc: int,
     return o, k[:, -ntc:], vt[:, -ntc:]
 
 
-def causal_history(sd: SD, p: str, x: Tensor, heads: int, ws: int, ntc: int,
+def positional_encoding_2d(d_model: int, height: int, width: int) -> Tensor:
+    """Sinusoidal 2-D encoding of the t0 StateAlignBlock (turtle_arch.py:412-439): the first half
+    of the channels encodes the column (sin / cos interleaved), the second half the row."""
+    if d_model % 4 != 0:
+        raise ValueError(f"Cannot use sin/cos positional encoding with odd dimension (got dim={d_model})")
+    pe = torch.zeros(d_model, height, width)
+    half = d_model // 2
+    div = torch.exp(torch.arange(0.0, half, 2) * -(math.log(10000.0) / half))
+    pos_w = torch.arange(0.0, width).unsqueeze(1)
+    pos_h = torch.arange(0.0, height).unsqueeze(1)
+    pe[0:half:2] = torch.sin(pos_w * div).transpose(0, 1).unsqueeze(1).repeat(1, height, 1)
+    pe[1:half:2] = torch.cos(pos_w * div).transpose(0, 1).unsqueeze(1).repeat(1, height, 1)
+    pe[half::2] = torch.sin(pos_h * div).transpose(0, 1).unsqueeze(2).repeat(1, 1, width)
+    pe[half + 1::2] = torch.cos(pos_h * div).transpose(0, 1).unsqueeze(2).repeat(1, 1, width)
+    return pe
+
+
+def _dilated_tokens(t: Tensor, ws: int) -> Tensor:
+    """'b d (p1 h) (p2 w) -> b 1 1 (h w) (p1 p2 d)' (turtle_t1_arch.py:573-574, turtle_arch.py:487-492)."""
+    b, c, hl, wl = t.shape
+    hh, ww_ = hl // ws, wl // ws
+    return t.reshape(b, c, ws, hh, ws, ww_).permute(0, 3, 5, 2, 4, 1).reshape(b, 1, 1, hh * ww_, ws * ws * c)
+
+
+def state_align_t0(sd: SD, p: str, x: Tensor, ws: int, ntc: int,
                    k_cached: Optional[Tensor], v_cached: Optional[Tensor]):
+    """StateAlignBlock of the t0 network, live forward turtle_arch.py:459-533 (the later of the
+    class's two `forward` definitions). q/k come from x + a 2-D positional encoding, all of q, k, v
+    are dilated token groups (one head), q/k L2-normalised over ws*ws*c. The attention is computed
+    and then discarded (`out = v`, 521-523): the output is project_out of every frame's v, the
+    caches are the last ntc frames of k and v. The discarded attention still runs top-5 over the
+    keys, so fewer than 5 tokens raises like the reference."""
+    b, c, hl, wl = x.shape
+    pos = positional_encoding_2d(c, hl, wl).to(x.dtype)
+    qk = _dw(sd, p + ".qk_dwconv", _conv(sd, p + ".qk", x + pos))
+    k = qk[:, c:]
+    v = _dw(sd, p + ".v_dwconv", _conv(sd, p + ".v", x))
+    hh, ww_ = hl // ws, wl // ws
+    if hh * ww_ < SAB_TOPK:
+        raise RuntimeError("selected index k out of range")
+    kt = l2n(_dilated_tokens(k, ws), -1)
+    vt = _dilated_tokens(v, ws)
+    if k_cached is not None and v_cached is not None:
+        kt = torch.cat([k_cached, kt], dim=1)
+        vt = torch.cat([v_cached, vt], dim=1)
+    t = vt.shape[1]
+    o = vt.reshape(b * t, hh, ww_, ws, ws, c).permute(0, 5, 3, 1, 4, 2).reshape(b * t, c, hl, wl)
+    o = _conv(sd, p + ".project_out", o).reshape(b, t, c, hl, wl)
+    return o, kt[:, -ntc:], vt[:, -ntc:]
+
+
+def causal_history(sd: SD, p: str, x: Tensor, heads: int, ws: int, ntc: int,
+                   k_cached: Optional[Tensor], v_cached: Optional[Tensor], t0: bool = False):
     """CausalHistoryModel 612-662: SAB -> kv conv on the aligned frames -> FHR(x, k_hist, v_hist)."""
     b, c, h, w = x.shape
-    xs, k_keep, v_keep = state_align(sd, p + ".spatial_aligner", x, ws, ntc, k_cached, v_cached)
+    sab = state_align_t0 if t0 else state_align
+    xs, k_keep, v_keep = sab(sd, p + ".spatial_aligner", x, ws, ntc, k_cached, v_cached)
     t = xs.shape[1]
     kv = _dw(sd, p + ".kv_dwconv", _conv(sd, p + ".kv", xs.reshape(b * t, c, h, w)))
     kh, vh = kv[:, :c], kv[:, c:]
@@ -256,7 +317,7 @@ def turtle_block(sd: SD, blk: Block, x: Tensor, ln_type: str, ffe: float,
         elif blk.attn == "FHR":
             a, kc, vc = frame_history_router(sd, p + ".attn", y, blk.heads, blk.ntc, k_cached, v_cached)
         else:  # CHM
-            a, kc, vc = causal_history(sd, p + ".attn", y, blk.heads, blk.ws, blk.ntc, k_cached, v_cached)
+            a, kc, vc = causal_history(sd, p + ".attn", y, blk.heads, blk.ws, blk.ntc, k_cached, v_cached, blk.t0)
         x = x + a
     y = layer_norm(sd, p + ".norm2", x, ln_type)
     x = x + (gated_ffn(sd, p + ".ffn", y) if blk.ffn == "GFFW" else feed_forward(sd, p + ".ffn", y))

@@ -88,6 +88,21 @@ def test_state_align_block():
     close(y, g["y0"]); close(k, g["k0"]); close(v, g["v0"])
 
 
+def test_state_align_block_t0():
+    """t0 StateAlignBlock (turtle_arch.py:459-533): out = project_out(v) of every frame, k tokens
+    from x + positional encoding, dilated and L2-normalised."""
+    from turtlevsr_amd.params import StateAlignParams
+    g, meta = load("block_sab_t0")
+    sd = _block_sd(lambda: StateAlignParams(32, 8, False), seed=meta["seed"])
+    x, kc, vc = (torch.from_numpy(g[k]) for k in ("x", "kc", "vc"))
+    y, k, v = R.state_align_t0(sd, "blk", x, 8, 2, kc, vc)
+    close(y, g["y"]); close(k, g["k"]); close(v, g["v"])
+    y, k, v = R.state_align_t0(sd, "blk", x, 8, 2, None, None)
+    close(y, g["y0"]); close(k, g["k0"]); close(v, g["v0"])
+    with pytest.raises(RuntimeError):                     # < 5 tokens: the discarded top-5 raises
+        R.state_align_t0(sd, "blk", x[..., :16, :16], 8, 2, None, None)
+
+
 def test_causal_history_model():
     from turtlevsr_amd.params import CausalHistoryParams
     g, _ = load("block_chm")
@@ -100,7 +115,7 @@ def test_causal_history_model():
 
 
 CLIPS = ["clip_tiny_64", "clip_tiny_ragged", "clip_tiny_both", "clip_tiny_biasfree", "clip_tiny_sr",
-         "clip_gopro_64"]
+         "clip_gopro_64", "clip_tiny_t0", "clip_gopro_t0"]
 
 
 @pytest.mark.parametrize("name", CLIPS)
