@@ -11,7 +11,7 @@ from turtlevsr_amd.model import TurtleHIP
 
 class Turtle_t1(TurtleHIP):
     def __init__(self, opt: dict, dtype: str = "fp32"):
-        super().__init__(opt, sr=False, dtype=dtype)
+        super().__init__(opt, sr=False, dtype=dtype, t0=False)
 
 
 def make_model(opt):

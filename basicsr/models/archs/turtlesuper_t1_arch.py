@@ -9,7 +9,7 @@ from turtlevsr_amd.model import TurtleHIP
 
 class TurtleSuper_t1(TurtleHIP):
     def __init__(self, opt: dict, dtype: str = "fp32"):
-        super().__init__(opt, sr=True, dtype=dtype)
+        super().__init__(opt, sr=True, dtype=dtype, t0=False)
 
 
 def make_model(opt):

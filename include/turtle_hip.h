@@ -58,6 +58,8 @@ typedef struct TurtleConfig {
   int latent_ffn;
   int super_resolution;     /* 1: TurtleSuper_t1 (4x bilinear front-end) */
   int dtype;                /* TURTLE_DTYPE_* storage / MFMA type; accumulation is fp32 */
+  int variant;              /* 0: Turtle_t1 (turtle_t1_arch.py); 1: the t0 network "Turtle"
+                               (turtle_arch.py: StateAlignBlock 459-533, option `model: Turtle_arch`) */
 } TurtleConfig;
 
 typedef struct TurtleHandle TurtleHandle;
@@ -78,7 +80,7 @@ int turtle_load_weights(TurtleHandle* h);
 /* History-state layout. For cache slot i (0..7, order of Turtle_t1.forward's k_to_cache list):
  *   kind[i] = 0 none, 1 FHR rows, 2 SAB frames.
  *   FHR:  shape [B, heads, rows, P]      with strides (P*heads*rows, rows, 1, heads*rows)
- *   SAB:  k [B, frames, 1, N, 2c], v [B, frames, 1, N, ws*ws*c], contiguous.
+ *   SAB:  k [B, frames, 1, N, 2c] (t0: ws*ws*c), v [B, frames, 1, N, ws*ws*c], contiguous.
  * `t_in[i]` = rows (FHR) / frames (SAB) of the incoming cache (0 when the caller passes None).
  * Writes kind[8], and for each slot the 5-d shapes (unused trailing dims = 1) of the k and v
  * tensors forward() will return: k_shape[i*5 + d], v_shape[i*5 + d]. */

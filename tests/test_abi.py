@@ -76,3 +76,24 @@ def test_errors_are_reported():
     assert rc == -2 and b"missing key" in L.turtle_last_error()
     rc = L.turtle_set_weight(h, b"nope.weight", C.c_void_p(1), 1)
     assert rc == -2
+
+
+def test_t0_variant_layout_and_plugin():
+    """The t0 network (option `model: Turtle_arch`, turtle_arch.py): same state_dict as Turtle_t1,
+    SAB k caches hold dilated ws*ws*c tokens (turtle_arch.py:480-495); SR is t1 only."""
+    o = dict(gopro(), model="Turtle_arch")
+    arch = resolve(o)
+    assert arch.t0 and not resolve(gopro()).t0
+    L, h = handle(o, False, 1)
+    kind, ks, vs = (C.c_int * 8)(), (C.c_int64 * 40)(), (C.c_int64 * 40)()
+    _lib.check(L.turtle_cache_layout(h, 1, 256, 256, (C.c_int * 8)(*([0] * 8)), kind, ks, vs))
+    assert tuple(ks[25:30]) == (1, 1, 1, 256, 4 * 4 * 256)    # dec3 k: D = ws*ws*c
+    assert tuple(ks[35:40]) == tuple(vs[35:40]) == (1, 1, 1, 256, 16 * 16 * 64)
+    L.turtle_destroy(h)
+    cfg = _lib.config_from_arch(arch, True, 0)
+    h2 = C.c_void_p()
+    assert L.turtle_create(C.byref(cfg), C.byref(h2)) != 0
+    from basicsr.models.archs import turtle_arch, turtle_t1_arch
+    m0, m1 = turtle_arch.make_model(o), turtle_t1_arch.make_model(o)
+    assert m0.arch.t0 and not m1.arch.t0          # the module decides, as in the reference
+    assert list(m0.state_dict()) == list(m1.state_dict())

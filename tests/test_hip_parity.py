@@ -14,7 +14,7 @@ from golden_io import check_summary, load, synth_sd
 pytestmark = pytest.mark.gpu
 
 CLIPS = ["clip_tiny_64", "clip_tiny_ragged", "clip_tiny_both", "clip_tiny_biasfree", "clip_tiny_sr",
-         "clip_gopro_64"]
+         "clip_gopro_64", "clip_tiny_t0", "clip_gopro_t0"]
 
 
 def psnr(a, b):
@@ -67,7 +67,7 @@ def test_clip_fp32_vs_reference(name):
                     np.testing.assert_allclose(t.numpy(), g[key], atol=2e-4, rtol=2e-3, err_msg=key)
 
 
-@pytest.mark.parametrize("name", ["clip_tiny_64", "clip_gopro_64"])
+@pytest.mark.parametrize("name", ["clip_tiny_64", "clip_gopro_64", "clip_gopro_t0"])
 def test_clip_bf16_psnr(name):
     g, meta = load(name)
     m = _model(meta, "bf16")

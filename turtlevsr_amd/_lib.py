@@ -23,7 +23,7 @@ class TurtleConfig(C.Structure):
         ("bias", C.c_int), ("layernorm_biasfree", C.c_int), ("use_both_input", C.c_int),
         ("num_frames_tocache", C.c_int), ("num_heads", C.c_int * 4), ("level_attn", (C.c_int * 2) * 7),
         ("level_ffn", C.c_int * 7), ("latent_attn", C.c_int * 3), ("latent_ffn", C.c_int),
-        ("super_resolution", C.c_int), ("dtype", C.c_int),
+        ("super_resolution", C.c_int), ("dtype", C.c_int), ("variant", C.c_int),
     ]
 
 
@@ -105,4 +105,5 @@ def config_from_arch(arch, sr: bool, dtype: int) -> TurtleConfig:
     cfg.latent_ffn = FFN[lb[0].ffn]
     cfg.super_resolution = int(sr)
     cfg.dtype = dtype
+    cfg.variant = int(getattr(arch, "t0", False))
     return cfg

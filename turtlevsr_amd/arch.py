@@ -59,6 +59,7 @@ class TurtleArch:
     ffe: float = 1.0
     heads: tuple = (1, 1, 1, 1)
     type1: Dict[str, str] = field(default_factory=dict)   # raw attn_type1 per level (+ latent_mid)
+    t0: bool = False     # option `model: Turtle_arch` -> the t0 network (turtle_arch.py)
 
     @property
     def order(self):
@@ -118,4 +119,10 @@ def resolve(opt: dict) -> TurtleArch:
              "refinement": o["refinement_attn_type1"], "latent_mid": o["latent_attn_type2"]}
     return TurtleArch(dim=dim, in_ch=n_col * (2 if use_both else 1), out_ch=n_col, bias=bias,
                       ln_type=o.get("LayerNorm_type", "WithBias"), use_both=use_both, ntc=ntc,
-                      levels=levels, ffe=ffe, heads=tuple(heads), type1=type1)
+                      levels=levels, ffe=ffe, heads=tuple(heads), type1=type1, t0=is_t0(o))
+
+
+def is_t0(opt: dict) -> bool:
+    """`model` selects the arch module (video_restoration_model.py:18-21): Turtle_arch is the t0
+    network (turtle_arch.py, StateAlignBlock 459-533), anything else Turtle_t1 / TurtleSuper_t1."""
+    return str(opt.get("model", "")).lower() in ("turtle_arch", "turtle")

@@ -212,4 +212,19 @@ void launch_pwdw(const PwdwArgs& a, hipStream_t st);
 
 void launch_cast_f32(const float* src, void* dst, int64_t n, int to_bf16, hipStream_t st);
 
+// t0 StateAlignBlock (turtle_arch.py:459-533), t0.hip
+struct T0PeArgs {                  // 2-D sinusoidal encoding (turtle_arch.py:412-439), [H*W][C]
+  void* out; int H, W, C;
+};
+template <typename T> void launch_t0_pe(const T0PeArgs& a, hipStream_t st);
+struct T0KnormArgs {               // k[b][n][:] = normalize(k[b][n][:] + kpos[n][:]) over D features
+  void* k; int64_t k_bstride; const void* kpos; int B, N, D;
+};
+template <typename T> void launch_t0_knorm(const T0KnormArgs& a, hipStream_t st);
+struct T0UntokArgs {               // out[b*T + t] = inverse dilated regroup of v token frame t
+  const void* v[TURTLE_MAX_T]; int64_t v_bstride[TURTLE_MAX_T];   // [N][ws*ws*C]
+  void* out; int B, T, H, W, C, ws;
+};
+template <typename T> void launch_t0_untok(const T0UntokArgs& a, hipStream_t st);
+
 }  // namespace turtle

@@ -77,6 +77,8 @@ static void build_arch(Arch& A) {
   if (c.n_colors < 1 || c.n_colors > 4) TFAIL(TURTLE_EINVAL, "n_colors must be 1..4");
   if (c.middle_blocks < 2) TFAIL(TURTLE_EINVAL, "LatentCacheBlock should have more than 2 layers (turtle_t1_arch.py:899-901)");
   if (c.super_resolution && c.use_both_input) TFAIL(TURTLE_EINVAL, "TurtleSuper_t1 with use_both_input is not runnable in the reference");
+  if (c.variant != 0 && c.variant != 1) TFAIL(TURTLE_EINVAL, "variant must be 0 (Turtle_t1) or 1 (t0 Turtle)");
+  if (c.variant == 1 && c.super_resolution) TFAIL(TURTLE_EINVAL, "the super-resolution network is t1 only (turtlesuper_t1_arch.py)");
   A.dim = c.dim;
   A.in_ch = c.n_colors * (c.use_both_input ? 2 : 1);
   A.out_ch = c.n_colors;
@@ -201,7 +203,8 @@ static void build_arch(Arch& A) {
 struct GemmW { size_t w = NONE, s = NONE, t = NONE, bias = NONE, scale = NONE; int N = 0, K = 0; bool ln = false; };
 struct DwW { size_t w = NONE, bias = NONE, w2 = NONE; int C = 0; };   // w2: bf16 tap pairs [5][C] (u32)
 struct BlockW {
-  GemmW a_in, a_out, q2, k2, kv, f_in, f_out;
+  GemmW a_in, a_out, q2, k2, kv, f_in, f_out, t0_kpw;   // t0_kpw: W_k of the t0 aligner (pos term)
+  DwW t0_kdw;                                           // t0 k-half depthwise taps without bias
   DwW a_dw, sab_qk_dw, sab_v_dw, fhr_dw, kv_dw, f_dw, chm_dw6;
   size_t q2_win = NONE, q2_winb = NONE, k2_win = NONE, k2_winb = NONE, sab_tau = NONE;
   size_t wp = NONE, po_bias = NONE, tau = NONE;   // channel-attention projection (fp32) + temperature
@@ -342,7 +345,7 @@ static std::vector<double> opt_bias(TurtleHandle* h, const std::string& n) {
   return has(h, n) ? dvec(W(h, n)) : std::vector<double>();
 }
 
-static DwW pack_dw(TurtleHandle* h, Packer& pk, const std::string& n, int c0, int C, int taps = 9) {
+static DwW pack_dw(TurtleHandle* h, Packer& pk, const std::string& n, int c0, int C, int taps = 9, bool with_bias = true) {
   // conv weight [Ctot][1][k][k] -> [taps][C] for channels [c0, c0 + C)
   const auto& w = W(h, n + ".weight");
   std::vector<double> o((size_t)taps * C);
@@ -350,7 +353,7 @@ static DwW pack_dw(TurtleHandle* h, Packer& pk, const std::string& n, int c0, in
     for (int t = 0; t < taps; ++t) o[(size_t)t * C + c] = w[(size_t)(c0 + c) * taps + t];
   DwW d; d.C = C; d.w = pk.f32(o);
   if (taps == 9) d.w2 = pk.dw_pairs(o, C);
-  if (has(h, n + ".bias")) {
+  if (with_bias && has(h, n + ".bias")) {
     const auto& b = W(h, n + ".bias");
     d.bias = pk.f32(std::vector<double>(b.begin() + c0, b.begin() + c0 + C));
   }
@@ -358,7 +361,9 @@ static DwW pack_dw(TurtleHandle* h, Packer& pk, const std::string& n, int c0, in
 }
 
 // several depthwise 3x3 convs side by side -> one [9][sum C] table (fused multi-output dw)
-static DwW pack_dw_cat(TurtleHandle* h, Packer& pk, const std::vector<std::string>& names, const std::vector<int>& cs) {
+static DwW pack_dw_cat(TurtleHandle* h, Packer& pk, const std::vector<std::string>& names, const std::vector<int>& cs,
+                       std::vector<int> c0s = {}) {
+  c0s.resize(names.size(), 0);
   int Ct = 0;
   for (int c : cs) Ct += c;
   std::vector<double> o((size_t)9 * Ct), bias;
@@ -368,9 +373,9 @@ static DwW pack_dw_cat(TurtleHandle* h, Packer& pk, const std::vector<std::strin
   for (size_t i = 0; i < names.size(); ++i) {
     const auto& w = W(h, names[i] + ".weight");
     for (int c = 0; c < cs[i]; ++c)
-      for (int t = 0; t < 9; ++t) o[(size_t)t * Ct + c0 + c] = w[(size_t)c * 9 + t];
+      for (int t = 0; t < 9; ++t) o[(size_t)t * Ct + c0 + c] = w[(size_t)(c0s[i] + c) * 9 + t];
     if (any_bias)
-      for (int c = 0; c < cs[i]; ++c) bias.push_back(has(h, names[i] + ".bias") ? W(h, names[i] + ".bias")[c] : 0.0);
+      for (int c = 0; c < cs[i]; ++c) bias.push_back(has(h, names[i] + ".bias") ? W(h, names[i] + ".bias")[c0s[i] + c] : 0.0);
     c0 += cs[i];
   }
   DwW d; d.C = Ct; d.w = pk.f32(o);
@@ -436,26 +441,40 @@ static void pack_all(TurtleHandle* h) {
       } else if (b.attn == TURTLE_ATTN_CHM) {
         const std::string s = a + ".spatial_aligner", ca = a + ".ChanAttn";
         // one LN-folded GEMM for everything that reads norm1(x): [SAB qk | SAB v | FHR qkv]
+        // (t0: the query half of qk is dead, only k = rows [c, 2c) is packed: [k | SAB v | FHR qkv])
+        const bool t0 = A.cfg.variant == 1;
+        const int q0 = t0 ? c : 0;
         std::vector<double> w6, b6;
-        pack_rows(W(h, s + ".qk.weight"), c, 0, 2 * c, w6);
+        pack_rows(W(h, s + ".qk.weight"), c, q0, 2 * c, w6);
         pack_rows(W(h, s + ".v.weight"), c, 0, c, w6);
         pack_rows(W(h, ca + ".qkv.weight"), c, 0, 3 * c, w6);
         if (A.cfg.bias) {
-          for (auto x : W(h, s + ".qk.bias")) b6.push_back(x);
+          const auto& qb = W(h, s + ".qk.bias");
+          for (int i = q0; i < 2 * c; ++i) b6.push_back(qb[i]);
           for (auto x : W(h, s + ".v.bias")) b6.push_back(x);
           for (auto x : W(h, ca + ".qkv.bias")) b6.push_back(x);
         }
-        bw.a_in = pack_gemm(h, pk, w6, 6 * c, c, n1, b6);
-        bw.sab_qk_dw = pack_dw(h, pk, s + ".qk_dwconv", 0, 2 * c);
+        bw.a_in = pack_gemm(h, pk, w6, 6 * c - q0, c, n1, b6);
+        bw.sab_qk_dw = pack_dw(h, pk, s + ".qk_dwconv", q0, 2 * c - q0);
         bw.sab_v_dw = pack_dw(h, pk, s + ".v_dwconv", 0, c);
         bw.fhr_dw = pack_dw(h, pk, ca + ".qkv_dwconv", 0, 3 * c);
-        bw.chm_dw6 = pack_dw_cat(h, pk, {s + ".qk_dwconv", s + ".v_dwconv", ca + ".qkv_dwconv"}, {2 * c, c, 3 * c});
-        bw.q2 = pack_gemm(h, pk, dvec(W(h, s + ".q2.weight")), 2 * c, c, "", opt_bias(h, s + ".q2.bias"));
-        bw.k2 = pack_gemm(h, pk, dvec(W(h, s + ".k2.weight")), 2 * c, c, "", opt_bias(h, s + ".k2.bias"));
-        const int taps = b.ws * b.ws;
-        DwW qw = pack_dw(h, pk, s + ".q2_dwconv", 0, 2 * c, taps), kw = pack_dw(h, pk, s + ".k2_dwconv", 0, 2 * c, taps);
-        bw.q2_win = qw.w; bw.q2_winb = qw.bias; bw.k2_win = kw.w; bw.k2_winb = kw.bias;
-        bw.sab_tau = pk.f32(dvec(W(h, s + ".temperature")));
+        bw.chm_dw6 = pack_dw_cat(h, pk, {s + ".qk_dwconv", s + ".v_dwconv", ca + ".qkv_dwconv"}, {2 * c - q0, c, 3 * c},
+                                 {q0, 0, 0});
+        if (t0) {
+          // W_k (x + pos) = W_k x + W_k pos: the encoding's term is W_k pos through the bias-free taps
+          std::vector<double> wk;
+          pack_rows(W(h, s + ".qk.weight"), c, c, 2 * c, wk);
+          bw.t0_kpw = pack_gemm(h, pk, wk, c, c, "", {});
+          bw.t0_kdw = pack_dw(h, pk, s + ".qk_dwconv", c, c, 9, false);
+        }
+        if (!t0) bw.q2 = pack_gemm(h, pk, dvec(W(h, s + ".q2.weight")), 2 * c, c, "", opt_bias(h, s + ".q2.bias"));
+        if (!t0) {
+          bw.k2 = pack_gemm(h, pk, dvec(W(h, s + ".k2.weight")), 2 * c, c, "", opt_bias(h, s + ".k2.bias"));
+          const int taps = b.ws * b.ws;
+          DwW qw = pack_dw(h, pk, s + ".q2_dwconv", 0, 2 * c, taps), kw = pack_dw(h, pk, s + ".k2_dwconv", 0, 2 * c, taps);
+          bw.q2_win = qw.w; bw.q2_winb = qw.bias; bw.k2_win = kw.w; bw.k2_winb = kw.bias;
+          bw.sab_tau = pk.f32(dvec(W(h, s + ".temperature")));
+        }
         // kv(project_out_sab(o)) = (W_kv W_po) o + (W_kv b_po + b_kv): one GEMM over the T frames
         const auto& wkv = W(h, a + ".kv.weight");
         const auto& wpo = W(h, s + ".project_out.weight");
@@ -815,8 +834,85 @@ struct Runner {
     launch(TURTLE_K_OTHER, ES * (double)B * HW * b.heads * (R + ch + Rnew), 0, [&] { launch_fhr_cache<T>(fv, st); });
   }
 
+  // t0 CausalHistoryModel (turtle_arch.py:535-590): the aligner's attention is discarded
+  // (`out = v`, turtle_arch.py:521-523), so the aligned frames are the v token frames themselves
+  // and only k (for the cache) and v are computed: k = normalize(dilated(dw(qk(x + pos))[k]))
+  void chm_t0(const Blk& b, const BlockW& bw, T* x, int H, int Wd) {
+    const int c = b.dim, HW = H * Wd, ch = c / b.heads, ws = b.ws, slot = b.cache_slot;
+    const int64_t P = (int64_t)B * HW;
+    const int th = H / ws, tw = Wd / ws, N = th * tw;
+    const int64_t D = (int64_t)ws * ws * c;
+    // the discarded attention still runs topk(5) over the keys (turtle_arch.py:509-510)
+    if (N < 5) TFAIL(TURTLE_EINVAL, "selected index k out of range: SAB needs >= 5 tokens (input too small)");
+    const int Tin = slot >= 0 ? io->t_in[slot] : 0;
+    const int NT = Tin + 1;
+    const int Tnew = std::min(NT, b.ntc);
+    if (NT > TURTLE_MAX_T) TFAIL(TURTLE_EINVAL, "too many cached frames");
+    T* kout = slot >= 0 ? reinterpret_cast<T*>(io->k_out[slot]) : buf((int64_t)B * Tnew * N * D);
+    T* vout = slot >= 0 ? reinterpret_cast<T*>(io->v_out[slot]) : buf((int64_t)B * Tnew * N * D);
+    const T* kin = slot >= 0 ? reinterpret_cast<const T*>(io->k_in[slot]) : nullptr;
+    const T* vin = slot >= 0 ? reinterpret_cast<const T*>(io->v_in[slot]) : nullptr;
+    const int64_t cstride = (int64_t)Tnew * N * D;
+    T* kcur = kout + (int64_t)(Tnew - 1) * N * D;
+    T* vcur = vout + (int64_t)(Tnew - 1) * N * D;
+    T* fq = buf(P * 3 * c);
+    T* pe = buf((int64_t)HW * c);
+    T* kp = buf((int64_t)HW * c);
+    T* kpos = buf((int64_t)N * D);
+    T* xs = buf(P * NT * c);
+    T* kvd = buf(P * NT * 2 * c);
+    // LN(x) -> [SAB k | SAB v | FHR qkv] -> depthwise; k and v go straight into the new caches'
+    // current frame in the dilated token layout
+    if (can_fuse(c, F_DWONLY, 5 * c, 0)) {
+      FusedDst dk{kcur, 0, 0, 0, c, c, ws, cstride}, dv{vcur, 0, 0, c, 2 * c, c, ws, cstride};
+      fused(F_DWONLY, bw.a_in, bw.chm_dw6, x, c, 0, c, B, H, Wd, 5 * c, nullptr, nullptr, nullptr,
+            {dk, dv, dst_map(fq, 3 * c, 0, 2 * c, 5 * c)});
+    } else {
+      T* t5 = buf(P * 5 * c);
+      gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t5, 5 * c, 0);
+      dw(bw.sab_qk_dw, t5, 5 * c, 0, kcur, 0, 0, B, H, Wd, DW_PLAIN, ws, cstride);
+      dw(bw.sab_v_dw, t5, 5 * c, c, vcur, 0, 0, B, H, Wd, DW_PLAIN, ws, cstride);
+      dw(bw.fhr_dw, t5, 5 * c, 2 * c, fq, 3 * c, 0, B, H, Wd, DW_PLAIN);
+    }
+    // positional term dw(W_k pos) in token layout (one image, shared by the batch), then
+    // k += it and L2-normalise each token (F.normalize over ws*ws*c, turtle_arch.py:494-495)
+    if (!dry()) {
+      T0PeArgs pa{pe, H, Wd, c};
+      tag("t0_pe H=%d W=%d C=%d", H, Wd, c);
+      launch(TURTLE_K_OTHER, ES * (double)HW * c, 0, [&] { launch_t0_pe<T>(pa, st); });
+    }
+    gemm(bw.t0_kpw, src1(pe, c, 0, c), HW, HW, Wd, kp, c, 0);
+    dw(bw.t0_kdw, kp, c, 0, kpos, 0, 0, 1, H, Wd, DW_PLAIN, ws, (int64_t)N * D);
+    if (!dry()) {
+      T0KnormArgs ka{kcur, cstride, kpos, B, N, (int)D};
+      tag("t0_knorm B=%d N=%d D=%d", B, N, (int)D);
+      launch(TURTLE_K_OTHER, ES * ((double)B * N * D * 3 + (double)N * D), 0, [&] { launch_t0_knorm<T>(ka, st); });
+      if (Tnew > 1) {   // keep the last Tnew-1 cached frames (reference: cat then [-ntc:])
+        const int keep = Tnew - 1, first = Tin - keep;
+        tag("sab_cache_shift keep=%d N=%d", keep, N);
+        launch(TURTLE_K_OTHER, 4.0 * ES * B * keep * (double)N * D, 0, [&] {
+          HIPCHK(hipMemcpy2DAsync(kout, (size_t)cstride * ES, kin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
+                                  (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
+          HIPCHK(hipMemcpy2DAsync(vout, (size_t)cstride * ES, vin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
+                                  (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
+        });
+      }
+      // out = v of every frame, back to pixel-major frames (b, t) -> image b*NT + t
+      T0UntokArgs ua{};
+      for (int t = 0; t < NT; ++t) {
+        ua.v[t] = t < Tin ? vin + (int64_t)t * N * D : vcur;
+        ua.v_bstride[t] = t < Tin ? (int64_t)Tin * N * D : cstride;
+      }
+      ua.out = xs; ua.B = B; ua.T = NT; ua.H = H; ua.W = Wd; ua.C = c; ua.ws = ws;
+      tag("t0_untok BT=%d H=%d W=%d C=%d", B * NT, H, Wd, c);
+      launch(TURTLE_K_OTHER, 2.0 * ES * P * NT * c, 0, [&] { launch_t0_untok<T>(ua, st); });
+    }
+    chm_tail(b, bw, x, xs, kvd, fq, NT, H, Wd);
+  }
+
   // Causal History Model: SAB + kv conv on the aligned frames + FHR (turtle_t1_arch.py:612-662)
   void chm(const Blk& b, const BlockW& bw, T* x, int H, int Wd) {
+    if (h->arch.cfg.variant == 1) { chm_t0(b, bw, x, H, Wd); return; }
     const int c = b.dim, HW = H * Wd, ch = c / b.heads, ws = b.ws, slot = b.cache_slot;
     const int64_t P = (int64_t)B * HW;
     const int th = H / ws, tw = Wd / ws, N = th * tw, d2 = 2 * c, D = ws * ws * c;
@@ -913,6 +1009,13 @@ struct Runner {
                else launch_sab_gather<T>(ga, st);
              });
     }
+    chm_tail(b, bw, x, xs, kvd, fq, NT, H, Wd);
+  }
+
+  // kv conv on the aligned frames + FHR(x, k_hist, v_hist) (turtle_t1_arch.py:640-662)
+  void chm_tail(const Blk& b, const BlockW& bw, T* x, T* xs, T* kvd, T* fq, int NT, int H, int Wd) {
+    const int c = b.dim, HW = H * Wd, ch = c / b.heads;
+    const int64_t P = (int64_t)B * HW;
     // kv = (W_kv W_po) xs over the B*T aligned frames, then dw3x3 per frame
     if (can_fuse(c, F_DWONLY, 2 * c, 0)) {
       fused(F_DWONLY, bw.kv, bw.kv_dw, xs, c, 0, c, B * NT, H, Wd, 2 * c, nullptr, nullptr, nullptr,
@@ -1201,7 +1304,8 @@ int turtle_cache_layout(const TurtleHandle* h, int B, int H, int W, const int t_
           const int frames = std::min(t_in[s] + 1, b.ntc);
           kind[s] = 2;
           ks[0] = vs[0] = B; ks[1] = vs[1] = frames; ks[2] = vs[2] = 1; ks[3] = vs[3] = N;
-          ks[4] = 2 * c; vs[4] = (int64_t)b.ws * b.ws * c;
+          vs[4] = (int64_t)b.ws * b.ws * c;
+          ks[4] = h->arch.cfg.variant == 1 ? vs[4] : 2 * c;   // t0 caches dilated k tokens (turtle_arch.py:480-491)
         }
       }
   });

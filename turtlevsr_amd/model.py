@@ -49,10 +49,14 @@ class _Handle:
 
 
 class TurtleHIP(TurtleParams):
-    """Turtle_t1 (``sr=False``) / TurtleSuper_t1 (``sr=True``) on MI355X."""
+    """Turtle_t1 (``sr=False``) / TurtleSuper_t1 (``sr=True``) / t0 Turtle (``t0=True``) on MI355X."""
 
-    def __init__(self, opt: dict, sr: bool = False, dtype: str = "fp32"):
+    def __init__(self, opt: dict, sr: bool = False, dtype: str = "fp32", t0: Optional[bool] = None):
         arch = resolve(opt)
+        if t0 is not None:          # the plug-in module decides (turtle_arch vs turtle_t1_arch)
+            arch.t0 = bool(t0)
+        if arch.t0 and sr:
+            raise ValueError("the super-resolution network is t1 only (turtlesuper_t1_arch.py)")
         super().__init__(arch)
         self.sr = sr
         self.padder_size = 32
