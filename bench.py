@@ -12,8 +12,10 @@ an independent clip replica ("replicas only", scaling weak); value = frames of a
 rank time.
 
 The JSON line also carries
-* roofline: the dominant kernel launch shape (most GPU time in the timed region, measured with
-  HIP events on the forward's stream) priced with its algorithmic bytes or FLOPs per launch;
+* roofline: the dominant kernel launch shape (most GPU time over the warmup frames, where every
+  launch is event-timed) priced with its algorithmic bytes or FLOPs per launch over its average
+  duration, timed by HIP events (on the forward's stream) around exactly that shape's launches
+  inside the timed region, so the events do not inflate the frame time;
   traffic = its PMC HBM bytes per launch from the committed profiles/r01_pmc_traffic.json;
 * cpu_baseline: the CPU oracle (oracle/turtle_ref.py, fp32 PyTorch CPU restatement of the
   reference) on a bounded 256x256 steady-state sample, scaled to 1080p frames/s by the
@@ -116,15 +118,16 @@ def pmc_traffic():
         return json.load(f).get("per_tag", {})
 
 
-def roofline(prof, dump, steps, dtype):
-    """Roofline of the dominant kernel: the launch shape with the most GPU time in the timed region,
-    its algorithmic bytes (or FLOPs) per launch over its average launch duration (HIP events on the
-    forward's stream); traffic = PMC HBM bytes per launch of that shape, when profiled."""
-    groups = launch_groups(dump)
-    if not groups:
+def roofline(wprof, wgroups, nwarm, tgroups, steps, dtype):
+    """Roofline of the dominant kernel: the launch shape with the most GPU time in the profiled
+    warmup frames; achieved = its algorithmic bytes (or FLOPs) per launch over its average launch
+    duration, from the HIP events bracketing exactly its launches inside the timed region (on the
+    forward's stream); traffic = PMC HBM bytes per launch of that shape, when profiled. The
+    whole-frame class / shape breakdown comes from the warmup frames (every launch timed)."""
+    if not wgroups or not tgroups:
         return None
-    tag = max(groups, key=lambda k: groups[k]["ms"])
-    g = groups[tag]
+    tag = max(tgroups, key=lambda k: tgroups[k]["ms"])
+    g = tgroups[tag]
     n = max(g["launches"], 1)
     avg_s = g["ms"] * 1e-3 / n
     bpl, fpl = g["bytes"] / n, g["flops"] / n
@@ -141,9 +144,11 @@ def roofline(prof, dump, steps, dtype):
                 launches_per_step=g["launches"] / steps, avg_launch_us=round(avg_s * 1e6, 2),
                 algorithmic_bytes_per_launch=round(bpl), algorithmic_flops_per_launch=round(fpl),
                 mfma_tflops=round(fpl / avg_s / 1e12, 2), hbm_gbs=round(bpl / avg_s / 1e9, 1),
-                class_ms_per_step={k: round(v["ms"] / steps, 3) for k, v in prof.items()},
-                top_launch_shapes_ms_per_step={k: round(groups[k]["ms"] / steps, 3)
-                                               for k in sorted(groups, key=lambda k: -groups[k]["ms"])[:6]})
+                timing="HIP events around this shape's launches only, inside the timed region",
+                breakdown_from=f"{nwarm} warmup frames with every launch event-timed",
+                class_ms_per_step={k: round(v["ms"] / nwarm, 3) for k, v in wprof.items()},
+                top_launch_shapes_ms_per_step={k: round(wgroups[k]["ms"] / nwarm, 3)
+                                               for k in sorted(wgroups, key=lambda k: -wgroups[k]["ms"])[:6]})
     return roof
 
 
@@ -156,6 +161,7 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-psnr", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--profile-all", action="store_true", help="print every kernel class's time")
     args = ap.parse_args()
 
@@ -183,16 +189,31 @@ def main():
     with torch.no_grad():
         for _ in range(3):           # prime the history caches (steady state: full caches)
             step()
-        for _ in range(args.warmup):
+        # warmup, profiled: every launch bracketed by HIP events -> whole-frame breakdown by kernel
+        # class / launch shape, and the dominant launch shape (most GPU time)
+        wdump = os.path.join("/tmp", f"turtle_bench_warm_{os.getpid()}.tsv")
+        if os.path.exists(wdump):
+            os.remove(wdump)
+        nwarm = max(args.warmup, 1)
+        if not args.no_roofline:
+            os.environ["TURTLE_PROF_DUMP"] = wdump
+            model.profile_begin("all")
+        for _ in range(nwarm):
             step()
         torch.cuda.synchronize()
+        wprof = model.profile_end() if not args.no_roofline else {}
+        wgroups = launch_groups(wdump)
+        dom = max(wgroups, key=lambda k: wgroups[k]["ms"]) if wgroups else None
         if world > 1:
             dist.barrier()
+        # timed region: HIP events only around the dominant shape's launches (per-launch events
+        # on all ~400 launches of a frame would add ~3 ms of stream bubbles to the frame time)
         dump = os.path.join("/tmp", f"turtle_bench_launches_{os.getpid()}.tsv")
         if os.path.exists(dump):
             os.remove(dump)
-        os.environ["TURTLE_PROF_DUMP"] = dump        # per-launch records of the timed region
-        model.profile_begin("all")
+        if dom is not None:
+            os.environ["TURTLE_PROF_DUMP"] = dump
+            model.profile_begin("all", tag=dom)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
@@ -201,14 +222,16 @@ def main():
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        prof = model.profile_end()
+        if dom is not None:
+            model.profile_end()
         os.environ.pop("TURTLE_PROF_DUMP", None)
     rep = replica_throughput(elapsed, args.steps, dev)
     tmax, fps = rep.t_max, rep.value
 
-    roof = roofline(prof, dump, args.steps, args.dtype)
-    if os.path.exists(dump):
-        os.remove(dump)
+    roof = roofline(wprof, wgroups, nwarm, launch_groups(dump), args.steps, args.dtype)
+    for f in (dump, wdump):
+        if os.path.exists(f):
+            os.remove(f)
 
     psnr = None
     if not args.no_psnr and rank == 0 and args.dtype == "bf16":

@@ -119,6 +119,10 @@ int turtle_forward(TurtleHandle* h, const float* inp, int B, int H, int W, float
 #define TURTLE_K_ALL 99
 int turtle_profile_begin(TurtleHandle* h, int kernel_class);
 int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
+/* Restrict profiling to launches whose shape tag (the TURTLE_PROF_DUMP tag column) equals `tag`
+ * (NULL or "" profiles every launch of the class again): keeps the event overhead of a timed
+ * region to the one launch shape being measured. */
+int turtle_profile_filter(TurtleHandle* h, const char* tag);
 
 /* Kernel-selection switches (performance A/B only; every setting computes the same function).
  *   "fuse"        1 (default): block-level fused pointwise->depthwise->pointwise kernels where

@@ -54,6 +54,7 @@ def lib():
                                  C.POINTER(vp), C.POINTER(vp), vp, C.c_size_t, vp]
     L.turtle_profile_begin.argtypes = [vp, C.c_int]
     L.turtle_profile_end.argtypes = [vp, C.POINTER(C.c_double)]
+    L.turtle_profile_filter.argtypes = [vp, C.c_char_p]
     L.turtle_set_option.argtypes = [vp, C.c_char_p, C.c_int]
     L.turtle_last_error.restype = C.c_char_p
     _lib = L
@@ -62,7 +63,8 @@ def lib():
 
 EXPORTED = ["turtle_create", "turtle_destroy", "turtle_num_weights", "turtle_weight_info", "turtle_set_weight",
             "turtle_load_weights", "turtle_cache_layout", "turtle_workspace_size", "turtle_forward",
-            "turtle_profile_begin", "turtle_profile_end", "turtle_set_option", "turtle_last_error"]
+            "turtle_profile_begin", "turtle_profile_end", "turtle_profile_filter", "turtle_set_option",
+            "turtle_last_error"]
 K_CLASSES = ["gemm", "dwconv", "chan_attn", "sab_score", "sab_av", "sab_window", "other", "fused"]
 K_ALL = 99
 

@@ -280,6 +280,7 @@ struct TurtleHandle {
   int prof_cls = -1;
   std::vector<ProfRec> prof;
   std::string prof_tag;                               // shape note of the next launch (per-launch dump)
+  std::string prof_filter;                            // non-empty: profile only launches with this tag
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::map<std::string, std::vector<float>> staged;
@@ -566,7 +567,8 @@ struct Runner {
   template <typename F>
   void launch(int cls, double bytes, double flops, F&& f) {
     if (dry()) return;
-    const bool p = h->prof_cls == TURTLE_K_ALL || h->prof_cls == cls;
+    const bool p = (h->prof_cls == TURTLE_K_ALL || h->prof_cls == cls) &&
+                   (h->prof_filter.empty() || h->prof_filter == h->prof_tag);
     if (!p) { f(); h->prof_tag.clear(); return; }
     ProfRec r{cls, event(), event(), bytes, flops, std::move(h->prof_tag)};
     h->prof_tag.clear();
@@ -1200,6 +1202,13 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]) {
     h->prof.clear();
     h->ev_used = 0;
     h->prof_cls = -1;
+  });
+}
+
+int turtle_profile_filter(TurtleHandle* h, const char* tag) {
+  return guard([&] {
+    if (!h) TFAIL(TURTLE_EINVAL, "null handle");
+    h->prof_filter = tag ? tag : "";
   });
 }
 

@@ -189,12 +189,15 @@ class TurtleHIP(TurtleParams):
         _lib.check(_lib.lib().turtle_set_option(self._handle.h, name.encode(), int(value)))
         return self
 
-    def profile_begin(self, kernel_class: str = "all"):
-        """Bracket every launch of `kernel_class` (see _lib.K_CLASSES, or 'all') with HIP events."""
+    def profile_begin(self, kernel_class: str = "all", tag: Optional[str] = None):
+        """Bracket every launch of `kernel_class` (see _lib.K_CLASSES, or 'all') with HIP events;
+        with `tag`, only the launches of that shape (the per-launch dump's tag column)."""
         cls = _lib.K_ALL if kernel_class == "all" else _lib.K_CLASSES.index(kernel_class)
         if self._handle is None or self._sig is None:
             self.refresh_weights()
-        _lib.check(_lib.lib().turtle_profile_begin(self._handle.h, cls))
+        L = _lib.lib()
+        _lib.check(L.turtle_profile_filter(self._handle.h, tag.encode() if tag else None))
+        _lib.check(L.turtle_profile_begin(self._handle.h, cls))
 
     def profile_end(self) -> dict:
         """Per class: summed kernel ms, launches, algorithmic bytes and FLOPs."""
