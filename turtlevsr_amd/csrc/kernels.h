@@ -227,4 +227,13 @@ struct T0UntokArgs {               // out[b*T + t] = inverse dilated regroup of 
 };
 template <typename T> void launch_t0_untok(const T0UntokArgs& a, hipStream_t st);
 
+// hipBLASLt plain-GEMM path (blas.cpp): D = X W^T (+ bias) (+ C), bf16, fp32 accumulation
+struct BlasCtx;
+BlasCtx* blas_create();
+void blas_destroy(BlasCtx* c);
+bool blas_ready(BlasCtx* c, int64_t M, int N, int K, int64_t ldx, int64_t ldw, int64_t ldc, int64_t ldd, bool has_c,
+                bool has_bias);
+bool blas_gemm_bf16(BlasCtx* c, int64_t M, int N, int K, const void* X, int64_t ldx, const void* W, int64_t ldw,
+                    const float* bias, const void* C, int64_t ldc, void* D, int64_t ldd, hipStream_t st);
+
 }  // namespace turtle

@@ -297,6 +297,8 @@ struct TurtleHandle {
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
+  bool blaslt = getenv("TURTLE_NO_BLASLT") == nullptr; // hipBLASLt for the plain projections it wins (blas.cpp)
+  BlasCtx* blas = nullptr;                            // created on the first bf16 forward
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
   const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
   const float* fptr(size_t off) const { return reinterpret_cast<const float*>(ptr(off)); }
@@ -612,9 +614,42 @@ struct Runner {
     const double Ka = conv3 ? cin : a.Ktot;
     const double nset = wstride ? (double)(M / HW) / wdiv : 1.0;
     const double bytes = ES * ((double)M * Ka + nset * g.N * a.Ktot + (double)M * g.N * (res ? 2 : 1));
-    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d", (long long)M, g.N, a.Ktot, conv3, g.ln,
-        res != nullptr, store, a.n);
-    launch(TURTLE_K_GEMM, bytes, 2.0 * M * g.N * a.Ktot, [&] { launch_gemm<T>(g, st); });
+    const bool lt = use_blas(g);
+    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
+        res != nullptr, store, a.n, lt ? " lt" : "");
+    launch(TURTLE_K_GEMM, bytes, 2.0 * M * g.N * a.Ktot, [&] {
+      if (lt) run_blas(g);
+      else launch_gemm<T>(g, st);
+    });
+  }
+  // plain bf16 projections where hipBLASLt beats the in-tree kernels (measured, blas.cpp): no LN
+  // prologue, activation, scale, 3x3 or multi-source operand; K >= 512, or <= 140k pixels x >= 256
+  // output channels. Per-image weight sets (W_eff) run one call per image.
+  bool use_blas(const GemmArgs& g) {
+    if (ES != 2 || !h->blaslt || g.conv3 || g.ln || g.gelu || g.scale || g.store_mode != STORE_NHWC || g.a.n != 1)
+      return false;
+    const SrcDesc& s = g.a.s[0];
+    if (s.img_mul != 1 || s.img_add != 0 || s.K != g.a.Ktot) return false;
+    if (g.wstride && (g.HW <= 0 || g.M % g.HW || g.wstride % 8)) return false;
+    const int64_t Mi = g.wstride ? g.HW : g.M;
+    const int K = g.a.Ktot;
+    if (!(K >= 512 || (Mi <= 140000 && g.N >= 256))) return false;
+    if (s.ld % 8 || s.off % 8 || g.ldo % 8 || g.offo % 8 || g.ldw % 8 || K % 8 || g.N % 8) return false;
+    if (g.res && (g.ldr % 8 || g.offr % 8)) return false;
+    if (!h->blas) h->blas = blas_create();
+    return blas_ready(h->blas, Mi, g.N, K, s.ld, g.ldw, g.res ? g.ldr : 0, g.ldo, g.res != nullptr, g.bias != nullptr);
+  }
+  void run_blas(const GemmArgs& g) {
+    const SrcDesc& s = g.a.s[0];
+    const int64_t nimg = g.wstride ? g.M / g.HW : 1, Mi = g.wstride ? g.HW : g.M;
+    for (int64_t i = 0; i < nimg; ++i) {
+      const T* X = reinterpret_cast<const T*>(s.base) + s.off + i * Mi * s.ld;
+      const T* Wp = reinterpret_cast<const T*>(g.w) + (g.wstride ? (i / g.wdiv) * g.wstride : 0);
+      const T* Cp = g.res ? reinterpret_cast<const T*>(g.res) + g.offr + i * Mi * g.ldr : nullptr;
+      T* D = reinterpret_cast<T*>(g.out) + g.offo + i * Mi * g.ldo;
+      if (!blas_gemm_bf16(h->blas, Mi, g.N, g.a.Ktot, X, s.ld, Wp, g.ldw, g.bias, Cp, g.ldr, D, g.ldo, st))
+        TFAIL(TURTLE_EHIP, "hipBLASLt matmul failed");
+    }
   }
   void dw(const DwW& w, const void* in, int64_t ldi, int offi, void* out, int64_t ldo, int offo,
           int nimg, int H, int Wd, int mode, int tok_ws = 0, int64_t tok_stride = 0) {
@@ -1219,6 +1254,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     if (n == "fuse") h->fuse = value != 0;
     else if (n == "panel_gemm") h->panel = value != 0;
     else if (n == "dw_rows") h->dw_rows = value != 0;
+    else if (n == "blaslt") h->blaslt = value != 0;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
     else if (n == "pwdw") h->pwdw = value != 0;
@@ -1248,6 +1284,7 @@ void turtle_destroy(TurtleHandle* h) {
   if (!h) return;
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->dev) (void)hipFree(h->dev);
+  blas_destroy(h->blas);
   delete h;
 }
 
