@@ -26,6 +26,7 @@ The JSON line also carries
 from __future__ import annotations
 
 import argparse
+import shutil
 import json
 import os
 import sys
@@ -229,6 +230,9 @@ def main():
     tmax, fps = rep.t_max, rep.value
 
     roof = roofline(wprof, wgroups, nwarm, launch_groups(dump), args.steps, args.dtype)
+    keep = os.environ.get("TURTLE_BENCH_DUMP")     # keep the warmup frames' per-launch records
+    if keep and os.path.exists(wdump):
+        shutil.copyfile(wdump, keep)
     for f in (dump, wdump):
         if os.path.exists(f):
             os.remove(f)

@@ -10,8 +10,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/t.log
 [ $rc -ne 0 ] && exit $rc
 rm -f gpurun_out/launches.tsv
-TURTLE_PROF_DUMP=gpurun_out/launches.tsv timeout -k 10 200 python -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-psnr > gpurun_out/b2.log 2>&1 || exit $?
-timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b.log 2>&1
+TURTLE_BENCH_DUMP=gpurun_out/launches.tsv timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b.log 2>&1
 rc=$?; tail -1 gpurun_out/b.log; [ $rc -ne 0 ] && exit $rc
 # (optional) kernel-trace summary of a short run: GPU_CHECK_PROF=1
 if [ -n "$GPU_CHECK_PROF" ]; then

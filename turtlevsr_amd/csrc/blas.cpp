@@ -111,4 +111,60 @@ bool blas_gemm_bf16(BlasCtx* c, int64_t M, int N, int K, const void* X, int64_t 
                          c->ws_bytes, st) == HIPBLAS_STATUS_SUCCESS;
 }
 
+// LayerNorm prologue of the vendor path: the in-tree GEMMs fold LayerNorm into their operand
+// staging; hipBLASLt cannot, so LN-folded latent projections first write the normalised rows
+// xn = (x - mu) * rstd (BiasFree: x * rstd, turtle_t1_arch.py:68-80) in storage precision and run
+// D = W' xn + (W b_ln + bias) (W' = W diag(g_ln), packed by pack_gemm). One wave per pixel row,
+// fp32 statistics (biased variance, eps 1e-5: turtle_t1_arch.py:83-112).
+template <typename T>
+__global__ __launch_bounds__(256) void ln_rows_kernel(LnRowsArgs a) {
+  constexpr int VEC = Vec<T>::N;
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= a.M) return;
+  const T* x = reinterpret_cast<const T*>(a.x) + r * a.ldx + a.offx;
+  T* o = reinterpret_cast<T*>(a.out) + r * a.ldo;
+  constexpr int MAXV = 4;                               // K <= 64 lanes * VEC * MAXV
+  float v[MAXV][VEC];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int k = (j * 64 + lane) * VEC;
+    if (k < a.K) {
+      Vec<T> q; q.load(x + k);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) { v[j][i] = q.v[i]; s += q.v[i]; }
+    }
+  }
+  const float mu = wave_sum(s) / a.K;
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int k = (j * 64 + lane) * VEC;
+    if (k < a.K) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) { const float d = v[j][i] - mu; ss += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / a.K + 1e-5f);
+  const float sub = a.centred ? mu : 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXV; ++j) {
+    const int k = (j * 64 + lane) * VEC;
+    if (k < a.K) {
+      Vec<T> q;
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) q.v[i] = (v[j][i] - sub) * rstd;
+      q.store(o + k);
+    }
+  }
+}
+
+template <typename T>
+void launch_ln_rows(const LnRowsArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(ln_rows_kernel<T>, dim3((unsigned)((a.M + 3) / 4)), dim3(256), 0, st, a);
+}
+template void launch_ln_rows<float>(const LnRowsArgs&, hipStream_t);
+template void launch_ln_rows<bf16>(const LnRowsArgs&, hipStream_t);
+
 }  // namespace turtle

@@ -44,7 +44,9 @@ template <typename T, int MODE, int CM>
 struct F3 {
   static constexpr int ES = sizeof(T);
   static constexpr int SL = MODE == F_GATE ? 8 : 16;                // hidden channels per slice
-  static constexpr int HP = MODE == F_GATE ? 160 : (MODE == F_GELU ? 128 : 0);   // hidden per pass
+  // hidden per pass: at C = 64 a 64-wide pass keeps LDS (and the W2 fragments in flight) small
+  // enough for 3 blocks per CU
+  static constexpr int HP = MODE == F_GATE ? (CM <= 64 ? 64 : 160) : (MODE == F_GELU ? (CM <= 64 ? 64 : 128) : 0);
   static constexpr int XROW = CM * ES + 16;                        // sX row bytes
   static constexpr int HROW = 16 * ES + 16;                        // wave strip row bytes
   static constexpr int GROW = HP * ES + 16;                        // sG row bytes
@@ -90,7 +92,7 @@ TURTLE_DEV void f_stamp(unsigned long long* buf, int& si) {
 }
 
 template <typename T, int MODE, int CM>
-__global__ __launch_bounds__(256, 2) void fused_kernel(FusedArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CM <= 64 && MODE != F_DWONLY ? 3 : 2))) void fused_kernel(FusedArgs a) {
   using F = F3<T, MODE, CM>;
   using FR = typename Frag<T>::type;
   constexpr int VEC = Vec<T>::N, ES = F::ES, KF = Frag<T>::K, SL = F::SL;

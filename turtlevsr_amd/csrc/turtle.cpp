@@ -200,7 +200,11 @@ static void build_arch(Arch& A) {
 // ------------------------------------------------------------------------------------------
 // packed weights
 // ------------------------------------------------------------------------------------------
-struct GemmW { size_t w = NONE, s = NONE, t = NONE, bias = NONE, scale = NONE; int N = 0, K = 0; bool ln = false; };
+struct GemmW {
+  size_t w = NONE, s = NONE, t = NONE, bias = NONE, scale = NONE;
+  size_t tb = NONE;   // LN GEMMs: W b_ln + bias (the vendor path's bias after an explicit LN prologue)
+  int N = 0, K = 0; bool ln = false;
+};
 struct DwW { size_t w = NONE, bias = NONE, w2 = NONE; int C = 0; };   // w2: bf16 tap pairs [5][C] (u32)
 struct BlockW {
   GemmW a_in, a_out, q2, k2, kv, f_in, f_out, t0_kpw;   // t0_kpw: W_k of the t0 aligner (pos term)
@@ -341,6 +345,11 @@ static GemmW pack_gemm(TurtleHandle* h, Packer& pk, std::vector<double> Wm, int 
     g.w = pk.stor(Wm);
   }
   if (!bias.empty()) g.bias = pk.f32(bias);
+  if (g.ln) {
+    std::vector<double> tb(N, 0.0);
+    for (int n = 0; n < N; ++n) tb[n] = (t.empty() ? 0.0 : t[n]) + (bias.empty() ? 0.0 : bias[n]);
+    g.tb = pk.f32(tb);
+  }
   return g;
 }
 
@@ -598,6 +607,15 @@ struct Runner {
             const void* res = nullptr, int64_t ldr = 0, int offr = 0, int gelu = 0,
             int store = STORE_NHWC, const void* wptr = nullptr, int64_t wstride = 0, int wdiv = 1,
             int N = -1, const float* bias = nullptr, int conv3 = 0, int cin = 0) {
+    // LN-folded projections with K >= 512 (latent level) may run as an explicit LayerNorm pass +
+    // hipBLASLt: their normalised rows need workspace (sized in the dry run as well)
+    // (the workspace test is shape-only, so sizing - which runs without packed weights - and every
+    // switch setting reserve the same bytes; <= 32 Mi elements keeps it to the latent level at 1080p)
+    const bool ln_ws = ES == 2 && a.n == 1 && !conv3 && !gelu && store == STORE_NHWC && a.Ktot >= 512 &&
+                       a.Ktot <= 64 * 8 * 4 && a.Ktot % 8 == 0 && M * a.Ktot <= ((int64_t)32 << 20);
+    T* xn = ln_ws ? buf(M * a.Ktot) : nullptr;
+    const bool ln_cand = ln_ws && h->blaslt && w.ln && w.scale == NONE && a.s[0].img_mul == 1 &&
+                         a.s[0].img_add == 0 && !wptr && !bias && w.tb != NONE;
     if (dry()) return;
     GemmArgs g{};
     g.a = a; g.M = M; g.N = N >= 0 ? N : w.N; g.HW = HW; g.Wimg = Wimg;
@@ -614,12 +632,23 @@ struct Runner {
     const double Ka = conv3 ? cin : a.Ktot;
     const double nset = wstride ? (double)(M / HW) / wdiv : 1.0;
     const double bytes = ES * ((double)M * Ka + nset * g.N * a.Ktot + (double)M * g.N * (res ? 2 : 1));
-    const bool lt = use_blas(g);
+    GemmArgs gl = g;   // vendor form of an LN GEMM: operand = normalised rows, bias = W b_ln + bias
+    if (ln_cand) {
+      gl.a = src1(xn, a.Ktot, 0, a.Ktot); gl.ln = 0; gl.ln_s = gl.ln_t = nullptr; gl.bias = h->fptr(w.tb);
+    }
+    const bool lt = ln_cand ? use_blas(gl) : use_blas(g);
     tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
         res != nullptr, store, a.n, lt ? " lt" : "");
-    launch(TURTLE_K_GEMM, bytes, 2.0 * M * g.N * a.Ktot, [&] {
-      if (lt) run_blas(g);
-      else launch_gemm<T>(g, st);
+    launch(TURTLE_K_GEMM, bytes + (ln_cand && lt ? 2.0 * ES * M * a.Ktot : 0.0), 2.0 * M * g.N * a.Ktot, [&] {
+      if (lt && ln_cand) {
+        LnRowsArgs la{a.s[0].base, a.s[0].ld, a.s[0].off, xn, a.Ktot, M, a.Ktot, h->arch.cfg.layernorm_biasfree ? 0 : 1};
+        launch_ln_rows<T>(la, st);
+        run_blas(gl);
+      } else if (lt) {
+        run_blas(g);
+      } else {
+        launch_gemm<T>(g, st);
+      }
     });
   }
   // plain bf16 projections where hipBLASLt beats the in-tree kernels (measured, blas.cpp): no LN
