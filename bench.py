@@ -62,15 +62,15 @@ def load_opt():
         return yaml.safe_load(f)
 
 
-def build_model(opt, dtype, dev):
-    m = TurtleHIP(opt, dtype=dtype)
+def build_model(opt, dtype, dev, sr=False):
+    m = TurtleHIP(opt, sr=sr, dtype=dtype)
     shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
     m.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(shapes, 0).items()})
     return m.to(dev).eval()
 
 
-def clip_frames(h, w, seed, dev, n=5):
-    clip = torch.from_numpy(synthetic_frames((1, n, 3, h, w), seed)).to(dev)
+def clip_frames(h, w, seed, dev, n=5, batch=1):
+    clip = torch.from_numpy(synthetic_frames((batch, n, 3, h, w), seed)).to(dev)
     return [torch.stack([clip[:, max(j - 1, 0)], clip[:, j]], dim=1).contiguous() for j in range(n)]
 
 
@@ -160,6 +160,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--res", default="1080p", choices=list(RES))
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--batch", type=int, default=1, help="clips per GPU restored together (B of [B,2,3,H,W])")
+    ap.add_argument("--sr", action="store_true", help="TurtleSuper_t1 4x SR: LR input = res/4, output at res")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-psnr", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events in the timed region")
@@ -176,8 +178,13 @@ def main():
     h, w = RES[args.res]
     opt = load_opt()
 
-    model = build_model(opt, args.dtype, dev)
-    frames = clip_frames(h, w, clip_seed(rank), dev)
+    model = build_model(opt, args.dtype, dev, args.sr)
+    if args.sr:
+        if h % 4 or w % 4:
+            raise SystemExit(f"--sr needs an output size divisible by 4, got {w}x{h}")
+        frames = clip_frames(h // 4, w // 4, clip_seed(rank), dev, batch=args.batch)
+    else:
+        frames = clip_frames(h, w, clip_seed(rank), dev, batch=args.batch)
     kc = vc = None
     j = 0
 
@@ -226,7 +233,7 @@ def main():
         if dom is not None:
             model.profile_end()
         os.environ.pop("TURTLE_PROF_DUMP", None)
-    rep = replica_throughput(elapsed, args.steps, dev)
+    rep = replica_throughput(elapsed, args.steps * args.batch, dev)
     tmax, fps = rep.t_max, rep.value
 
     roof = roofline(wprof, wgroups, nwarm, launch_groups(dump), args.steps, args.dtype)
@@ -239,7 +246,7 @@ def main():
 
     psnr = None
     if not args.no_psnr and rank == 0 and args.dtype == "bf16":
-        ref = build_model(opt, "fp32", dev)
+        ref = build_model(opt, "fp32", dev, args.sr)
         kr = vr = None
         kb = vb = None
         vals = []
@@ -262,8 +269,9 @@ def main():
                           f"{threads} threads), scaled to {args.res} by F_alg ratio {scale:.5f}")
 
     line = {
-        "metric": "restored frames/sec @1080p (1/2/4/8 GPU) + PSNR delta vs ref" if args.res == "1080p"
-        else f"restored frames/sec @{args.res}",
+        "metric": "restored frames/sec @1080p (1/2/4/8 GPU) + PSNR delta vs ref"
+        if args.res == "1080p" and not args.sr and args.batch == 1
+        else f"restored frames/sec @{args.res}" + (" (4x SR output)" if args.sr else "") + (f" B={args.batch}" if args.batch > 1 else ""),
         "value": round(fps, 3),
         "unit": "frames/s",
         "n_gpus": world,
@@ -275,8 +283,9 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic frames (uniform [0,1)), synthetic random-init GoPro weights",
-        "config": {"workload": f"Turtle_t1 GoPro deblur, causal 5-frame clip, {w}x{h}, B=1, caches full",
-                   "model": "Turtle_t1 (GoPro arch, 59.08M params)", "global_batch": world, "seq_len": 5,
+        "config": {"workload": (f"TurtleSuper_t1 GoPro-arch 4x SR, {w // 4}x{h // 4} -> {w}x{h}" if args.sr
+                                else f"Turtle_t1 GoPro deblur, {w}x{h}") + f", causal 5-frame clip, B={args.batch}, caches full",
+                   "model": "Turtle_t1 (GoPro arch, 59.08M params)", "global_batch": world * args.batch, "seq_len": 5,
                    "parallelism": f"replicas x{world}"},
         "roofline": roof,
         "cpu_baseline": cpu,

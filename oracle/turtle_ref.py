@@ -353,7 +353,7 @@ def _up(sd, name, x):     # Upsample 146-154: 3x3 c->2c, PixelShuffle(2)
 def pad_to(x: Tensor, mult: int = PAD_MULT) -> Tensor:
     """check_image_size 1134-1139: zero-pad right/bottom to a multiple of 32."""
     h, w = x.shape[-2:]
-    return F.pad(x, (0, (mult - h % mult) % mult, 0, (mult - w % mult) % mult))
+    return F.pad(x, (0, (mult - w % mult) % mult, 0, (mult - h % mult) % mult))   # (w, h) order: 1138
 
 
 @torch.no_grad()

@@ -138,3 +138,17 @@ def test_clip(name):
                 check_summary(g, key, t, rtol=1e-3, atol=5e-5)
                 if key in g:
                     close(t, g[key], atol=5e-5, rtol=1e-3)
+
+
+def test_pad_to_non_square_ragged():
+    """check_image_size (turtle_t1_arch.py:1134-1139) pads H and W each to a multiple of 32 with
+    zeros at the bottom/right: 540x960 -> 544x960 and 36x70 -> 64x96 (unequal H/W pads)."""
+    x = torch.rand(1, 2, 3, 540, 960)
+    y = R.pad_to(x)
+    assert y.shape[-2:] == (544, 960)
+    assert torch.equal(y[..., :540, :], x) and float(y[..., 540:, :].abs().max()) == 0.0
+    x = torch.rand(1, 3, 36, 70)
+    y = R.pad_to(x)
+    assert y.shape[-2:] == (64, 96)
+    assert torch.equal(y[..., :36, :70], x)
+    assert float(y[..., 36:, :].abs().max()) == 0.0 and float(y[..., :, 70:].abs().max()) == 0.0
