@@ -40,6 +40,7 @@ import yaml
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
+from turtlevsr_amd.graph import GraphedTurtle  # noqa: E402
 from turtlevsr_amd.model import TurtleHIP  # noqa: E402
 from turtlevsr_amd.replicas import clip_seed, replica_throughput  # noqa: E402
 from turtlevsr_amd.synthetic import synthetic_frames, synthetic_state_dict  # noqa: E402
@@ -162,11 +163,14 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--batch", type=int, default=1, help="clips per GPU restored together (B of [B,2,3,H,W])")
     ap.add_argument("--sr", action="store_true", help="TurtleSuper_t1 4x SR: LR input = res/4, output at res")
+    ap.add_argument("--graph", action="store_true", help="steady-state frames replayed as captured HIP graphs (turtlevsr_amd/graph.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-psnr", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--profile-all", action="store_true", help="print every kernel class's time")
     args = ap.parse_args()
+    if args.graph:
+        args.no_roofline = True      # per-launch profiling events cannot live inside a captured graph
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -188,9 +192,14 @@ def main():
     kc = vc = None
     j = 0
 
+    runner = GraphedTurtle(model, *frames[0].shape[:1], *frames[0].shape[-2:]) if args.graph else None
+
     def step():
         nonlocal kc, vc, j
-        out, kc, vc = model(frames[j % len(frames)], kc, vc)
+        if runner is not None:
+            out, kc, vc = runner(frames[j % len(frames)])
+        else:
+            out, kc, vc = model(frames[j % len(frames)], kc, vc)
         j += 1
         return out
 
@@ -286,7 +295,8 @@ def main():
         "config": {"workload": (f"TurtleSuper_t1 GoPro-arch 4x SR, {w // 4}x{h // 4} -> {w}x{h}" if args.sr
                                 else f"Turtle_t1 GoPro deblur, {w}x{h}") + f", causal 5-frame clip, B={args.batch}, caches full",
                    "model": "Turtle_t1 (GoPro arch, 59.08M params)", "global_batch": world * args.batch, "seq_len": 5,
-                   "parallelism": f"replicas x{world}"},
+                   "parallelism": f"replicas x{world}",
+                   "execution": "HIP graph replay (2 captured graphs, ping-pong caches)" if args.graph else "eager launches"},
         "roofline": roof,
         "cpu_baseline": cpu,
         "psnr_bf16_vs_fp32_db": psnr,

@@ -97,3 +97,17 @@ def test_t0_variant_layout_and_plugin():
     m0, m1 = turtle_arch.make_model(o), turtle_t1_arch.make_model(o)
     assert m0.arch.t0 and not m1.arch.t0          # the module decides, as in the reference
     assert list(m0.state_dict()) == list(m1.state_dict())
+
+
+def test_graphed_runner_refuses_cpu_and_foreign_modules():
+    """GraphedTurtle is a ROCm-only serving wrapper: no CPU path, TurtleHIP modules only."""
+    import torch
+    from turtlevsr_amd.graph import GraphedTurtle
+    from turtlevsr_amd.model import TurtleHIP
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "options",
+                           "Turtle_Deblur_Gopro.yml")) as f:
+        opt = yaml.safe_load(f)
+    with pytest.raises(RuntimeError):
+        GraphedTurtle(TurtleHIP(opt), 1, 64, 64)
+    with pytest.raises(TypeError):
+        GraphedTurtle(torch.nn.Linear(2, 2), 1, 64, 64)

@@ -115,3 +115,33 @@ def test_unequal_pad_fp32_vs_oracle(name, h, w):
         assert o.shape == r.shape == (1, 3, h, w)
         err = float((o - r).abs().max())
         assert err <= 2e-4, (j, err)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_graphed_frame_loop_matches_eager(dtype):
+    """GraphedTurtle (two captured HIP graphs, ping-pong caches) restores the same frames as the
+    eager drop-in forward: GoPro widths, 256x256, 7 frames (graphs from frame 3 on, both
+    directions replayed twice), outputs and the final history."""
+    from turtlevsr_amd.graph import GraphedTurtle
+    from turtlevsr_amd.synthetic import synthetic_frames
+    _, meta = load("clip_gopro_64")
+    clip = torch.from_numpy(synthetic_frames((1, 7, 3, 256, 256), 23)).cuda()
+    m = _model(meta["opt"], meta["seed"], False, dtype)
+    runner = GraphedTurtle(m, 1, 256, 256)
+    kc = vc = None
+    with torch.no_grad():
+        for j in range(clip.shape[1]):
+            inp = torch.stack([clip[:, max(j - 1, 0)], clip[:, j]], dim=1)
+            ref, kc, vc = m(inp, kc, vc)
+            out, kg, vg = runner(inp)
+            if dtype == "fp32":
+                err = float((out - ref).abs().max())
+                assert err <= 1e-5, (j, err)
+            else:   # the bf16 path is not bitwise run-to-run (hipBLASLt stream-K GEMMs): 50 dB gate
+                p = psnr(out.cpu().numpy(), ref.cpu().numpy())
+                assert p >= 50.0, (j, p)
+    assert len(runner.graphs) == 2 and runner.frame == 4
+    for a, b in zip(kg + vg, kc + vc):
+        if b is not None:
+            d = float((a.float() - b.float()).abs().mean())
+            assert d <= (1e-6 if dtype == "fp32" else 3e-2 * float(b.float().abs().mean()) + 1e-6), d

@@ -1,0 +1,140 @@
+"""Steady-state causal frame loop replayed as HIP graphs (serving mode).
+
+The reference restores a clip frame by frame, each call feeding the previous call's caches back
+(video_restoration_model.py:85-92; inference.py:276-308). Once every cache slot is full
+(frame index >= num_frames_tocache) the cache shapes stop changing, so the whole per-frame launch
+sequence of `turtle_forward` (~450 kernels at GoPro widths) is the same every frame except for which
+buffers hold the history. `GraphedTurtle` captures it twice with ping-pong cache sets:
+
+    graph 0: caches A -> caches B        graph 1: caches B -> caches A
+
+and replays them alternately, so a frame costs one `hipGraphLaunch` and no host work. Frames before
+the caches fill run through the eager module (`TurtleHIP.forward`) and their caches seed set A.
+
+Difference from the drop-in forward: the returned caches are the runner's own buffers and are
+overwritten two frames later (the eager forward returns fresh, caller-owned tensors, SURVEY.md
+§8(b) "Ownership"). Use the eager module where caches are moved or kept (tiled inference).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional
+
+import torch
+
+from . import _lib
+from .model import TurtleHIP
+
+
+class GraphedTurtle:
+    def __init__(self, model: TurtleHIP, B: int, H: int, W: int):
+        if not isinstance(model, TurtleHIP):
+            raise TypeError("GraphedTurtle wraps a TurtleHIP module")
+        self.m, self.B, self.H, self.W = model, B, H, W
+        self.dev = next(model.parameters()).device
+        if self.dev.type != "cuda":
+            raise RuntimeError("GraphedTurtle needs the module on a ROCm device")
+        self.kc: Optional[list] = None
+        self.vc: Optional[list] = None
+        self.graphs: List[torch.cuda.CUDAGraph] = []
+        self.frame = 0          # graph replays so far (selects the ping-pong direction)
+        self.inp = None
+        self.out = None
+        self.sets = None        # [(k[8], v[8]) for A, B]
+        self.t_full = None
+
+    # ------------------------------------------------------------------------------------------
+    def _full(self, kc) -> bool:
+        """True once every cache slot has its steady-state extent (outputs shaped like inputs)."""
+        if kc is None:
+            return False
+        t_in = self._t_in(kc)
+        _, ks, _ = self.m.cache_layout(self.B, self.H, self.W, t_in)
+        kind, _, _ = self.m.cache_layout(self.B, self.H, self.W, [0] * 8)
+        for i in range(8):
+            if kind[i] == 0:
+                continue
+            got = tuple(kc[i].shape)
+            want = ks[i][:4] if kind[i] == 1 else ks[i]
+            if got != tuple(want):
+                return False
+        return True
+
+    def _t_in(self, kc) -> List[int]:
+        kind, _, _ = self.m.cache_layout(self.B, self.H, self.W, [0] * 8)
+        t = [0] * 8
+        for i in range(8):
+            if kind[i] == 1 and kc[i] is not None:
+                t[i] = int(kc[i].shape[2])
+            elif kind[i] == 2 and kc[i] is not None:
+                t[i] = int(kc[i].shape[1])
+        return t
+
+    def _alloc_set(self, kind, ks, vs, cdt):
+        k, v = [None] * 8, [None] * 8
+        for i in range(8):
+            if kind[i] == 1:
+                s4 = ks[i][:4]
+                st = TurtleHIP._fhr_strides(s4)
+                k[i] = torch.empty_strided(s4, st, dtype=cdt, device=self.dev)
+                v[i] = torch.empty_strided(s4, st, dtype=cdt, device=self.dev)
+            elif kind[i] == 2:
+                k[i] = torch.empty(ks[i], dtype=cdt, device=self.dev)
+                v[i] = torch.empty(vs[i], dtype=cdt, device=self.dev)
+        return k, v
+
+    def _capture(self):
+        m = self.m
+        cdt = m.compute_dtype
+        self.t_full = self._t_in(self.kc)
+        kind, ks, vs = m.cache_layout(self.B, self.H, self.W, self.t_full)
+        A = self._alloc_set(kind, ks, vs, cdt)
+        Bs = self._alloc_set(kind, ks, vs, cdt)
+        for i in range(8):                       # seed set A with the eager frames' history
+            if kind[i]:
+                A[0][i].copy_(self.kc[i])
+                A[1][i].copy_(self.vc[i])
+        self.sets = [A, Bs]
+        s = 4 if m.sr else 1
+        self.out = torch.empty(self.B, 3, self.H * s, self.W * s, dtype=torch.float32, device=self.dev)
+        ws = m._workspace(self.B, self.H, self.W, self.dev)
+        L = _lib.lib()
+
+        def ptrs(lst):
+            return (C.c_void_p * 8)(*[C.c_void_p(t.data_ptr()) if t is not None else None for t in lst])
+
+        torch.cuda.synchronize(self.dev)
+        for d in range(2):
+            src, dst = self.sets[d], self.sets[1 - d]
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                stream = torch.cuda.current_stream(self.dev).cuda_stream
+                _lib.check(L.turtle_forward(
+                    m._handle.h, C.c_void_p(self.inp.data_ptr()), self.B, self.H, self.W,
+                    C.c_void_p(self.out.data_ptr()), ptrs(src[0]), ptrs(src[1]),
+                    (C.c_int * 8)(*self.t_full), ptrs(dst[0]), ptrs(dst[1]),
+                    C.c_void_p(ws.data_ptr()), ws.numel(), C.c_void_p(stream)))
+            self.graphs.append(g)
+        self._ws = ws
+
+    # ------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def __call__(self, inp_img_: torch.Tensor):
+        """Restore one frame: ``inp_img_`` [B, 2, 3, H, W] (previous, current). Returns
+        (out [B, 3, H', W'] fp32, k_list[8], v_list[8]); out and caches are runner-owned buffers."""
+        if tuple(inp_img_.shape) != (self.B, 2, 3, self.H, self.W):
+            raise ValueError(f"expected [{self.B}, 2, 3, {self.H}, {self.W}], got {tuple(inp_img_.shape)}")
+        if not self.graphs:
+            if not self._full(self.kc):
+                out, self.kc, self.vc = self.m(inp_img_, self.kc, self.vc)
+                return out, self.kc, self.vc
+            self.inp = torch.empty(self.B, 2, 3, self.H, self.W, dtype=torch.float32, device=self.dev)
+            self.inp.copy_(inp_img_)
+            self._capture()
+        else:
+            self.inp.copy_(inp_img_)
+        d = self.frame % 2
+        self.graphs[d].replay()
+        self.frame += 1
+        k, v = self.sets[1 - d]
+        return self.out, k, v
