@@ -134,14 +134,24 @@ def test_graphed_frame_loop_matches_eager(dtype):
             inp = torch.stack([clip[:, max(j - 1, 0)], clip[:, j]], dim=1)
             ref, kc, vc = m(inp, kc, vc)
             out, kg, vg = runner(inp)
-            if dtype == "fp32":
-                err = float((out - ref).abs().max())
-                assert err <= 1e-5, (j, err)
-            else:   # the bf16 path is not bitwise run-to-run (hipBLASLt stream-K GEMMs): 50 dB gate
-                p = psnr(out.cpu().numpy(), ref.cpu().numpy())
-                assert p >= 50.0, (j, p)
+            # every kernel is deterministic, so replay and eager launches agree bit for bit
+            assert torch.equal(out, ref), (j, float((out - ref).abs().max()))
     assert len(runner.graphs) == 2 and runner.frame == 4
     for a, b in zip(kg + vg, kc + vc):
         if b is not None:
-            d = float((a.float() - b.float()).abs().mean())
-            assert d <= (1e-6 if dtype == "fp32" else 3e-2 * float(b.float().abs().mean()) + 1e-6), d
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_forward_is_bitwise_repeatable(dtype):
+    """The same frame through the same module three times gives identical bits (no atomics or
+    order-dependent reductions on the path; the Gram norms once used LDS float atomics, which made
+    bf16 frames differ by ~3.5e-3 run to run)."""
+    from turtlevsr_amd.synthetic import synthetic_frames
+    _, meta = load("clip_gopro_64")
+    x = torch.from_numpy(synthetic_frames((1, 2, 3, 256, 256), 29)).cuda()
+    m = _model(meta["opt"], meta["seed"], False, dtype)
+    with torch.no_grad():
+        outs = [m(x, None, None)[0].clone() for _ in range(3)]
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0]), float((o - outs[0]).abs().max())

@@ -31,6 +31,13 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_gram[4];
 // GP pixels keeps ~16-32 KB per block in flight. MT = accumulator tiles per wave (compile time,
 // so the accumulators of a 1-segment Gram do not cost the registers of a 6-segment one).
 constexpr int GNU = 8;
+// byte offset of the norms in the Gram kernel's dynamic LDS: past the [GP] operand rows and past
+// the [PS][ch + ncol] fp32 norm partials that reuse them after the pixel loop
+__host__ __device__ inline int gram_nrm_off(int GP, int ch, int ncol, int ES, int VEC) {
+  const int tiles = GP * ((ch + ncol) * ES + 32);
+  const int parts = (256 / ((ch + ncol) / VEC)) * (ch + ncol) * 4;
+  return tiles > parts ? tiles : parts;
+}
 template <typename T, int GP, int MT>
 __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
@@ -39,7 +46,6 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
   const int RQ = ch * ES + 16, RK = ncol * ES + 16;          // LDS row strides (bytes)
   char* sq = gsm;                                            // [GP][RQ]
   char* sk = gsm + GP * RQ;                                  // [GP][RK]
-  float* nrm = reinterpret_cast<float*>(gsm + GP * (RQ + RK)); // [ch + ncol]
   const int bh = blockIdx.x / a.nchunk, chunk = blockIdx.x % a.nchunk;
   const int b = bh / a.heads, h = bh % a.heads;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -47,6 +53,8 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
   const int tj_n = ncol / 16, TT = (ch / 16) * tj_n;
   const int qv = ch / VEC, CVt = (ch + ncol) / VEC;          // vectors per pixel
   const int PS = 256 / CVt;                                  // pixel rows per pass
+  // [ch + ncol] norms after the operand tiles / the norm partials, whichever is larger
+  float* nrm = reinterpret_cast<float*>(gsm + gram_nrm_off(GP, ch, ncol, ES, VEC));
   const int cv = tid % CVt, pg = tid / CVt;
   const bool tact = pg < PS;
 
@@ -155,10 +163,23 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
     }
     __syncthreads();
   }
-  // column sums of squares: PS threads per channel vector -> LDS atomics
-  if (tact) {
+  // column sums of squares: PS threads per channel vector, summed in a fixed order (the operand
+  // tiles are dead after the loop's last barrier, so their LDS holds the [PS][ch + ncol] partials:
+  // PS * (ch + ncol) * 4 <= GP * (RQ + RK) for every GP >= 32). LDS float atomics here made the
+  // norms - and through bf16 rounding the whole frame - differ run to run.
+  {
+    float* part = reinterpret_cast<float*>(gsm);
+    const int ncw = ch + ncol;
+    if (tact) {
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) atomicAdd(&nrm[cv * VEC + e], sqs[e]);
+      for (int e = 0; e < VEC; ++e) part[pg * ncw + cv * VEC + e] = sqs[e];
+    }
+    __syncthreads();
+    for (int i = tid; i < ncw; i += 256) {
+      float s = 0.f;
+      for (int r = 0; r < PS; ++r) s += part[r * ncw + i];
+      nrm[i] = s;
+    }
   }
   __syncthreads();
   const int stride = ch * ncol + ch + ncol;
@@ -179,7 +200,7 @@ __global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
 template <typename T, int GP, int MT>
 static void launch_gram_cfg(const GramArgs& a, hipStream_t st) {
   const int ncol = a.nseg * a.ch;
-  const size_t lds = (size_t)GP * ((a.ch + ncol) * sizeof(T) + 32) + (a.ch + ncol) * sizeof(float);
+  const size_t lds = (size_t)gram_nrm_off(GP, a.ch, ncol, (int)sizeof(T), Vec<T>::N) + (a.ch + ncol) * sizeof(float);
   hipLaunchKernelGGL((gram_kernel<T, GP, MT>), dim3((unsigned)(a.B * a.heads * a.nchunk)), dim3(256), lds, st, a);
 }
 
