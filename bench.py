@@ -9,19 +9,25 @@ synthetic frames resident in HBM; weights are the deterministic synthetic init o
 architecture (59.08 M params, random-init, no checkpoint reachable offline).
 Multi-GPU: inference does not shard (a clip's frames are sequentially dependent): every rank runs
 an independent clip replica ("replicas only", scaling weak); value = frames of all ranks / max
-rank time.
+rank time. `--gpus N` without an external launcher spawns the N worker processes itself (before
+any GPU call); under torch.distributed.run, WORLD_SIZE must equal N.
 
 The JSON line also carries
 * roofline: the dominant kernel launch shape (most GPU time over the warmup frames, where every
   launch is event-timed) priced with its algorithmic bytes or FLOPs per launch over its average
   duration, timed by HIP events (on the forward's stream) around exactly that shape's launches
-  inside the timed region, so the events do not inflate the frame time;
-  traffic = its PMC HBM bytes per launch from the committed profiles/r01_pmc_traffic.json;
+  inside the timed region, so the events do not inflate the frame time. Bytes count each distinct
+  tensor once (a fused block's residual is its own input); both the HBM and the MFMA fraction are
+  given, `frac` is the binding one (arithmetic intensity vs the 312 FLOP/B ridge);
+  traffic = its PMC HBM bytes per launch from profiles/pmc_traffic.json, used only when that file
+  was measured on the same kernel sources (source hash), else null;
 * cpu_baseline: the CPU oracle (oracle/turtle_ref.py, fp32 PyTorch CPU restatement of the
-  reference) on a bounded 256x256 steady-state sample, scaled to 1080p frames/s by the
-  algorithmic FLOP ratio (BASELINE.md §3);
+  reference, dense SAB like the reference) timed on a bounded 256x256 steady-state sample on the
+  host cores, scaled to the bench resolution by the reference's own FLOP ratio F_ref
+  (SURVEY.md §8(a)); host CPU model, nproc and threads stated;
 * psnr_bf16_vs_fp32_db: the bf16 output vs the fp32 HIP output (itself parity-tested against the
-  reference) on the same 1080p frames.
+  reference) on the same frames; psnr_delta_vs_fp32_db: |uint8 PSNR(bf16, clean) - uint8
+  PSNR(fp32, clean)| on a denoising clip at the bench resolution (north star: <= 0.01 dB).
 """
 from __future__ import annotations
 
@@ -42,7 +48,7 @@ sys.path.insert(0, REPO)
 
 from turtlevsr_amd.graph import GraphedTurtle  # noqa: E402
 from turtlevsr_amd.model import TurtleHIP  # noqa: E402
-from turtlevsr_amd.replicas import clip_seed, replica_throughput  # noqa: E402
+from turtlevsr_amd.replicas import check_world, clip_seed, launch_workers, replica_throughput  # noqa: E402
 from turtlevsr_amd.synthetic import synthetic_frames, synthetic_state_dict  # noqa: E402
 
 RES = {"1080p": (1080, 1920), "540p": (540, 960), "256": (256, 256), "128": (128, 128)}
@@ -58,6 +64,41 @@ def f_alg(h, w):
     return 5.8884e6 * p1 + 6912 * n * n + 9.0440e6 * n
 
 
+def f_ref(h, w):
+    """The reference's FLOPs per steady-state frame (dense SAB A.v):
+    5.8884e6 P1 + 2 N^2 * 101760. The CPU oracle computes the same dense graph."""
+    hp, wp = (h + 31) // 32 * 32, (w + 31) // 32 * 32
+    p1 = hp * wp
+    n = p1 / 256
+    return 5.8884e6 * p1 + 2 * n * n * 101760
+
+
+def source_hash():
+    """Hash of the HIP kernel sources + build script: ties committed PMC counters to the kernels
+    they were measured on."""
+    import hashlib
+    hs = hashlib.sha256()
+    base = os.path.join(REPO, "turtlevsr_amd")
+    for rel in sorted(os.listdir(os.path.join(base, "csrc"))) + ["../build.py"]:
+        path = os.path.join(base, "csrc", rel)
+        if os.path.isfile(path):
+            hs.update(rel.encode())
+            with open(path, "rb") as f:
+                hs.update(f.read())
+    return hs.hexdigest()[:16]
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def load_opt():
     with open(os.path.join(REPO, "options", "Turtle_Deblur_Gopro.yml")) as f:
         return yaml.safe_load(f)
@@ -70,13 +111,22 @@ def build_model(opt, dtype, dev, sr=False):
     return m.to(dev).eval()
 
 
+def denoise_clip(n, h, w, batch, dev, sigma=25.0, seed=3):
+    """Smooth clean frames (x8 bilinear-upsampled noise) and noisy inputs (+ N(0, sigma/255))."""
+    g = torch.Generator().manual_seed(seed)
+    low = torch.rand(batch * n, 3, h // 8 + 1, w // 8 + 1, generator=g)
+    clean = torch.nn.functional.interpolate(low, size=(h, w), mode="bilinear", align_corners=False)
+    noisy = clean + torch.randn(clean.shape, generator=g) * (sigma / 255.0)
+    return (clean.reshape(batch, n, 3, h, w).to(dev), noisy.reshape(batch, n, 3, h, w).to(dev))
+
+
 def clip_frames(h, w, seed, dev, n=5, batch=1):
     clip = torch.from_numpy(synthetic_frames((batch, n, 3, h, w), seed)).to(dev)
     return [torch.stack([clip[:, max(j - 1, 0)], clip[:, j]], dim=1).contiguous() for j in range(n)]
 
 
 def cpu_baseline(opt, threads):
-    """Oracle fp32 on a 256x256 steady-state frame (3 priming frames untimed, 2 timed)."""
+    """Oracle fp32 on a 256x256 steady-state frame (3 priming frames untimed, 2 timed): s/frame."""
     from oracle import turtle_ref as R
     torch.set_num_threads(threads)
     m = TurtleHIP(opt)
@@ -112,12 +162,16 @@ def launch_groups(dump):
 
 def pmc_traffic():
     """HBM bytes per launch by launch tag, from the committed rocprofv3 FETCH_SIZE / WRITE_SIZE
-    passes (tools/pmc_traffic.py; FETCH_SIZE doubled for the gfx950 wide-read undercount)."""
-    path = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+    passes (tools/pmc_traffic.py; FETCH_SIZE doubled for the gfx950 wide-read undercount), only
+    if they were measured on the current kernel sources."""
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return {}
+        return {}, None
     with open(path) as f:
-        return json.load(f).get("per_tag", {})
+        d = json.load(f)
+    if d.get("source_hash") != source_hash():
+        return {}, d.get("source")
+    return d.get("per_tag", {}), d.get("source")
 
 
 def roofline(wprof, wgroups, nwarm, tgroups, steps, dtype):
@@ -134,6 +188,8 @@ def roofline(wprof, wgroups, nwarm, tgroups, steps, dtype):
     avg_s = g["ms"] * 1e-3 / n
     bpl, fpl = g["bytes"] / n, g["flops"] / n
     ridge = MFMA_PEAK[dtype] * 1e12 / (HBM_PEAK_GBS * 1e9)
+    hbm_frac = bpl / avg_s / 1e9 / HBM_PEAK_GBS
+    mfma_frac = fpl / avg_s / 1e12 / MFMA_PEAK[dtype]
     if fpl / max(bpl, 1.0) < ridge:
         ach = bpl / avg_s / 1e9
         roof = dict(bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4))
@@ -141,8 +197,12 @@ def roofline(wprof, wgroups, nwarm, tgroups, steps, dtype):
         ach = fpl / avg_s / 1e12
         roof = dict(bound="mfma", achieved=round(ach, 2), peak=MFMA_PEAK[dtype], unit="TFLOP/s",
                     frac=round(ach / MFMA_PEAK[dtype], 4))
-    tr = pmc_traffic().get(tag)
+    per_tag, pmc_src = pmc_traffic()
+    tr = per_tag.get(tag)
     roof.update(traffic=round(tr["hbm_bytes_per_launch"]) if tr else None, kernel=tag,
+                hbm_frac=round(hbm_frac, 4), mfma_frac=round(mfma_frac, 4),
+                arithmetic_intensity=round(fpl / max(bpl, 1.0), 1), ridge_flop_per_byte=round(ridge, 1),
+                traffic_source=(pmc_src if tr else f"none measured on kernel sources {source_hash()}"),
                 launches_per_step=g["launches"] / steps, avg_launch_us=round(avg_s * 1e6, 2),
                 algorithmic_bytes_per_launch=round(bpl), algorithmic_flops_per_launch=round(fpl),
                 mfma_tflops=round(fpl / avg_s / 1e12, 2), hbm_gbs=round(bpl / avg_s / 1e9, 1),
@@ -172,6 +232,10 @@ def main():
     if args.graph:
         args.no_roofline = True      # per-launch profiling events cannot live inside a captured graph
 
+    # one process per GPU: spawn the workers here, before this process touches the GPU, unless an
+    # external launcher (torch.distributed.run) already did; its WORLD_SIZE must match --gpus
+    if check_world(args.gpus) is None and args.gpus > 1:
+        sys.exit(launch_workers(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -253,8 +317,9 @@ def main():
         if os.path.exists(f):
             os.remove(f)
 
-    psnr = None
+    psnr = dpsnr = None
     if not args.no_psnr and rank == 0 and args.dtype == "bf16":
+        from turtlevsr_amd.harness import calc_PSNR, tensor2img
         ref = build_model(opt, "fp32", dev, args.sr)
         kr = vr = None
         kb = vb = None
@@ -265,17 +330,37 @@ def main():
                 o16, kb, vb = model(frames[jj], kb, vb)
                 mse = float(((o32 - o16) ** 2).mean())
                 vals.append(10 * np.log10(1.0 / max(mse, 1e-20)))
-        psnr = round(min(vals), 2)
+            psnr = round(min(vals), 2)
+            # north-star PSNR delta: a denoising clip (smooth clean frames + N(0, 25/255)) through the
+            # fp32 and bf16 builds, uint8 PSNR vs the clean frames (inference.py:52-61, 324-325)
+            clean, noisy = denoise_clip(4, h // 4 if args.sr else h, w // 4 if args.sr else w, args.batch, dev)
+            kr = vr = kb = vb = None
+            deltas = []
+            for jj in range(4):
+                x = torch.stack([noisy[:, max(jj - 1, 0)], noisy[:, jj]], dim=1).contiguous()
+                o32, kr, vr = ref(x, kr, vr)
+                o16, kb, vb = model(x, kb, vb)
+                if args.sr:
+                    gt = torch.nn.functional.interpolate(clean[:, jj], scale_factor=4, mode="bilinear", align_corners=False)
+                else:
+                    gt = clean[:, jj]
+                p32 = calc_PSNR(tensor2img(o32[0]), tensor2img(gt[0]))
+                p16 = calc_PSNR(tensor2img(o16[0]), tensor2img(gt[0]))
+                deltas.append(abs(p16 - p32))
+            dpsnr = round(max(deltas), 5)
         del ref
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         dt = cpu_baseline(opt, threads)
-        scale = f_alg(256, 256) / f_alg(h, w)
+        scale = f_ref(256, 256) / f_ref(h, w)     # (SR: the network runs at the output size)
         cpu = dict(value=round(scale / dt, 6), unit="frames/s", cores=threads, kind="port",
-                   sample=f"oracle/turtle_ref.py fp32 on 2 steady-state 256x256 GoPro frames ({dt:.2f} s/frame, "
-                          f"{threads} threads), scaled to {args.res} by F_alg ratio {scale:.5f}")
+                   measured_s_per_frame_256=round(dt, 3), cpu_model=cpu_model(), nproc=os.cpu_count(),
+                   torch_threads=torch.get_num_threads(),
+                   sample=f"oracle/turtle_ref.py fp32 (dense SAB, as the reference) on 2 steady-state 256x256 GoPro "
+                          f"frames after 3 priming frames: {dt:.2f} s/frame on {threads} threads; scaled to "
+                          f"{w}x{h} by the reference FLOP ratio F_ref(256^2)/F_ref = {scale:.5f}")
 
     line = {
         "metric": "restored frames/sec @1080p (1/2/4/8 GPU) + PSNR delta vs ref"
@@ -300,6 +385,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "psnr_bf16_vs_fp32_db": psnr,
+        "psnr_delta_vs_fp32_db": dpsnr,
         "alg_tflops": round(f_alg(h, w) * fps / 1e12, 2),
     }
     if rank == 0:

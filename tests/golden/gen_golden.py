@@ -85,8 +85,11 @@ def summary(t: torch.Tensor, nsamp: int = 256) -> dict:
                 idx=idx.astype(np.int64), samp=a[idx].astype(np.float32))
 
 
-def run_clip(model, clip: np.ndarray, full_caches: bool):
-    """Causal loop of video_restoration_model.py:85-92 on the reference model."""
+def run_clip(model, clip: np.ndarray, full_caches: bool, full_out=None):
+    """Causal loop of video_restoration_model.py:85-92 on the reference model.
+
+    full_out: frame indices whose output is stored in full (None: every frame); the others are
+    stored as checksums + samples (``out{j}__*``) to keep large clips small."""
     x = torch.from_numpy(clip)
     kc = vc = None
     rec = {}
@@ -94,7 +97,11 @@ def run_clip(model, clip: np.ndarray, full_caches: bool):
         for j in range(x.shape[1]):
             inp = torch.stack([x[:, max(j - 1, 0)], x[:, j]], dim=1)
             out, kc, vc = model(inp, kc, vc)
-            rec[f"out{j}"] = out.numpy().astype(np.float32)
+            if full_out is None or j in full_out:
+                rec[f"out{j}"] = out.numpy().astype(np.float32)
+            else:
+                for sk, sv in summary(out, 1024).items():
+                    rec[f"out{j}__{sk}"] = sv
             for which, lst in (("k", kc), ("v", vc)):
                 for i, t in enumerate(lst):
                     if t is None:
@@ -114,7 +121,24 @@ def save(name: str, arrays: dict, meta: dict):
     print("wrote", name, sum(v.nbytes for v in arrays.values() if hasattr(v, "nbytes")) / 1e6, "MB raw")
 
 
-def gen_clips(t1, sr):
+# heterogeneous per-level attention / FFN types (tiny widths): every decoder level differs from
+# its encoder twin and from the other decoder levels, so a swapped decoder1/decoder3 key mapping
+# (turtle_t1_arch.py:1009-1027), a cache slot on an encoder level (FHR at slot 0, CHM with ws=2 at
+# slot 1), an FHR cache on a decoder level and a level without cache all change the output
+HETERO = dict(encoder1_attn_type1="Channel", encoder1_attn_type2="FHR", encoder1_ffw_type="GFFW",
+              encoder2_attn_type1="ReducedAttn", encoder2_attn_type2="FHR", encoder2_ffw_type="GFFW",
+              encoder3_attn_type1="NoAttn", encoder3_attn_type2="ReducedAttn", encoder3_ffw_type="FFW",
+              decoder1_attn_type1="ReducedAttn", decoder1_attn_type2="FHR", decoder1_ffw_type="FFW",
+              decoder2_attn_type1="FHR", decoder2_attn_type2="CHM", decoder2_ffw_type="GFFW",
+              decoder3_attn_type1="Channel", decoder3_attn_type2="Channel", decoder3_ffw_type="GFFW",
+              latent_attn_type1="FHR", latent_attn_type2="ReducedAttn", latent_attn_type3="Channel",
+              refinement_attn_type1="Channel", refinement_attn_type2="NoAttn", refinement_ffw_type="FFW",
+              Middle_blocks=3, Enc_blocks=[2, 2, 2], Dec_blocks=[2, 2, 2])
+# (a CHM on an encoder / latent / refinement level has SAB window 2, where the reference's q/k token
+# grid (H+2-2)/2+1 no longer matches the v tokens: torch.matmul raises there, turtle_t1_arch.py:599)
+
+
+def gen_clips(t1, sr, only=None):
     torch.set_num_threads(8)
     jobs = [
         # name, module, opt, clip shape, full caches, seed
@@ -124,15 +148,31 @@ def gen_clips(t1, sr):
         ("clip_tiny_biasfree", t1, tiny_opt(LayerNorm_type="BiasFree"), (1, 2, 3, 64, 64), False, 4),
         ("clip_tiny_sr", sr, tiny_opt(), (1, 3, 3, 16, 24), False, 5),
         ("clip_gopro_64", t1, gopro_opt(), (1, 4, 3, 64, 64), False, 6),
+        # round 2: steady state (T = 4 / 3 cached frames) with N >= 64 SAB tokens at every CHM level,
+        # where the radius-4 L1 ball no longer covers the key set and top-5 picks far keys
+        # (turtle_t1_arch.py:585-596): 256x256 -> N = 256, 128x224 (non-square) -> N = 112
+        ("clip_gopro_256", t1, gopro_opt(), (1, 5, 3, 256, 256), False, 8, (3, 4)),
+        ("clip_gopro_128x224", t1, gopro_opt(), (1, 5, 3, 128, 224), False, 9, None),
+        ("clip_tiny_hetero", t1, tiny_opt(**HETERO), (1, 5, 3, 64, 64), True, 10, None),
     ]
-    for name, mod, opt, shape, full, seed in jobs:
+    for job in jobs:
+        name, mod, opt, shape, full, seed = job[:6]
+        full_out = job[6] if len(job) > 6 else None
+        if only and name not in only:
+            continue
         torch.manual_seed(0)
         model = mod.make_model(opt).eval()
         fill(model, seed)
         clip = synthetic_frames(shape, seed, name="frames")
-        rec = run_clip(model, clip, full)
-        rec["clip"] = clip
-        save(name, rec, dict(opt=arch_opt(opt), seed=seed, sr=mod is sr, shape=list(shape)))
+        rec = run_clip(model, clip, full, full_out)
+        meta = dict(opt=arch_opt(opt), seed=seed, sr=mod is sr, shape=list(shape))
+        if clip.size > 600_000:
+            # large inputs are not stored: tests regenerate them with
+            # synthetic_frames(shape, seed, name="frames") and check this checksum
+            meta["clip_sum"] = float(clip.astype(np.float64).sum())
+        else:
+            rec["clip"] = clip
+        save(name, rec, meta)
 
 
 def gen_blocks(t1):
@@ -230,3 +270,6 @@ if __name__ == "__main__":
         gen_blocks(t1)
     if "clips" in which:
         gen_clips(t1, sr)
+    named = [w for w in which if w.startswith("clip_")]   # e.g. `gen_golden.py clip_gopro_256`
+    if named:
+        gen_clips(t1, sr, only=named)

@@ -40,3 +40,25 @@ def check_summary(rec, key, t, rtol=1e-4, atol=1e-5):
     np.testing.assert_allclose(samp, rec[key + "__samp"], rtol=rtol, atol=atol, err_msg=key)
     np.testing.assert_allclose(a.sum(), rec[key + "__sum"], rtol=1e-4, atol=atol * a.size ** 0.5, err_msg=key)
     np.testing.assert_allclose(np.abs(a).sum(), rec[key + "__abssum"], rtol=1e-4, err_msg=key)
+
+
+def clip_input(g, meta):
+    """The clip a golden file was generated from: stored (`clip`) for small inputs, else regenerated
+    with the same deterministic generator and checked against the stored checksum."""
+    if "clip" in g:
+        return g["clip"]
+    from turtlevsr_amd.synthetic import synthetic_frames
+    clip = synthetic_frames(tuple(meta["shape"]), meta["seed"], name="frames")
+    np.testing.assert_allclose(clip.astype(np.float64).sum(), meta["clip_sum"], rtol=1e-12)
+    return clip
+
+
+def check_out(g, j, o, atol, rtol):
+    """Frame j's output against the golden record: in full where stored, else checksum + samples."""
+    o = o.detach().cpu() if torch.is_tensor(o) else torch.from_numpy(np.asarray(o))
+    key = f"out{j}"
+    if key in g:
+        np.testing.assert_allclose(o.numpy(), g[key], atol=atol, rtol=rtol, err_msg=key)
+        return float(np.abs(o.numpy() - g[key]).max())
+    check_summary(g, key, o, rtol=rtol, atol=atol)
+    return None

@@ -111,3 +111,18 @@ def test_graphed_runner_refuses_cpu_and_foreign_modules():
         GraphedTurtle(TurtleHIP(opt), 1, 64, 64)
     with pytest.raises(TypeError):
         GraphedTurtle(torch.nn.Linear(2, 2), 1, 64, 64)
+
+
+def test_chm_on_encoder_level_is_refused():
+    """A CHM on a level with Scale_patchsize 1 has SAB window 2: the reference's q/k token grid
+    ((H+2-2)/2+1) no longer matches the v tokens (H/2) and attn @ v raises (turtle_t1_arch.py:
+    573-599). The library refuses it when sizing the workspace (a dry run of the frame driver)."""
+    o = dict(gopro(), encoder2_attn_type2="CHM")
+    L, h = handle(o, False, 1)
+    ws = C.c_size_t()
+    rc = L.turtle_workspace_size(h, 1, 64, 64, C.byref(ws))
+    assert rc != 0 and b"token grid" in L.turtle_last_error()
+    L.turtle_destroy(h)
+    L, h = handle(gopro(), False, 1)
+    _lib.check(L.turtle_workspace_size(h, 1, 64, 64, C.byref(ws)))
+    L.turtle_destroy(h)

@@ -112,6 +112,70 @@ def test_load_checkpoint_strips_module_prefix(tmp_path):
         load_checkpoint(dst, path)
 
 
+def test_y_channel_psnr_follows_reference_conversion():
+    """Y-channel PSNR builds its uint8 images like inference.py:314-319: (x*255).astype(uint8),
+    truncating, no clamp (the RGB path rounds through tensor2img instead)."""
+    gt = torch.full((3, 4, 4), 0.5)               # 127.5 -> 127 truncated (128 rounded)
+    out = torch.full((3, 4, 4), 0.5)
+    out[:, 0, 0] = 0.503                          # 128.27 -> 128
+    res = run_video([out], [gt], lambda x, k, v: (x[:, 1], [None] * 8, [None] * 8), y_channel_PSNR=True)
+    g8 = (gt * 255.0).permute(1, 2, 0).numpy().astype(np.uint8)
+    o8 = (out * 255.0).permute(1, 2, 0).numpy().astype(np.uint8)
+    want = calc_PSNR(bgr2ycbcr(o8[:, :, ::-1]), bgr2ycbcr(g8[:, :, ::-1]))
+    assert res.psnr[0] == pytest.approx(want)
+    assert int(g8[0, 0, 0]) == 127 and int(o8[0, 0, 0]) == 128
+
+
+def test_load_checkpoint_full_turtle_state_dict(tmp_path):
+    """A reference-style GoPro checkpoint ({'params': state_dict} with the DDP `module.` prefix,
+    base_model.py:194-224) loads strictly into the HIP module: all 633 keys, values unchanged."""
+    import yaml
+    from golden_io import synth_sd
+    from turtlevsr_amd.model import TurtleHIP
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "options",
+                           "Turtle_Deblur_Gopro.yml")) as f:
+        opt = yaml.safe_load(f)
+    m = TurtleHIP(opt)
+    shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+    assert len(shapes) == 633
+    sd = synth_sd(shapes, 3)
+    path = os.path.join(tmp_path, "net_g_latest.pth")
+    torch.save({"params": {"module." + k: v for k, v in sd.items()}}, path)
+    load_checkpoint(m, path)
+    for k, v in m.state_dict().items():
+        assert torch.equal(v, sd[k]), k
+    torch.save({"params": {"module." + k: v for k, v in list(sd.items())[:-1]}}, path)
+    with pytest.raises(RuntimeError):
+        load_checkpoint(TurtleHIP(opt), path)
+
+
+def test_cache_shapes_are_checked_against_the_frame():
+    """Incoming caches must match this frame's batch / size up to their temporal extent (the
+    kernels index them with the frame's dimensions)."""
+    from turtlevsr_amd.model import TurtleHIP
+    kind = [0, 0, 0, 1, 0, 2, 0, 0]
+    ks = [(1,) * 5] * 3 + [(2, 8, 128, 1024, 1)] + [(1,) * 5] + [(2, 2, 1, 256, 512)] + [(1,) * 5] * 2
+    vs = [(1,) * 5] * 5 + [(2, 2, 1, 256, 4096)] + [(1,) * 5] * 2
+    t_in = [0, 0, 0, 64, 0, 1, 0, 0]
+    kc = [None] * 8
+    vc = [None] * 8
+    kc[3] = vc[3] = torch.empty(2, 8, 64, 1024)
+    kc[5], vc[5] = torch.empty(2, 1, 1, 256, 512), torch.empty(2, 1, 1, 256, 4096)
+    TurtleHIP._check_caches(kind, ks, vs, t_in, kc, vc)
+    bad = list(kc)
+    bad[5] = torch.empty(2, 1, 1, 64, 512)           # caches of a smaller frame
+    with pytest.raises(ValueError):
+        TurtleHIP._check_caches(kind, ks, vs, t_in, bad, vc)
+    bad = list(kc)
+    bad[3] = torch.empty(1, 8, 64, 1024)             # another batch size
+    with pytest.raises(ValueError):
+        TurtleHIP._check_caches(kind, ks, vs, t_in, bad, vc)
+    bad = list(vc)
+    bad[5] = None
+    with pytest.raises(ValueError):
+        TurtleHIP._check_caches(kind, ks, vs, t_in, kc, bad)
+
+
 def _oracle_model(meta):
     from golden_io import synth_sd
     from oracle import turtle_ref as R

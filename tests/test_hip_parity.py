@@ -2,19 +2,23 @@
 
 All calls go through the C ABI (ctypes) of the in-tree library; there is no fallback.
 fp32 gate: max-abs <= 2e-4 on outputs (values O(1)) and PSNR(build, reference) >= 80 dB;
-bf16 gate: PSNR(build, reference fp32) >= 45 dB per frame (the reference's own fp32 vs
-bf16-autocast gap is 62 dB).
+bf16 gate: PSNR(build, reference fp32) >= 58 dB per frame (the reference's own fp32 vs
+bf16-autocast gap is 62 dB; the build measured 61.7 dB at 1080p in round 1).
+Steady state with N >= 64 SAB tokens is pinned by reference clips at 256x256 (N = 256, 5 frames,
+T = 4 cached frames at dec3/dec2) and 128x224 (non-square, N = 112).
 """
 import numpy as np
 import pytest
 import torch
 
-from golden_io import check_summary, load, synth_sd
+from golden_io import check_out, check_summary, clip_input, load, synth_sd
 
 pytestmark = pytest.mark.gpu
 
 CLIPS = ["clip_tiny_64", "clip_tiny_ragged", "clip_tiny_both", "clip_tiny_biasfree", "clip_tiny_sr",
-         "clip_gopro_64", "clip_tiny_t0", "clip_gopro_t0"]
+         "clip_gopro_64", "clip_tiny_t0", "clip_gopro_t0", "clip_tiny_hetero", "clip_gopro_128x224",
+         "clip_gopro_256"]
+BF16_DB = 58.0
 
 
 def psnr(a, b):
@@ -49,12 +53,11 @@ def _run(m, clip):
 def test_clip_fp32_vs_reference(name):
     g, meta = load(name)
     m = _model(meta, "fp32")
-    outs, caches = _run(m, g["clip"])
+    outs, caches = _run(m, clip_input(g, meta))
     for j, o in enumerate(outs):
-        ref = g[f"out{j}"]
-        err = float(np.abs(o.numpy() - ref).max())
-        assert err <= 2e-4, (name, j, err)
-        assert psnr(o.numpy(), ref) >= 80.0
+        check_out(g, j, o, atol=2e-4, rtol=2e-3)
+        if f"out{j}" in g:
+            assert psnr(o.numpy(), g[f"out{j}"]) >= 80.0
         kc, vc = caches[j]
         for which, lst in (("k", kc), ("v", vc)):
             for i, t in enumerate(lst):
@@ -67,37 +70,76 @@ def test_clip_fp32_vs_reference(name):
                     np.testing.assert_allclose(t.numpy(), g[key], atol=2e-4, rtol=2e-3, err_msg=key)
 
 
-@pytest.mark.parametrize("name", ["clip_tiny_64", "clip_gopro_64", "clip_gopro_t0"])
+@pytest.mark.parametrize("name", ["clip_tiny_64", "clip_gopro_64", "clip_gopro_t0", "clip_tiny_hetero",
+                                  "clip_gopro_128x224", "clip_gopro_256"])
 def test_clip_bf16_psnr(name):
     g, meta = load(name)
     m = _model(meta, "bf16")
-    outs, _ = _run(m, g["clip"])
-    for j, o in enumerate(outs):
-        p = psnr(o.numpy(), g[f"out{j}"])
-        assert p >= 45.0, (name, j, p)
+    outs, _ = _run(m, clip_input(g, meta))
+    vals = [psnr(o.numpy(), g[f"out{j}"]) for j, o in enumerate(outs) if f"out{j}" in g]
+    print(name, "bf16 vs reference fp32 PSNR per frame:", [round(v, 2) for v in vals])
+    assert vals and min(vals) >= BF16_DB, (name, vals)
 
 
-def test_fp32_vs_oracle_256():
-    """GoPro widths at 256x256 (the bench shape), 3 frames, HIP fp32 vs the CPU oracle."""
+def test_fp32_vs_oracle_256_steady_state():
+    """GoPro widths at 256x256 (the bench shape), 5 frames: caches full from frame 3 on (T = 4 at
+    dec3 / dec2, 3 at dec1), HIP fp32 vs the CPU oracle on a clip no golden file holds."""
     from oracle import turtle_ref as R
     from turtlevsr_amd.synthetic import synthetic_frames
     g, meta = load("clip_gopro_64")
     m = _model(meta, "fp32")
-    clip = synthetic_frames((1, 3, 3, 256, 256), 7)
-    outs, _ = _run(m, clip)
+    clip = synthetic_frames((1, 5, 3, 256, 256), 7)
+    outs, caches = _run(m, clip)
     sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
     torch.set_num_threads(16)
-    ref, _ = R.run_clip(sd, meta["opt"], torch.from_numpy(clip))
-    for o, r in zip(outs, ref):
+    ref, rc = R.run_clip(sd, meta["opt"], torch.from_numpy(clip))
+    for j, (o, r) in enumerate(zip(outs, ref)):
+        assert float((o - r).abs().max()) <= 2e-4, j
         assert psnr(o.numpy(), r.numpy()) >= 80.0
+    for a, b in zip(caches[-1][0] + caches[-1][1], rc[-1][0] + rc[-1][1]):
+        if b is not None:
+            assert a.shape == b.shape
+            np.testing.assert_allclose(a.numpy(), b.numpy(), atol=2e-4, rtol=2e-3)
+
+
+def test_batched_clips_match_single_clip_runs():
+    """B = 8 clips restored together (per-image W_eff, per-image vendor / in-tree GEMM calls, Gram
+    splits that depend on B) equal the same clips restored one at a time: GoPro widths, 256x256,
+    4 frames (caches reach T = 4), fp32 to 2e-5 and bf16 to >= 58 dB; one clip also vs the oracle."""
+    from oracle import turtle_ref as R
+    from turtlevsr_amd.synthetic import synthetic_frames
+    _, meta = load("clip_gopro_64")
+    clip = synthetic_frames((8, 4, 3, 256, 256), 31)
+    for dtype in ("fp32", "bf16"):
+        m = _model(meta, dtype)
+        batched, bc = _run(m, clip)
+        for i in (0, 3, 7):
+            single, sc = _run(m, clip[i:i + 1])
+            for j in range(clip.shape[1]):
+                a, b = batched[j][i:i + 1], single[j]
+                if dtype == "fp32":
+                    assert float((a - b).abs().max()) <= 2e-5, (i, j)
+                else:
+                    assert psnr(a.numpy(), b.numpy()) >= BF16_DB, (i, j)
+            for x, y in zip(bc[-1][0] + bc[-1][1], sc[-1][0] + sc[-1][1]):
+                if y is not None:
+                    assert x.shape[0] == 8 and x.shape[1:] == y.shape[1:]
+                    if dtype == "fp32":
+                        np.testing.assert_allclose(x[i:i + 1].numpy(), y.numpy(), atol=2e-5, rtol=1e-4)
+        if dtype == "fp32":
+            sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+            torch.set_num_threads(16)
+            ref, _ = R.run_clip(sd, meta["opt"], torch.from_numpy(clip[5:6]))
+            for j, r in enumerate(ref):
+                assert float((batched[j][5:6] - r).abs().max()) <= 2e-4, j
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_kernel_variants_agree(dtype):
     """The kernel-selection switches (fused block kernels, panel GEMM) compute the same function:
     GoPro widths at 128x128, 3 frames, every switch setting against the reference golden clip's
-    arch/weights. fp32: variants agree to 2e-4; bf16: each variant >= 45 dB vs the fp32 build and
-    the variants within 50 dB of each other."""
+    arch/weights. fp32: variants agree to 2e-4; bf16: each variant >= 58 dB vs the fp32 build and
+    vs the all-off bf16 variant."""
     from turtlevsr_amd.synthetic import synthetic_frames
     _, meta = load("clip_gopro_64")
     clip = synthetic_frames((1, 3, 3, 128, 128), 11)
@@ -118,8 +160,8 @@ def test_kernel_variants_agree(dtype):
                 err = float((a - r).abs().max())
                 assert err <= 2e-4, (key, j, err)
             else:
-                assert psnr(a.numpy(), r.numpy()) >= 45.0, (key, j)
-                assert psnr(a.numpy(), outs[k0][j].numpy()) >= 50.0, (key, j)
+                assert psnr(a.numpy(), r.numpy()) >= BF16_DB, (key, j)
+                assert psnr(a.numpy(), outs[k0][j].numpy()) >= BF16_DB, (key, j)
 
 
 def _opts(m, opts):
@@ -138,7 +180,7 @@ def test_set_option_rejects_unknown():
 def test_biasfree_layernorm_gemm_variants():
     """BiasFree LayerNorm (x * rstd, uncentred: turtle_t1_arch.py:68-80) at GoPro widths, where the
     resident-panel GEMM applies the LayerNorm to its LDS panel: bf16 with gemm_pn on vs off agree
-    (>= 50 dB) and both stay >= 45 dB from the fp32 build (golden tiny clips are too narrow to
+    (>= 58 dB) and both stay >= 58 dB from the fp32 build (golden tiny clips are too narrow to
     reach that kernel)."""
     from turtlevsr_amd.synthetic import synthetic_frames
     _, meta = load("clip_gopro_64")
@@ -148,5 +190,5 @@ def test_biasfree_layernorm_gemm_variants():
     on = _run(_opts(_model(meta, "bf16"), {"gemm_pn": 1}), clip)[0]
     off = _run(_opts(_model(meta, "bf16"), {"gemm_pn": 0}), clip)[0]
     for j in range(len(ref)):
-        assert psnr(on[j].numpy(), off[j].numpy()) >= 50.0, j
-        assert psnr(on[j].numpy(), ref[j].numpy()) >= 45.0, j
+        assert psnr(on[j].numpy(), off[j].numpy()) >= BF16_DB, j
+        assert psnr(on[j].numpy(), ref[j].numpy()) >= BF16_DB, j

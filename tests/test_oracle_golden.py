@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from oracle import turtle_ref as R
-from golden_io import check_summary, load, synth_sd
+from golden_io import check_out, check_summary, clip_input, load, synth_sd
 from turtlevsr_amd.params import TurtleParams
 
 torch.set_num_threads(8)
@@ -115,7 +115,8 @@ def test_causal_history_model():
 
 
 CLIPS = ["clip_tiny_64", "clip_tiny_ragged", "clip_tiny_both", "clip_tiny_biasfree", "clip_tiny_sr",
-         "clip_gopro_64", "clip_tiny_t0", "clip_gopro_t0"]
+         "clip_gopro_64", "clip_tiny_t0", "clip_gopro_t0", "clip_tiny_hetero", "clip_gopro_128x224",
+         pytest.param("clip_gopro_256", marks=pytest.mark.slow)]
 
 
 @pytest.mark.parametrize("name", CLIPS)
@@ -124,10 +125,10 @@ def test_clip(name):
     opt = meta["opt"]
     shapes = {k: tuple(v.shape) for k, v in TurtleParams(opt).state_dict().items()}
     sd = synth_sd(shapes, meta["seed"])
-    clip = torch.from_numpy(g["clip"])
+    clip = torch.from_numpy(clip_input(g, meta))
     outs, caches = R.run_clip(sd, opt, clip, sr=meta["sr"])
     for j, o in enumerate(outs):
-        close(o, g[f"out{j}"], atol=5e-5, rtol=1e-3)
+        check_out(g, j, o, atol=5e-5, rtol=1e-3)
         kc, vc = caches[j]
         for which, lst in (("k", kc), ("v", vc)):
             for i, t in enumerate(lst):

@@ -65,3 +65,30 @@ def test_assign_clips_partition():
         assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         assign_clips(4, 2, 2)
+
+
+def _probe(args, env=None):
+    import json
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(here, "_launch_probe.py")] + args, env=e,
+                       capture_output=True, text=True, timeout=300)
+    return r.returncode, [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")], r.stderr
+
+
+def test_launcher_spawns_one_worker_per_gpu_gloo():
+    """`--gpus N` without an external launcher spawns N workers (the bench's own launcher); the
+    gloo replica reduction over them gives frames of all ranks / slowest rank time."""
+    rc, lines, err = _probe(["3"])
+    assert rc == 0, err
+    assert len(lines) == 1                                   # rank 0 only prints
+    assert lines[0]["world"] == 3 and lines[0]["frames"] == 5 + 6 + 7
+    assert lines[0]["t_max"] == pytest.approx(3.0) and lines[0]["value"] == pytest.approx(18 / 3.0)
+
+
+def test_launcher_refuses_mismatched_world():
+    rc, lines, err = _probe(["2"], env={"WORLD_SIZE": "4", "RANK": "0"})
+    assert rc != 0 and not lines and "WORLD_SIZE=4" in err

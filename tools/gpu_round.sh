@@ -6,7 +6,7 @@ set -o pipefail
 TAG=${1:-r01}
 mkdir -p gpurun_out/$TAG
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/$TAG/pytest_gpu.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/$TAG/pytest_gpu.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/$TAG/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$TAG/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; [ $rc -ne 0 ] && exit $rc

@@ -303,6 +303,7 @@ struct TurtleHandle {
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool blaslt = getenv("TURTLE_NO_BLASLT") == nullptr; // hipBLASLt for the plain projections it wins (blas.cpp)
   BlasCtx* blas = nullptr;                            // created on the first bf16 forward
+  bool blas_failed = false;                           // creation failed once: never retried
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
   const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
   const float* fptr(size_t off) const { return reinterpret_cast<const float*>(ptr(off)); }
@@ -528,8 +529,11 @@ static void pack_all(TurtleHandle* h) {
   M.zeros = pk.f32(std::vector<double>(16384, 0.0));
   M.ones = pk.f32(std::vector<double>(8192, 1.0));
   pk.align();
-  if (h->dev) { (void)hipFree(h->dev); h->dev = nullptr; }
-  HIPCHK(hipMalloc(&h->dev, pk.host.size()));
+  // same arch and dtype -> same packed size: repack in place, so device addresses (and launches
+  // captured against them) stay valid across a weight update
+  if (h->dev && h->dev_bytes != pk.host.size()) { (void)hipFree(h->dev); h->dev = nullptr; }
+  if (!h->dev) HIPCHK(hipMalloc(&h->dev, pk.host.size()));
+  else HIPCHK(hipDeviceSynchronize());   // no in-flight forward still reads the old weights
   HIPCHK(hipMemcpy(h->dev, pk.host.data(), pk.host.size(), hipMemcpyHostToDevice));
   h->dev_bytes = pk.host.size();
 }
@@ -665,7 +669,9 @@ struct Runner {
     if (!(K >= 512 || (Mi <= 140000 && g.N >= 256))) return false;
     if (s.ld % 8 || s.off % 8 || g.ldo % 8 || g.offo % 8 || g.ldw % 8 || K % 8 || g.N % 8) return false;
     if (g.res && (g.ldr % 8 || g.offr % 8)) return false;
+    if (h->blas_failed) return false;
     if (!h->blas) h->blas = blas_create();
+    if (!h->blas) { h->blas_failed = true; return false; }
     return blas_ready(h->blas, Mi, g.N, K, s.ld, g.ldw, g.res ? g.ldr : 0, g.ldo, g.res != nullptr, g.bias != nullptr);
   }
   void run_blas(const GemmArgs& g) {
@@ -709,7 +715,9 @@ struct Runner {
       if (w2->N > 128 || w2->N % 16) TFAIL(TURTLE_EINVAL, "fused GEMM2 needs N2 <= 128, N2 % 16 == 0");
       f.w2 = h->ptr(w2->w); f.N2 = w2->N; f.b2 = h->fptr(w2->bias); f.scale2 = h->fptr(w2->scale);
       f.res = res; f.ldr = w2->N; f.offr = 0; f.out = out; f.ldo = w2->N; f.offo = 0;
-      bytes += ES * px * w2->N * (res ? 2 : 1);
+      // algorithmic bytes count each distinct tensor once: the residual of a fused block is its own
+      // input x (already counted), re-read from L2 by the epilogue
+      bytes += ES * px * w2->N * ((res && res != x) ? 2 : 1);
       flops += 2.0 * px * hidden * w2->N;
     } else {
       if (dsts.empty() || dsts.size() > 3) TFAIL(TURTLE_EINVAL, "fused dw-only needs 1..3 destinations");
@@ -982,6 +990,15 @@ struct Runner {
     const int c = b.dim, HW = H * Wd, ch = c / b.heads, ws = b.ws, slot = b.cache_slot;
     const int64_t P = (int64_t)B * HW;
     const int th = H / ws, tw = Wd / ws, N = th * tw, d2 = 2 * c, D = ws * ws * c;
+    // q/k tokens come from a ws x ws stride-ws conv with padding 1: (H + 2 - ws) / ws + 1 per side,
+    // which equals the v token grid H / ws only for ws >= 3. A CHM on an encoder / latent /
+    // refinement level (Scale_patchsize 1 -> ws 2) makes the reference's attn @ v raise
+    // (turtle_t1_arch.py:573-599): refuse it the same way instead of computing something else
+    if ((H + 2 - ws) / ws + 1 != th || (Wd + 2 - ws) / ws + 1 != tw)
+      TFAIL(TURTLE_EINVAL, "SAB q/k token grid " + std::to_string((H + 2 - ws) / ws + 1) + "x" +
+                               std::to_string((Wd + 2 - ws) / ws + 1) + " != v token grid " + std::to_string(th) + "x" +
+                               std::to_string(tw) + " (CHM with window " + std::to_string(ws) +
+                               " cannot run: turtle_t1_arch.py:599 raises)");
     if (N < 5) TFAIL(TURTLE_EINVAL, "selected index k out of range: SAB needs >= 5 tokens (input too small)");
     const int Tin = slot >= 0 ? io->t_in[slot] : 0;
     const int NT = Tin + 1;

@@ -42,6 +42,7 @@ class GraphedTurtle:
         self.out = None
         self.sets = None        # [(k[8], v[8]) for A, B]
         self.t_full = None
+        self._cap = None        # (handle object, weight signature) the graphs were captured against
 
     # ------------------------------------------------------------------------------------------
     def _full(self, kc) -> bool:
@@ -85,6 +86,8 @@ class GraphedTurtle:
 
     def _capture(self):
         m = self.m
+        if m._handle is None or m._sig is None or m._sig != m._signature():
+            m.refresh_weights()
         cdt = m.compute_dtype
         self.t_full = self._t_in(self.kc)
         kind, ks, vs = m.cache_layout(self.B, self.H, self.W, self.t_full)
@@ -116,6 +119,15 @@ class GraphedTurtle:
                     C.c_void_p(ws.data_ptr()), ws.numel(), C.c_void_p(stream)))
             self.graphs.append(g)
         self._ws = ws
+        self._cap = (m._handle, m._sig)
+
+    def _stale(self) -> bool:
+        """The captured launches hold raw pointers into the module's packed weights, its handle and
+        workspace: a new handle (dtype / device change) or changed parameters (load_state_dict,
+        in-place update) invalidate them."""
+        m = self.m
+        return m._handle is not self._cap[0] or m._sig is None or m._sig != self._cap[1] or \
+            m._signature() != self._cap[1]
 
     # ------------------------------------------------------------------------------------------
     @torch.no_grad()
@@ -132,7 +144,17 @@ class GraphedTurtle:
             self.inp.copy_(inp_img_)
             self._capture()
         else:
-            self.inp.copy_(inp_img_)
+            if self._stale():
+                # recapture against the current weights, continuing from the latest history
+                last = self.sets[self.frame % 2]
+                self.kc = [None if t is None else t.clone() for t in last[0]]
+                self.vc = [None if t is None else t.clone() for t in last[1]]
+                self.graphs, self.sets, self.frame = [], None, 0
+                torch.cuda.synchronize(self.dev)
+                self.inp.copy_(inp_img_)
+                self._capture()
+            else:
+                self.inp.copy_(inp_img_)
         d = self.frame % 2
         self.graphs[d].replay()
         self.frame += 1

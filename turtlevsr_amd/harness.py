@@ -89,6 +89,12 @@ def tensor2img(t: torch.Tensor) -> np.ndarray:
     return (x * 255.0).round().astype(np.uint8)
 
 
+def to_uint8_trunc(t: torch.Tensor) -> np.ndarray:
+    """[C, H, W] -> uint8 HWC as the reference's Y-channel branch builds it (inference.py:314,
+    317): `(x * 255.0).permute(1, 2, 0).numpy().astype(np.uint8)`, truncating and unclamped."""
+    return (t.detach().float().cpu() * 255.0).permute(1, 2, 0).numpy().astype(np.uint8)
+
+
 def calc_PSNR(img1: np.ndarray, img2: np.ndarray) -> float:
     """PSNR of two [0, 255] images (inference.py:52-61)."""
     mse = np.mean((img1.astype(np.float64) - img2.astype(np.float64)) ** 2)
@@ -164,8 +170,9 @@ def run_video(frames_lq, frames_gt, model, tile: int | None = None, tile_overlap
             out, k_cache, v_cache = model(x, k_cache, v_cache)
         out = out.squeeze(0)[:, :h, :w]
         if y_channel_PSNR:
-            gy = bgr2ycbcr(tensor2img(gt)[:, :, ::-1])
-            oy = bgr2ycbcr(tensor2img(out)[:, :, ::-1])
+            # inference.py:314-319: (x * 255).astype(uint8) - truncating, no clamp, no rounding
+            gy = bgr2ycbcr(to_uint8_trunc(gt)[:, :, ::-1])
+            oy = bgr2ycbcr(to_uint8_trunc(out)[:, :, ::-1])
             res.psnr.append(calc_PSNR(oy, gy))
             res.ssim.append(ssim_calculate(oy, gy))
         else:

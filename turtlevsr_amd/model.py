@@ -62,6 +62,7 @@ class TurtleHIP(TurtleParams):
         self.padder_size = 32
         self._dtype_name = dtype
         self._handle = None
+        self._handle_dev = None
         self._sig = None
         self._ws = None
         self.set_compute_dtype(dtype)
@@ -90,8 +91,13 @@ class TurtleHIP(TurtleParams):
         dev = next(self.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("TurtleHIP runs on a ROCm device only: call .to('cuda') first")
-        if self._handle is None:
-            self._handle = _Handle(_lib.config_from_arch(self.arch, self.sr, _DT[self._dtype_name][0]))
+        if self._handle is None or self._handle_dev != dev:
+            # a handle's lazily created device state (vendor GEMM workspace, events) lives on the
+            # device it was first used on: a module moved to another device gets a fresh handle
+            with torch.cuda.device(dev):
+                self._handle = _Handle(_lib.config_from_arch(self.arch, self.sr, _DT[self._dtype_name][0]))
+            self._handle_dev = dev
+            self._ws = None
         h = self._handle.h
         with torch.cuda.device(dev):
             for name, t in self.state_dict().items():
@@ -155,6 +161,7 @@ class TurtleHIP(TurtleParams):
                 k_in[i] = kc.detach().to(device=dev, dtype=cdt).contiguous()
                 v_in[i] = vc.detach().to(device=dev, dtype=cdt).contiguous()
         kind, kshape, vshape = self.cache_layout(B, H, W, t_in)
+        self._check_caches(kind, kshape, vshape, t_in, k_cached, v_cached)
         k_out, v_out = [None] * 8, [None] * 8
         for i in range(8):
             if kind[i] == 1:
@@ -180,6 +187,26 @@ class TurtleHIP(TurtleParams):
         # keep inputs alive until the stream has consumed them (caller-owned caches are freed lazily)
         self._keepalive = (inp, k_in, v_in)
         return out, k_out, v_out
+
+    @staticmethod
+    def _check_caches(kind, kshape, vshape, t_in, k_cached, v_cached):
+        """Every incoming cache must have the layout this frame's size and batch imply, up to its
+        temporal extent: the kernels index the caller's buffers with these dimensions (the
+        reference fails in torch.cat on a mismatch, turtle_t1_arch.py:272, 581)."""
+        for i in range(8):
+            kc, vc = k_cached[i], v_cached[i]
+            if kind[i] == 0 or (kc is None and vc is None):
+                continue
+            if kc is None or vc is None:
+                raise ValueError(f"cache slot {i}: k and v must both be given or both be None")
+            if kind[i] == 1:             # FHR [B, heads, rows, P]: rows = t_in
+                want_k = want_v = (kshape[i][0], kshape[i][1], t_in[i], kshape[i][3])
+            else:                        # SAB [B, T, 1, N, d]: T = t_in
+                want_k = (kshape[i][0], t_in[i], kshape[i][2], kshape[i][3], kshape[i][4])
+                want_v = (vshape[i][0], t_in[i], vshape[i][2], vshape[i][3], vshape[i][4])
+            if tuple(kc.shape) != want_k or tuple(vc.shape) != want_v:
+                raise ValueError(f"cache slot {i}: got k {tuple(kc.shape)} / v {tuple(vc.shape)}, expected "
+                                 f"{want_k} / {want_v} for this batch and frame size")
 
     # ---------------------------------------------------------------------------------------
     def set_option(self, name: str, value: int):

@@ -46,3 +46,45 @@ def replica_throughput(elapsed_s: float, frames_local: int, device: torch.device
     dist.all_reduce(n, op=dist.ReduceOp.SUM)
     tmax, frames = float(t.item()), int(n.item())
     return ReplicaResult(frames / tmax, tmax, frames)
+
+
+def check_world(n_gpus: int) -> int | None:
+    """World size this process belongs to. None: no launcher set one (the caller may spawn
+    `n_gpus` workers itself); raises when an external launcher's WORLD_SIZE disagrees with the
+    requested GPU count, so a mismatched launch never reports another configuration's numbers."""
+    import os
+    w = os.environ.get("WORLD_SIZE")
+    if w is None:
+        return None
+    if int(w) != n_gpus:
+        raise SystemExit(f"WORLD_SIZE={w} but --gpus {n_gpus}: launch one process per requested GPU")
+    return int(w)
+
+
+def launch_workers(n: int, argv: list[str], extra_env: dict | None = None, timeout: float | None = None) -> int:
+    """Run `argv` as `n` worker processes, one per GPU (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT set as torch.distributed.run does), and return the worst
+    exit code. Called BEFORE the parent touches the GPU: the workers are children, never an exec
+    of an initialised process. A worker that fails makes the others exit through the process
+    group's own error path; the parent kills whatever is left at `timeout`."""
+    import os
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.update(extra_env or {})
+        procs.append(subprocess.Popen(argv, env=env))
+    rc = 0
+    for p in procs:
+        try:
+            code = p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            code = p.wait()
+        rc = code if rc == 0 else rc
+    return rc
