@@ -195,8 +195,11 @@ struct FusedArgs {                 // fused.hip: [LN ->] pw -> dw3x3 -> [act -> 
   FusedDst dst[3]; int ndst;
   int dbg;                         // tools/fbench ablations (0 in the product path)
   unsigned long long* stamps;      // tools/fbench s_memtime stamps (null in the product path)
+  int up;                          // fused2.hip: 16-channel hidden units per GEMM2 pass (set by its launcher)
 };
 template <typename T> void launch_fused(const FusedArgs& a, hipStream_t st);
+bool fused2_ok(const FusedArgs& a);                               // fused2.hip (bf16 row walk)
+void launch_fused2(const FusedArgs& a, hipStream_t st);
 
 struct PwdwArgs {                  // pwdw.hip: [LN ->] pw (C -> N1) -> dw3x3 [-> gelu(x1)*x2], bf16
   const void* x; int64_t ldx; int offx; int C;   // input pixel-major [nimg][H][W][ldx]

@@ -293,6 +293,7 @@ struct TurtleHandle {
   size_t dev_bytes = 0;
   bool loaded = false;
   bool fuse = getenv("TURTLE_NO_FUSE") == nullptr;   // block-level fused kernels (fused.hip)
+  bool fused2 = true;                                 // bf16 row-walk fused kernels (fused2.hip) where eligible
   bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
   bool gemm_lds = true;                               // LDS-pipelined bf16 GEMM (gemm2.hip)
@@ -728,7 +729,12 @@ struct Runner {
     if (dwp.C != w1.N) TFAIL(TURTLE_EINVAL, "fused: dw width != pointwise width");
     if (C > 128) TFAIL(TURTLE_EINVAL, "fused: input width > 128");
     tag("fused mode=%d nimg=%d H=%d W=%d C=%d N1=%d N2=%d ln=%d ndst=%d", mode, nimg, H, Wd, C, w1.N, f.N2, f.ln, f.ndst);
-    launch(TURTLE_K_FUSED, bytes, flops, [&] { launch_fused<T>(f, st); });
+    const bool rw = ES == 2 && h->fused2 && fused2_ok(f);
+    if (rw) tag("fused2 mode=%d nimg=%d H=%d W=%d C=%d N1=%d N2=%d ln=%d ndst=%d", mode, nimg, H, Wd, C, w1.N, f.N2, f.ln, f.ndst);
+    launch(TURTLE_K_FUSED, bytes, flops, [&] {
+      if (rw) launch_fused2(f, st);
+      else launch_fused<T>(f, st);
+    });
   }
   // fused.hip handles input widths <= 128 in 16-channel slices and 32-deep GEMM2 K steps
   bool can_fuse(int c, int mode, int n1, int hidden) const {
@@ -1307,6 +1313,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "sab_tile") h->sab_tile = value != 0;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
     else if (n == "stem_mfma") h->stem_mfma = value != 0;
+    else if (n == "fused2") h->fused2 = value != 0;
     else TFAIL(TURTLE_EINVAL, "unknown option '" + n + "'");
   });
 }
