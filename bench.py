@@ -214,6 +214,48 @@ def roofline(wprof, wgroups, nwarm, tgroups, steps, dtype):
     return roof
 
 
+def train_bench(args, world, rank, dev):
+    """BASELINE config 5: Turtle GoPro training, B x 5-frame 256x256 clips per GPU, one DDP step
+    (forward over the causal loop, BPTT, RCCL gradient all-reduce, AdamW) per timed step."""
+    from turtlevsr_amd.train import Trainer, TurtleTrain
+    opt = load_opt()
+    net = TurtleTrain(opt)
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(shapes, 0).items()})
+    net = net.to(dev).train()
+    tr = Trainer(net, amp="bf16")
+    B = args.train_batch
+    lq = torch.from_numpy(synthetic_frames((B, 5, 3, 256, 256), clip_seed(rank), name="lq")).to(dev)
+    gt = (lq + 0.05 * torch.from_numpy(synthetic_frames((B, 5, 3, 256, 256), clip_seed(rank), name="gt")).to(dev)).clamp(0, 1)
+    for _ in range(max(args.warmup, 1)):
+        tr.train_step(lq, gt)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    loss = None
+    for _ in range(args.steps):
+        loss = tr.train_step(lq, gt)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    rep = replica_throughput(time.perf_counter() - t0, args.steps * B * 5, dev)
+    line = {
+        "metric": "training frames/sec (Turtle GoPro, 5-frame 256x256 clips, DDP)",
+        "value": round(rep.value, 3), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(rep.t_max / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "bf16", "data": "synthetic clips, synthetic random-init GoPro weights",
+        "config": {"workload": f"Turtle GoPro training, {B} x 5-frame 256x256 clips per GPU, BPTT through the caches, "
+                               "L1, AdamW 4e-4, bf16 autocast", "global_batch": B * world, "seq_len": 5,
+                   "parallelism": f"ddp{world} (RCCL)" if world > 1 else "single GPU"},
+        "loss": loss,
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,6 +270,9 @@ def main():
     ap.add_argument("--no-psnr", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--profile-all", action="store_true", help="print every kernel class's time")
+    ap.add_argument("--train", action="store_true",
+                    help="config 5: one DDP training step per `step` (8 x 5-frame 256x256 clips per GPU, bf16 autocast, AdamW)")
+    ap.add_argument("--train-batch", type=int, default=8)
     args = ap.parse_args()
     if args.graph:
         args.no_roofline = True      # per-launch profiling events cannot live inside a captured graph
@@ -243,6 +288,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    if args.train:
+        return train_bench(args, world, rank, dev)
     h, w = RES[args.res]
     opt = load_opt()
 

@@ -1,0 +1,25 @@
+"""Test infrastructure: the training graph's op set (layer_norm, dwconv3x3, gelu_gate) as plain
+torch ops, so the distributed trainer logic (DDP, BPTT, AdamW, loss reduction) can run in gloo
+processes on CPU. The product op set is turtlevsr_amd.train_ops.HipOps (HIP kernels, no CPU path);
+tests/test_train.py checks both against the reference's own gradients."""
+import torch
+import torch.nn.functional as F
+
+
+class AtenOps:
+    @staticmethod
+    def layer_norm(x, w, b, biasfree):
+        mu = x.mean(dim=1, keepdim=True)
+        var = ((x - mu) ** 2).mean(dim=1, keepdim=True)
+        if biasfree:
+            return x / torch.sqrt(var + 1e-5) * w.view(1, -1, 1, 1)
+        return (x - mu) / torch.sqrt(var + 1e-5) * w.view(1, -1, 1, 1) + b.view(1, -1, 1, 1)
+
+    @staticmethod
+    def dwconv3x3(x, w, b):
+        return F.conv2d(x, w, b, 1, 1, 1, x.shape[1])
+
+    @staticmethod
+    def gelu_gate(x):
+        h = x.shape[1] // 2
+        return F.gelu(x[:, :h]) * x[:, h:]

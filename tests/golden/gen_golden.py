@@ -248,6 +248,39 @@ def gen_blocks(t1):
                            "v0": v0.numpy()}, dict(dim=32, heads=2, ws=4, ntc=3))
 
 
+def gen_train(t1):
+    """Gradients of the training loss of video_restoration_model.py:78-99 on the reference
+    (fp32, CPU): frame-averaged L1 over a causal 4-frame clip with un-detached caches (BPTT), plus
+    the 0 * sum(p) term. Stores the loss and, per parameter, its gradient's checksum + samples
+    (full tensors for a few)."""
+    torch.set_num_threads(8)
+    for name, opt, shape, seed in [("train_tiny", tiny_opt(), (2, 4, 3, 64, 64), 21),
+                                   ("train_tiny_hetero", tiny_opt(**HETERO), (1, 4, 3, 64, 64), 22)]:
+        torch.manual_seed(0)
+        model = t1.make_model(opt).train()
+        fill(model, seed)
+        lq = torch.from_numpy(synthetic_frames(shape, seed, name="lq"))
+        gt = torch.from_numpy(synthetic_frames(shape, seed, name="gt"))
+        kc = vc = None
+        loss = 0
+        for j in range(shape[1]):
+            inp = torch.cat([lq[:, j if j == 0 else j - 1].unsqueeze(1), lq[:, j].unsqueeze(1)], dim=1)
+            out, kc, vc = model(inp, kc, vc)
+            loss = loss + torch.nn.functional.l1_loss(out, gt[:, j])
+        loss = loss / shape[1]
+        total = loss + 0 * sum(p.sum() for p in model.parameters())
+        total.backward()
+        rec = {"loss": np.float64(loss.item())}
+        full = {"input_projection.weight", "ending.weight", "ending.bias", "encoder_level1.transformer_blocks.0.norm1.body.weight"}
+        for k, p in model.named_parameters():
+            g = p.grad if p.grad is not None else torch.zeros_like(p)
+            for sk, sv in summary(g, 64).items():
+                rec[f"g_{k}__{sk}"] = sv
+            if k in full:
+                rec[f"g_{k}"] = g.numpy().astype(np.float32)
+        save(name, rec, dict(opt=arch_opt(opt), seed=seed, shape=list(shape), n_params=len(list(model.parameters()))))
+
+
 def gen_keys(t1, sr):
     res = {}
     for name, mod in (("Turtle_t1", t1), ("TurtleSuper_t1", sr)):
@@ -270,6 +303,8 @@ if __name__ == "__main__":
         gen_blocks(t1)
     if "clips" in which:
         gen_clips(t1, sr)
+    if "train" in which:
+        gen_train(t1)
     named = [w for w in which if w.startswith("clip_")]   # e.g. `gen_golden.py clip_gopro_256`
     if named:
         gen_clips(t1, sr, only=named)

@@ -1,0 +1,202 @@
+"""Training step (BASELINE config 5; video_restoration_model.py:78-108, base_model.py:340-365).
+
+* the differentiable graph (turtlevsr_amd/train.py) against the reference's own gradients
+  (tests/golden/train_*.npz: the reference arch run with autograd on a tiny config, 4-frame BPTT
+  through un-detached caches, frame-averaged L1, 0 * sum(p));
+* DDP over gloo, world_size 2: averaged gradients equal a single process at 2x batch, and the loss
+  after one AdamW step is equal;
+* on the GPU (gpu marker): the same graph on the HIP training kernels (LayerNorm, depthwise 3x3,
+  GELU gate, forward and backward) against the reference gradients, each kernel against torch
+  autograd, and a bf16 step of the GoPro network.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from _aten_ops import AtenOps
+from golden_io import check_summary, load, synth_sd
+from turtlevsr_amd.synthetic import synthetic_frames
+from turtlevsr_amd.train import Trainer, TurtleTrain
+
+
+def _net(meta, ops, dev="cpu"):
+    net = TurtleTrain(meta["opt"], ops=ops)
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    net.load_state_dict(synth_sd(shapes, meta["seed"]), strict=True)
+    return net.to(dev)
+
+
+def _data(meta, dev="cpu"):
+    shape = tuple(meta["shape"])
+    lq = torch.from_numpy(synthetic_frames(shape, meta["seed"], name="lq")).to(dev)
+    gt = torch.from_numpy(synthetic_frames(shape, meta["seed"], name="gt")).to(dev)
+    return lq, gt
+
+
+def _check_grads(net, g, rtol, atol):
+    n = 0
+    for k, p in net.named_parameters():
+        grad = p.grad if p.grad is not None else torch.zeros_like(p)
+        check_summary(g, "g_" + k, grad.detach().float().cpu(), rtol=rtol, atol=atol)
+        if "g_" + k in g:
+            np.testing.assert_allclose(grad.detach().float().cpu().numpy(), g["g_" + k], rtol=rtol, atol=atol, err_msg=k)
+        n += 1
+    return n
+
+
+@pytest.mark.parametrize("name", ["train_tiny", "train_tiny_hetero"])
+def test_graph_gradients_match_reference(name):
+    torch.set_num_threads(8)
+    g, meta = load(name)
+    net = _net(meta, AtenOps)
+    tr = Trainer(net, amp=None)
+    lq, gt = _data(meta)
+    loss = tr.loss(lq, gt)
+    (loss + 0 * sum(p.sum() for p in net.parameters())).backward()
+    assert float(loss.detach()) == pytest.approx(float(g["loss"]), rel=1e-5)
+    assert _check_grads(net, g, rtol=2e-3, atol=2e-6) == meta["n_params"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _ddp_worker(rank, world, port, meta, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        net = _net(meta, AtenOps)
+        tr = Trainer(net, amp=None)
+        lq, gt = _data(meta)                        # [2, T, ...]: rank r takes sample r
+        tr.opt.zero_grad()
+        loss = tr.loss(lq[rank:rank + 1], gt[rank:rank + 1])
+        (loss + 0 * sum(p.sum() for p in net.parameters())).backward()     # DDP all-reduce (mean)
+        grads = {k: p.grad.detach().numpy().copy() for k, p in net.named_parameters()}   # by value
+        tr.opt.step()
+        after = float(tr.loss(lq, gt).detach())     # same batch on every rank after the step
+        red = tr.train_step(lq[rank:rank + 1], gt[rank:rank + 1])
+        q.put((rank, grads, after, red, float(loss.detach())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_ddp_gloo_two_ranks_match_single_process():
+    torch.set_num_threads(8)
+    _, meta = load("train_tiny")
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, meta, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    # single process, the 2-sample batch
+    net = _net(meta, AtenOps)
+    tr = Trainer(net, amp=None)
+    lq, gt = _data(meta)
+    tr.opt.zero_grad()
+    loss = tr.loss(lq, gt)
+    (loss + 0 * sum(p.sum() for p in net.parameters())).backward()
+    for k, p in net.named_parameters():
+        for r in res:
+            np.testing.assert_allclose(r[1][k], p.grad.numpy(), rtol=1e-4, atol=1e-7, err_msg=k)
+    tr.opt.step()
+    after = float(tr.loss(lq, gt).detach())
+    for r in res:
+        assert r[2] == pytest.approx(after, rel=1e-5)
+    # loss reduction of train_step: rank 0 holds the mean over ranks
+    assert res[0][3] == pytest.approx(0.5 * (res[0][4] + res[1][4]), rel=0.2)
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU: the HIP training kernels
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_hip_train_ops_match_autograd(dtype):
+    from turtlevsr_amd.train_ops import HipOps
+    torch.manual_seed(0)
+    dev = "cuda"
+    tol = dict(rtol=1e-4, atol=1e-5) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    for biasfree in (False, True):
+        x = (torch.randn(2, 48, 9, 13, device=dev) * 2 + 0.5).to(dtype).requires_grad_()
+        w = (1 + 0.1 * torch.randn(48, device=dev)).requires_grad_()
+        b = None if biasfree else (0.1 * torch.randn(48, device=dev)).requires_grad_()
+        gy = torch.randn(2, 48, 9, 13, device=dev).to(dtype)
+        y = HipOps.layer_norm(x, w, b, biasfree)
+        gx, gw, *gb = torch.autograd.grad(y, [x, w] + ([b] if b is not None else []), gy)
+        x2 = x.detach().float().requires_grad_()
+        w2 = w.detach().requires_grad_()
+        b2 = None if b is None else b.detach().requires_grad_()
+        y2 = AtenOps.layer_norm(x2, w2, b2, biasfree)
+        rx, rw, *rb = torch.autograd.grad(y2, [x2, w2] + ([b2] if b2 is not None else []), gy.float())
+        torch.testing.assert_close(y.float(), y2, **tol)
+        torch.testing.assert_close(gx.float(), rx, **tol)
+        torch.testing.assert_close(gw, rw, rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
+        if gb:
+            torch.testing.assert_close(gb[0], rb[0], rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
+    x = torch.randn(3, 40, 37, 21, device=dev).to(dtype).requires_grad_()
+    w = (0.3 * torch.randn(40, 1, 3, 3, device=dev)).requires_grad_()
+    b = (0.1 * torch.randn(40, device=dev)).requires_grad_()
+    gy = torch.randn(3, 40, 37, 21, device=dev).to(dtype)
+    y = HipOps.dwconv3x3(x, w, b)
+    gx, gw, gb = torch.autograd.grad(y, [x, w, b], gy)
+    x2, w2, b2 = (t.detach().float().requires_grad_() for t in (x, w, b))
+    y2 = AtenOps.dwconv3x3(x2, w2, b2)
+    rx, rw, rb = torch.autograd.grad(y2, [x2, w2, b2], gy.float())
+    torch.testing.assert_close(y.float(), y2, **tol)
+    torch.testing.assert_close(gx.float(), rx, **tol)
+    torch.testing.assert_close(gw, rw, rtol=tol["rtol"] * 10, atol=tol["atol"] * 300)
+    torch.testing.assert_close(gb, rb, rtol=tol["rtol"] * 10, atol=tol["atol"] * 300)
+    x = torch.randn(2, 64, 11, 7, device=dev).to(dtype).requires_grad_()
+    gy = torch.randn(2, 32, 11, 7, device=dev).to(dtype)
+    y = HipOps.gelu_gate(x)
+    (gx,) = torch.autograd.grad(y, [x], gy)
+    x2 = x.detach().float().requires_grad_()
+    y2 = AtenOps.gelu_gate(x2)
+    (rx,) = torch.autograd.grad(y2, [x2], gy.float())
+    torch.testing.assert_close(y.float(), y2, **tol)
+    torch.testing.assert_close(gx.float(), rx, **tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["train_tiny", "train_tiny_hetero"])
+def test_hip_training_graph_matches_reference_gradients(name):
+    """fp32 on the GPU with the HIP kernels: loss and every parameter gradient vs the reference."""
+    g, meta = load(name)
+    net = _net(meta, None, "cuda")                   # default op set: HipOps
+    tr = Trainer(net, amp=None)
+    lq, gt = _data(meta, "cuda")
+    loss = tr.loss(lq, gt)
+    (loss + 0 * sum(p.sum() for p in net.parameters())).backward()
+    torch.cuda.synchronize()
+    assert float(loss.detach()) == pytest.approx(float(g["loss"]), rel=1e-4)
+    assert _check_grads(net, g, rtol=1e-2, atol=1e-5) == meta["n_params"]
+
+
+@pytest.mark.gpu
+def test_bf16_train_steps_gopro_network():
+    """The GoPro network (59 M params) trains under bf16 autocast on the HIP kernels: 2 x 3-frame
+    128x128 clips, three AdamW steps on a fixed batch lower the loss."""
+    import yaml
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "options",
+                           "Turtle_Deblur_Gopro.yml")) as f:
+        opt = yaml.safe_load(f)
+    net = _net(dict(opt=opt, seed=0), None, "cuda")
+    tr = Trainer(net, amp="bf16", lr=1e-4)
+    lq = torch.from_numpy(synthetic_frames((2, 3, 3, 128, 128), 41, name="lq")).cuda()
+    gt = (lq + 0.05 * torch.from_numpy(synthetic_frames((2, 3, 3, 128, 128), 42, name="gt")).cuda()).clamp(0, 1)
+    losses = [tr.train_step(lq, gt) for _ in range(3)]
+    assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses

@@ -1,0 +1,267 @@
+"""Training step of Turtle (BASELINE config 5): BPTT over the causal frame loop, AdamW, DDP over RCCL.
+
+Restates the reference's training semantics (basicsr/models/video_restoration_model.py:26-108,
+base_model.py:340-365, dist_util.py:15-30) on the GPU:
+
+* ``TurtleTrain`` is the differentiable Turtle_t1 graph over the SAME parameter tree as the
+  inference module (633 keys, turtlevsr_amd/params.py), so checkpoints move between training and
+  the HIP inference path unchanged. Its LayerNorms, depthwise 3x3 convolutions and GELU gates run
+  on hand-written HIP kernels with hand-written backward (``train_ops.HipOps``); pointwise 1x1
+  convolutions, the attention contractions and the SAB top-5 selection are torch ops (hipBLASLt /
+  MIOpen on ROCm), differentiated by autograd.
+* caches are NOT detached between frames: the loss of frame j back-propagates into frames < j
+  through the history state (video_restoration_model.py:85-95);
+* ``Trainer.train_step``: zero_grad -> autocast forward over the T frames -> L1 per frame summed,
+  / T -> ``+ 0 * sum(p.sum())`` (every parameter in the graph, so DDP needs no unused-parameter
+  search, :99) -> (GradScaler for fp16) backward -> AdamW step -> loss reduced to rank 0 (dist.reduce
+  + / world_size, base_model.py:340-365);
+* multi-GPU: one process per GPU, ``torch.nn.parallel.DistributedDataParallel`` over the
+  ``nccl`` backend (RCCL over xGMI on MI355X): the gradient all-reduce is bucketed and overlaps the
+  backward; buckets are sized for xGMI (fewer, larger all-reduces of the 236 MB fp32 gradient).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+
+from .params import TurtleParams
+
+LN_EPS = 1e-5
+L2_EPS = 1e-12
+SAB_TOPK = 5
+SAB_RADIUS = 4
+
+
+def _l2n(x, dim):
+    return x / x.norm(dim=dim, keepdim=True).clamp_min(L2_EPS)
+
+
+def _conv1(m, x):
+    return F.conv2d(x, m.weight, m.bias)
+
+
+class TurtleTrain(TurtleParams):
+    """Differentiable Turtle_t1 (turtle_t1_arch.py:932-1139); ``ops`` supplies layer_norm,
+    dwconv3x3 and gelu_gate (``train_ops.HipOps`` on the GPU)."""
+
+    def __init__(self, opt: dict, ops=None):
+        super().__init__(opt)
+        if self.arch.t0:
+            raise ValueError("training is implemented for the Turtle_t1 network")
+        if ops is None:
+            from .train_ops import HipOps
+            ops = HipOps
+        self.ops = ops
+        self._ball = {}
+
+    # ---- blocks (turtle_t1_arch.py:159-811) ------------------------------------------------------
+    def _ln(self, m, x):
+        return self.ops.layer_norm(x, m.body.weight, getattr(m.body, "bias", None), self.arch.ln_type == "BiasFree")
+
+    def _dw(self, m, x):
+        return self.ops.dwconv3x3(x, m.weight, m.bias)
+
+    def _gffw(self, m, x):                          # GatedFeedForward 159-178
+        return _conv1(m.project_out, self.ops.gelu_gate(self._dw(m.dwconv, _conv1(m.project_in, x))))
+
+    def _ffw(self, m, x):                           # FeedForward 181-210
+        return _conv1(m.conv5, F.gelu(_conv1(m.conv4, x))) * m.gamma
+
+    def _reduced(self, m, x):                       # ReducedAttn 704-742
+        return _conv1(m.conv3, F.gelu(self._dw(m.conv2, _conv1(m.conv1, x)))) * m.beta
+
+    @staticmethod
+    def _heads(t, heads):
+        b, c, h, w = t.shape
+        return t.reshape(b, heads, c // heads, h * w)
+
+    def _chan(self, m, x, heads, kc=None, vc=None, ntc=None):
+        """ChannelAttention 666-702; with caches / ntc: FrameHistoryRouter 218-286."""
+        b, c, h, w = x.shape
+        q, k, v = self._dw(m.qkv_dwconv, _conv1(m.qkv, x)).chunk(3, dim=1)
+        q, k, v = _l2n(self._heads(q, heads), -1), _l2n(self._heads(k, heads), -1), self._heads(v, heads)
+        if kc is not None and vc is not None:
+            k = torch.cat([kc.to(k.dtype), k], dim=2)
+            v = torch.cat([vc.to(v.dtype), v], dim=2)
+        a = torch.softmax(q @ k.transpose(-2, -1) * m.temperature, dim=-1)
+        out = _conv1(m.project_out, (a @ v).reshape(b, c, h, w))
+        if ntc is None:
+            return out, None, None
+        keep = int(ntc * c / heads)
+        return out, k[:, :, -keep:, :], v[:, :, -keep:, :]
+
+    def _ball_mask(self, th, tw, dev, dtype):
+        key = (th, tw, dev, dtype)
+        if key not in self._ball:
+            i = torch.arange(th, device=dev).repeat_interleave(tw)
+            j = torch.arange(tw, device=dev).repeat(th)
+            self._ball[key] = (((i[:, None] - i[None, :]).abs() + (j[:, None] - j[None, :]).abs()) <= SAB_RADIUS).to(dtype)
+        return self._ball[key]
+
+    def _sab(self, m, x, ws, ntc, kc, vc):
+        """StateAlignBlock live forward 548-610 (top-5 394-416, L1 ball 448-464, clipped_softmax 115-132)."""
+        b, c, hl, wl = x.shape
+        qk = self._dw(m.qk_dwconv, _conv1(m.qk, x))
+        q, k = qk[:, :c], qk[:, c:]
+        v = self._dw(m.v_dwconv, _conv1(m.v, x))
+        g = 2 * c
+        k = F.conv2d(_conv1(m.k2, k), m.k2_dwconv.weight, m.k2_dwconv.bias, ws, 1, 1, g)
+        q = F.conv2d(_conv1(m.q2, q), m.q2_dwconv.weight, m.q2_dwconv.bias, ws, 1, 1, g)
+        th, tw = q.shape[2], q.shape[3]
+        hh, ww = hl // ws, wl // ws
+        if th * tw != hh * ww:
+            raise RuntimeError(f"SAB q/k token grid {th}x{tw} != v token grid {hh}x{ww} (turtle_t1_arch.py:599)")
+        n = th * tw
+        q = _l2n(q.reshape(b, g, n).transpose(1, 2).reshape(b, 1, 1, n, g), -1)
+        k = _l2n(k.reshape(b, g, n).transpose(1, 2).reshape(b, 1, 1, n, g), -1)
+        vt = v.reshape(b, c, ws, hh, ws, ww).permute(0, 3, 5, 2, 4, 1).reshape(b, 1, 1, n, ws * ws * c)
+        if kc is not None and vc is not None:
+            k = torch.cat([kc.to(k.dtype), k], dim=1)
+            vt = torch.cat([vc.to(vt.dtype), vt], dim=1)
+        t = k.shape[1]
+        s = (q @ k.transpose(-2, -1)) * m.temperature                   # [b, t, 1, n, n]
+        top = torch.zeros_like(s).scatter_(-1, torch.topk(s, SAB_TOPK, dim=-1).indices, 1.0)
+        s = s * top + s * self._ball_mask(th, tw, s.device, s.dtype)
+        zero = s == 0
+        p = torch.softmax(s.masked_fill(zero, float("-inf")), dim=-1).masked_fill(zero, 0.0)
+        a = p / p.sum(dim=-1, keepdim=True)
+        o = (a @ vt).reshape(b * t, hh, ww, ws, ws, c).permute(0, 5, 3, 1, 4, 2).reshape(b * t, c, hl, wl)
+        o = _conv1(m.project_out, o).reshape(b, t, c, hl, wl)
+        return o, k[:, -ntc:], vt[:, -ntc:]
+
+    def _chm(self, m, x, heads, ws, ntc, kc, vc):
+        """CausalHistoryModel 612-662."""
+        b, c, h, w = x.shape
+        xs, k_keep, v_keep = self._sab(m.spatial_aligner, x, ws, ntc, kc, vc)
+        t = xs.shape[1]
+        kv = self._dw(m.kv_dwconv, _conv1(m.kv, xs.reshape(b * t, c, h, w)))
+        kh, vh = kv[:, :c], kv[:, c:]
+        ch = c // heads
+        kh = kh.reshape(b, t, heads, ch, h * w).transpose(1, 2).reshape(b, heads, t * ch, h * w)
+        vh = vh.reshape(b, t, heads, ch, h * w).transpose(1, 2).reshape(b, heads, t * ch, h * w)
+        out, _, _ = self._chan(m.ChanAttn, x, heads, _l2n(kh, -1), vh, ntc=1)
+        return out, k_keep, v_keep
+
+    def _block(self, spec, m, x, kc=None, vc=None):
+        """TurtleAttnBlock 804-811."""
+        k_out = v_out = None
+        if spec.attn != "NoAttn":
+            y = self._ln(m.norm1, x)
+            if spec.attn == "ReducedAttn":
+                a = self._reduced(m.attn, y)
+            elif spec.attn == "Channel":
+                a, _, _ = self._chan(m.attn, y, spec.heads)
+            elif spec.attn == "FHR":
+                a, k_out, v_out = self._chan(m.attn, y, spec.heads, kc, vc, ntc=spec.ntc)
+            else:
+                a, k_out, v_out = self._chm(m.attn, y, spec.heads, spec.ws, spec.ntc, kc, vc)
+            x = x + a
+        y = self._ln(m.norm2, x)
+        x = x + (self._gffw(m.ffn, y) if spec.ffn == "GFFW" else self._ffw(m.ffn, y))
+        return x, k_out, v_out
+
+    def _level(self, name, x, kc=None, vc=None):    # LevelBlock 856-865
+        specs, mods = self.arch.levels[name].blocks, getattr(self, name).transformer_blocks
+        for s, m in zip(specs[:-1], mods[:-1]):
+            x, _, _ = self._block(s, m, x)
+        return self._block(specs[-1], mods[-1], x, kc, vc)
+
+    def _latent(self, x, k1, v1, k2, v2):          # LatentCacheBlock 919-928
+        specs, mods = self.arch.levels["latent"].blocks, self.latent.transformer_blocks
+        x, k1o, v1o = self._block(specs[0], mods[0], x, k1, v1)
+        for s, m in zip(specs[1:-1], mods[1:-1]):
+            x, _, _ = self._block(s, m, x)
+        x, k2o, v2o = self._block(specs[-1], mods[-1], x, k2, v2)
+        return x, k1o, v1o, k2o, v2o
+
+    def forward(self, inp_img_: torch.Tensor, k_cached: Optional[List] = None, v_cached: Optional[List] = None):
+        """Turtle_t1.forward 1045-1132: [B, 2, C, H, W] -> (out [B, C, H, W], k_list[8], v_list[8])."""
+        b, _, c, h, w = inp_img_.shape
+        if k_cached is None:
+            k_cached, v_cached = [None] * 8, [None] * 8
+        ph, pw = (32 - h % 32) % 32, (32 - w % 32) % 32
+        x5 = F.pad(inp_img_, (0, pw, 0, ph)) if ph or pw else inp_img_
+        current = x5[:, 1]
+        img = torch.cat([x5[:, 0], x5[:, 1]], dim=1) if self.arch.use_both else current
+        ip = self.input_projection
+        e1 = F.conv2d(img.float(), ip.weight, ip.bias, 1, 1)
+        ks, vs = [], []
+        e1, k, v = self._level("encoder_level1", e1, k_cached[0], v_cached[0]); ks.append(k); vs.append(v)
+        down = lambda m, t: F.pixel_unshuffle(F.conv2d(t, m.body[0].weight, None, 1, 1), 2)     # Downsample 136-144
+        up = lambda m, t: F.pixel_shuffle(F.conv2d(t, m.body[0].weight, None, 1, 1), 2)         # Upsample 146-154
+        e2, k, v = self._level("encoder_level2", down(self.down1_2, e1), k_cached[1], v_cached[1]); ks.append(k); vs.append(v)
+        e3, k, v = self._level("encoder_level3", down(self.down2_3, e2), k_cached[2], v_cached[2]); ks.append(k); vs.append(v)
+        lat, k1, v1, k2, v2 = self._latent(down(self.down3_4, e3), k_cached[3], v_cached[3], k_cached[4], v_cached[4])
+        ks += [k1, k2]; vs += [v1, v2]
+        d3 = _conv1(self.reduce_chan_level3, torch.cat([up(self.up4_3, lat), e3], 1))
+        d3, k, v = self._level("decoder_level3", d3, k_cached[5], v_cached[5]); ks.append(k); vs.append(v)
+        d2 = _conv1(self.reduce_chan_level2, torch.cat([up(self.up3_2, d3), e2], 1))
+        d2, k, v = self._level("decoder_level2", d2, k_cached[6], v_cached[6]); ks.append(k); vs.append(v)
+        d1 = _conv1(self.reduce_chan_level1, torch.cat([up(self.up2_1, d2), e1], 1))
+        d1, k, v = self._level("decoder_level1", d1, k_cached[7], v_cached[7]); ks.append(k); vs.append(v)
+        r, _, _ = self._level("refinement", d1)
+        out = F.conv2d(r, self.ending.weight, self.ending.bias, 1, 1) + current
+        return out[:, :, :h, :w], ks, vs
+
+
+class Trainer:
+    """One optimisation step per call, as VideoRestorationModel.optimize_parameters (78-108).
+
+    ``amp``: "bf16" (MI355X default: bf16 autocast, no loss scaling), "fp16" (the reference's
+    autocast + GradScaler) or None (fp32). With an initialised process group the network is wrapped
+    in DistributedDataParallel (RCCL on ROCm) with ``bucket_mb`` gradient buckets."""
+
+    def __init__(self, net: TurtleTrain, lr: float = 4e-4, betas=(0.9, 0.99), weight_decay: float = 0.0,
+                 amp: Optional[str] = "bf16", bucket_mb: int = 64):
+        self.net = net
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        dev = next(net.parameters()).device
+        self.device = dev
+        if self.world > 1:
+            kw = dict(device_ids=[dev.index]) if dev.type == "cuda" else {}
+            self.model = torch.nn.parallel.DistributedDataParallel(
+                net, find_unused_parameters=False, bucket_cap_mb=bucket_mb, gradient_as_bucket_view=True, **kw)
+        else:
+            self.model = net
+        self.opt = torch.optim.AdamW([{"params": [p for p in net.parameters() if p.requires_grad]}], lr=lr, betas=betas,
+                                     weight_decay=weight_decay)
+        self.amp = amp
+        self.scaler = torch.amp.GradScaler("cuda", enabled=(amp == "fp16" and dev.type == "cuda"))
+
+    def _autocast(self):
+        if self.amp is None or self.device.type != "cuda":
+            return torch.autocast(device_type=self.device.type, enabled=False)
+        return torch.autocast(device_type="cuda", dtype=torch.bfloat16 if self.amp == "bf16" else torch.float16)
+
+    def loss(self, lq: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+        """Frame-averaged L1 over the causal loop (video_restoration_model.py:84-98); caches are
+        carried un-detached (BPTT through the history)."""
+        T = lq.shape[1]
+        kc = vc = None
+        total = 0.0
+        with self._autocast():
+            for j in range(T):
+                inp = torch.stack([lq[:, j if j == 0 else j - 1], lq[:, j]], dim=1)
+                out, kc, vc = self.model(inp, kc, vc)
+                total = total + F.l1_loss(out.float(), gt[:, j].float())
+        return total / T
+
+    def train_step(self, lq: torch.Tensor, gt: torch.Tensor) -> float:
+        """One iteration; returns the loss averaged over ranks (valid on rank 0, like
+        reduce_loss_dict)."""
+        self.opt.zero_grad(set_to_none=True)
+        l_pix = self.loss(lq, gt)
+        l_total = l_pix + 0 * sum(p.sum() for p in self.net.parameters())
+        self.scaler.scale(l_total).backward()
+        self.scaler.unscale_(self.opt)
+        self.scaler.step(self.opt)
+        self.scaler.update()
+        red = l_pix.detach().clone()
+        if self.world > 1:                           # base_model.py:340-365: reduce to rank 0, / world
+            dist.reduce(red, dst=0)
+            if dist.get_rank() == 0:
+                red /= self.world
+        return float(red)
