@@ -175,7 +175,7 @@ bool stem_end_mfma_ok(int cin_end, int cin_stem, int cout_stem);   // bf16 matri
 void launch_ending_mfma(const EndArgs& a, hipStream_t st);
 void launch_stem_mfma(const StemArgs& a, hipStream_t st);
 
-enum FusedMode { F_DWONLY = 0, F_GELU = 1, F_GATE = 2 };
+enum FusedMode { F_DWONLY = 0, F_GELU = 1, F_GATE = 2, F_GATEOUT = 3 };   // F_GATEOUT: fused2 only
 struct FusedDst {                  // F_DWONLY output for channels [cbeg, cend)
   void* p; int64_t ld; int off; int cbeg, cend, ccount; int tok_ws; int64_t tok_stride;
 };

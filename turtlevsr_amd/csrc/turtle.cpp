@@ -294,6 +294,7 @@ struct TurtleHandle {
   bool loaded = false;
   bool fuse = getenv("TURTLE_NO_FUSE") == nullptr;   // block-level fused kernels (fused.hip)
   bool fused2 = true;                                 // bf16 row-walk fused kernels (fused2.hip) where eligible
+  bool fused2_wide = false;                           // fused2 at width 256 (level 3): correct, slower than GEMM + dw so far
   bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
   bool gemm_lds = true;                               // LDS-pipelined bf16 GEMM (gemm2.hip)
@@ -724,10 +725,11 @@ struct Runner {
       if (dsts.empty() || dsts.size() > 3) TFAIL(TURTLE_EINVAL, "fused dw-only needs 1..3 destinations");
       for (size_t i = 0; i < dsts.size(); ++i) f.dst[i] = dsts[i];
       f.ndst = (int)dsts.size();
-      bytes += ES * px * w1.N;
+      bytes += ES * px * (mode == F_GATEOUT ? hidden : w1.N);
     }
     if (dwp.C != w1.N) TFAIL(TURTLE_EINVAL, "fused: dw width != pointwise width");
-    if (C > 128) TFAIL(TURTLE_EINVAL, "fused: input width > 128");
+    if ((C > 128 || mode == F_GATEOUT) && !(ES == 2 && h->fused2 && fused2_ok(f)))
+      TFAIL(TURTLE_EINVAL, "fused: input width > 128 needs the bf16 row-walk kernel");
     tag("fused mode=%d nimg=%d H=%d W=%d C=%d N1=%d N2=%d ln=%d ndst=%d", mode, nimg, H, Wd, C, w1.N, f.N2, f.ln, f.ndst);
     const bool rw = ES == 2 && h->fused2 && fused2_ok(f);
     if (rw) tag("fused2 mode=%d nimg=%d H=%d W=%d C=%d N1=%d N2=%d ln=%d ndst=%d", mode, nimg, H, Wd, C, w1.N, f.N2, f.ln, f.ndst);
@@ -735,6 +737,13 @@ struct Runner {
       if (rw) launch_fused2(f, st);
       else launch_fused<T>(f, st);
     });
+  }
+  // fused2.hip at input width 256 (level 3): [LN ->] pw -> dw (qkv, kv) or pw -> dw -> gate
+  // (GatedFeedForward up to project_out), bf16 only
+  bool can_fused2_wide(int c, int mode, int n1, int hidden) const {
+    if (ES != 2 || !h->fuse || !h->fused2 || !h->fused2_wide || c != 256) return false;
+    if (mode == F_GATEOUT) return n1 == 2 * hidden && n1 <= 5 * c && hidden % 16 == 0;
+    return mode == F_DWONLY && n1 % 16 == 0 && n1 <= 3 * c;
   }
   // fused.hip handles input widths <= 128 in 16-channel slices and 32-deep GEMM2 K steps
   bool can_fuse(int c, int mode, int n1, int hidden) const {
@@ -848,6 +857,10 @@ struct Runner {
       if (can_fuse(c, F_GATE, 2 * hd, hd)) {
         fused(F_GATE, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, &bw.f_out, x, xalt, {});
         std::swap(x, xalt);
+      } else if (can_fused2_wide(c, F_GATEOUT, 2 * hd, hd)) {
+        T* t2 = buf(P * hd);
+        fused(F_GATEOUT, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, nullptr, nullptr, nullptr, {dst_map(t2, hd, 0, 0, hd)});
+        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
       } else if (can_pwdw(c, 2 * hd, true)) {
         T* t2 = buf(P * hd);
         pwdw(bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, 1, t2, hd, 0);
@@ -869,7 +882,7 @@ struct Runner {
 
   // LN(x) -> qkv 1x1 -> qkv_dwconv into `out` [P][3c] (fused, or GEMM + dw)
   void qkv_dw(const BlockW& bw, const T* x, int c, T* out, int nimg, int H, int Wd) {
-    if (can_fuse(c, F_DWONLY, 3 * c, 0)) {
+    if (can_fuse(c, F_DWONLY, 3 * c, 0) || can_fused2_wide(c, F_DWONLY, 3 * c, 0)) {
       fused(F_DWONLY, bw.a_in, bw.a_dw, x, c, 0, c, nimg, H, Wd, 3 * c, nullptr, nullptr, nullptr,
             {dst_map(out, 3 * c, 0, 0, 3 * c)});
     } else if (can_pwdw(c, 3 * c, false)) {
@@ -1106,7 +1119,7 @@ struct Runner {
     const int c = b.dim, HW = H * Wd, ch = c / b.heads;
     const int64_t P = (int64_t)B * HW;
     // kv = (W_kv W_po) xs over the B*T aligned frames, then dw3x3 per frame
-    if (can_fuse(c, F_DWONLY, 2 * c, 0)) {
+    if (can_fuse(c, F_DWONLY, 2 * c, 0) || can_fused2_wide(c, F_DWONLY, 2 * c, 0)) {
       fused(F_DWONLY, bw.kv, bw.kv_dw, xs, c, 0, c, B * NT, H, Wd, 2 * c, nullptr, nullptr, nullptr,
             {dst_map(kvd, 2 * c, 0, 0, 2 * c)});
     } else if (can_pwdw(c, 2 * c, false)) {
@@ -1314,6 +1327,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
     else if (n == "stem_mfma") h->stem_mfma = value != 0;
     else if (n == "fused2") h->fused2 = value != 0;
+    else if (n == "fused2_wide") h->fused2_wide = value != 0;
     else TFAIL(TURTLE_EINVAL, "unknown option '" + n + "'");
   });
 }
