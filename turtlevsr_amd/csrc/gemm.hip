@@ -556,6 +556,15 @@ static void launch_cfg(const GemmArgs& g, hipStream_t st) {
 template <typename T>
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
+    // measured per shape class (tools/kbench, MI355X): the 2-D tiled kernel for the resampling 3x3
+    // convolutions and K >= 640 (incl. the five-source W_eff GEMM), the A-resident kernel for the
+    // K = 256 residual projections, else the persistent panel kernel
+    const int K = g.a.Ktot;
+    if (((g.conv3 && g.N >= 256) || (!g.conv3 && K >= 640) || (!g.ln && K == 512 && g.N >= 512)) && gemm_kt_ok(g)) {
+      launch_gemm_kt(g, st);
+      return;
+    }
+    if (K == 256 && g.res && gemm_ar_ok(g)) { launch_gemm_ar(g, st); return; }
     if (gemm_pn_ok(g)) { launch_gemm_pn(g, st); return; }
     if (gemm_lds_ok(g)) { launch_gemm_lds(g, st); return; }
     if (panel_ok(g)) { launch_panel_any(g, st); return; }

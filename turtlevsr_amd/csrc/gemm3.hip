@@ -422,4 +422,240 @@ void launch_gemm_pn(const GemmArgs& g, hipStream_t st) {
   }
 }
 
+
+// ============================================================================================
+// "ar" kernel: A-resident, one panel per block (not persistent). For the projections where the
+// persistent pn kernel cannot amortise its start-up or does not fit two panels: the latent level
+// (M = 32640 pixels: two panels per CU in all) and K = 640 / 1280 (L3 GFFW project_out, latent
+// project_out, the CHM / FHR five-source W_eff GEMM). Measured against hipBLASLt in tools/kbench.
+//   * a 256-thread block owns a BM-pixel panel; the whole BM x K panel goes HBM -> LDS by LDS-DMA
+//     in one burst (<= 80 KB, XOR-swizzled chunks as in pn), so two blocks share a CU and one
+//     block's MFMA sweep overlaps the other's panel load;
+//   * the block then sweeps all N output channels in passes of 4 x CPW: each wave owns CPW
+//     channels x all BM pixels, W fragments stream from L2 through a register ring D K-steps deep
+//     that wraps into the next pass; the pass's residual and epilogue vectors are in flight across
+//     its K loop;
+//   * same permuted W rows as pn (lane = 8 consecutive channels of one pixel): epilogue
+//     acc + (W.b_ln + bias) (+ residual), one 16-byte store per lane, pixel row and 32 channels;
+//   * LayerNorm (single source): statistics and normalisation of the panel rows in LDS, as pn.
+// Eligible: bf16, NHWC store, no 3x3 / GELU / scale, K in {256, 512, 640, 1280}, N % (4 CPW) == 0.
+// ============================================================================================
+template <int BM, int KP, int NTW, bool RES>
+__global__ __launch_bounds__(256, 2) void gemm_ar_kernel(GemmArgs g) {
+  constexpr int CPR = KP / 8, KS = KP / 32, MT = BM / 16, CPW = NTW * 16, CPP = 4 * CPW, NG = NTW / 2;
+  constexpr int PANEL = BM * KP * 2, NDMA = PANEL / 4096, TPR = 256 / BM;
+  constexpr int D = 4;
+  static_assert(PANEL % 4096 == 0 && KS % D == 0 && NTW % 2 == 0 && MT >= 1 && (CPR < 16 || CPR % 16 == 0) &&
+                    CPR % TPR == 0, "ar geometry");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const PnPanel P = pn_panel<BM>(g, blockIdx.x);
+  const int rmax = (int)(P.mlim - P.m0) - 1;
+
+  // ---- the panel: LDS chunk q = row q / CPR, position q % CPR, holding k-chunk pos ^ swz(row);
+  // rows past the end of M repeat the last row. Source of a chunk by a select scan (<= 5 sources).
+#pragma unroll
+  for (int i = 0; i < NDMA; ++i) {
+    const int q = (i * 4 + wid) * 64 + lane, lr = q / CPR, r = min(lr, rmax);
+    const int k = ((q % CPR) ^ pn_swz<CPR>(lr)) * 8;
+    const bf16* base = reinterpret_cast<const bf16*>(g.a.s[0].base) + g.a.s[0].off;
+    int64_t ld = g.a.s[0].ld;
+    int smul = g.a.s[0].img_mul, sadd = g.a.s[0].img_add, kb = 0, kbj = g.a.s[0].K;
+#pragma unroll
+    for (int s = 1; s < TURTLE_MAX_SRC; ++s) {
+      const bool hit = s < g.a.n && k >= kbj;
+      base = hit ? reinterpret_cast<const bf16*>(g.a.s[s].base) + g.a.s[s].off : base;
+      ld = hit ? g.a.s[s].ld : ld;
+      smul = hit ? g.a.s[s].img_mul : smul;
+      sadd = hit ? g.a.s[s].img_add : sadd;
+      kb = hit ? kbj : kb;
+      kbj += s < g.a.n ? g.a.s[s].K : 0;
+    }
+    int pp = P.p0 + r, img = P.img0;
+    if (pp >= g.HW) { pp -= g.HW; ++img; }
+    pn_dma16(base + ((int64_t)(img * smul + sadd) * g.HW + pp) * ld + (k - kb), lds_base + (i * 4 + wid) * 1024);
+  }
+  pn_vmwait<0>();
+  __syncthreads();
+
+  if (g.ln) {   // LayerNorm of the panel rows in place (TPR threads per row), as pn
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 one2 = __builtin_bit_cast(bf16x2, 0x3F803F80u);
+    constexpr int CH = CPR / TPR;
+    const int lr = tid / TPR, lh = tid % TPR;
+    char* row = smem + lr * (KP * 2);
+    uint4 xs[CH];
+    float ls = 0.f, lq = 0.f;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      xs[j] = *reinterpret_cast<const uint4*>(row + (lh * CH + ((j + lr * TPR + lh) % CH)) * 16);
+      const uint32_t w[4] = {xs[j].x, xs[j].y, xs[j].z, xs[j].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16x2 v2 = __builtin_bit_cast(bf16x2, w[e]);
+        ls = __builtin_amdgcn_fdot2_f32_bf16(v2, one2, ls, false);
+        lq = __builtin_amdgcn_fdot2_f32_bf16(v2, v2, lq, false);
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) { ls += __shfl_xor(ls, o, 64); lq += __shfl_xor(lq, o, 64); }
+    const float mu = ls / KP, rs = rsqrtf(fmaxf(lq / KP - mu * mu, 0.f) + 1e-5f), nm = g.ln_s ? -mu * rs : 0.f;
+#pragma unroll
+    for (int j = 0; j < CH; ++j) {
+      const uint32_t w[4] = {xs[j].x, xs[j].y, xs[j].z, xs[j].w};
+      uint32_t o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float a = fmaf(__uint_as_float(w[e] << 16), rs, nm), b = fmaf(__uint_as_float(w[e] & 0xffff0000u), rs, nm);
+        typedef __bf16 bf2 __attribute__((ext_vector_type(2)));
+        o[e] = __builtin_bit_cast(uint32_t, bf2{(bf16)a, (bf16)b});
+      }
+      *reinterpret_cast<uint4*>(row + (lh * CH + ((j + lr * TPR + lh) % CH)) * 16) = uint4{o[0], o[1], o[2], o[3]};
+    }
+    __syncthreads();
+  }
+
+  // lane's W row of n-tile t: channel pass * CPP + wid * CPW + 32 (t / 2) + 8 (fr / 4) + 4 (t % 2) + fr % 4
+  const int64_t ldw = g.ldw;
+  const bf16* wl = P.w + (int64_t)(wid * CPW + (fr >> 2) * 8 + (fr & 3)) * ldw + fq * 8;
+  bf16x8 wb[D][NTW];
+  auto load_w = [&](const bf16* wp, int kstep, int slot) {
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+      wb[slot][t] = *reinterpret_cast<const bf16x8*>(wp + (int64_t)((t >> 1) * 32 + (t & 1) * 4) * ldw + kstep * 32);
+  };
+  const int npass = g.N / CPP;
+#pragma unroll
+  for (int j = 0; j < D; ++j) load_w(wl, j, j);
+  const bf16* prb = RES ? reinterpret_cast<const bf16*>(g.res) + P.m0 * g.ldr + g.offr : nullptr;
+  bf16* pob = reinterpret_cast<bf16*>(g.out) + P.m0 * g.ldo + g.offo;
+  const float* vt = g.ln_t ? g.ln_t : g.zeros;
+  const float* vb = g.bias ? g.bias : g.zeros;
+
+  for (int pass = 0; pass < npass; ++pass) {
+    const bf16* wcur = wl + (int64_t)pass * CPP * ldw;
+    const bf16* wnx = pass + 1 < npass ? wcur + (int64_t)CPP * ldw : wcur;
+    const int cb = pass * CPP + wid * CPW + fq * 8;   // + 32 j: the lane's 8 consecutive channels of group j
+    u32x4 rv[RES ? MT : 1][NG];
+    if constexpr (RES) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < NG; ++j)
+          rv[mt][j] = *reinterpret_cast<const u32x4*>(prb + (min(mt * 16 + fr, rmax) * (int)g.ldr + cb + 32 * j));
+    }
+    f32x4 tb[NG][2];
+#pragma unroll
+    for (int j = 0; j < NG; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(vt + cb + 32 * j + 4 * h);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(vb + cb + 32 * j + 4 * h);
+        tb[j][h] = a + b;
+      }
+    f32x4 acc[MT][NTW];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) acc[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 xf[MT];
+    auto read_x = [&](int ks, int mt) {
+      const int r = mt * 16 + fr;
+      const int c = (ks * 4 + fq) ^ pn_swz<CPR>(r);
+      xf[mt] = *reinterpret_cast<const bf16x8*>(smem + r * (KP * 2) + c * 16);
+    };
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) read_x(0, mt);
+    static_for<KS>([&](auto ksc) {
+      constexpr int ks = decltype(ksc)::value;
+      constexpr int slot = ks % D;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+        for (int t = 0; t < NTW; ++t) acc[mt][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[slot][t], xf[mt], acc[mt][t], 0, 0, 0);
+        if constexpr (ks + 1 < KS) read_x(ks + 1, mt);
+      }
+      if constexpr (ks + D < KS) load_w(wcur, ks + D, slot);
+      else load_w(wnx, ks + D - KS, slot);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < NG; ++j) {
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = acc[mt][2 * j + (e >> 2)][e & 3] + tb[j][e >> 2][e & 3];
+        if constexpr (RES) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] += __uint_as_float(rv[mt][j][e] << 16);
+            v[2 * e + 1] += __uint_as_float(rv[mt][j][e] & 0xffff0000u);
+          }
+        }
+        bf16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
+        pn_gstore(pob + (min(mt * 16 + fr, rmax) * (int)g.ldo + cb + 32 * j), o);
+      }
+  }
+  pn_vmwait<0>();
+}
+
+struct ArCfg { int bm, ntw; };
+static ArCfg ar_cfg(int K) {
+  switch (K) {
+    case 256: return {128, 2};
+    case 512: return {64, 4};
+    case 640: return {64, 4};
+    case 1280: return {32, 4};
+    default: return {0, 0};
+  }
+}
+
+bool gemm_ar_ok(const GemmArgs& g) {
+  if (!g.allow_ar || g.conv3 || g.store_mode != STORE_NHWC || g.gelu || g.scale) return false;
+  const ArCfg c = ar_cfg(g.a.Ktot);
+  if (!c.bm || g.N % (64 * c.ntw) || g.N > 8192) return false;
+  if (g.ldw % 8 || g.ldo % 8 || g.offo % 8) return false;
+  if (c.bm * g.ldo >= ((int64_t)1 << 31) || g.M >= ((int64_t)1 << 31) - 1024) return false;
+  if (g.res && (g.ldr % 8 || g.offr % 8 || c.bm * g.ldr >= ((int64_t)1 << 31))) return false;
+  if (g.HW < c.bm) return false;                    // a panel spans at most two images
+  if (g.ln && g.a.n != 1) return false;
+  int kb = 0;
+  for (int j = 0; j < g.a.n; ++j) {
+    const SrcDesc& s = g.a.s[j];
+    if (s.K % 8 || s.ld % 8 || s.off % 8 || reinterpret_cast<uintptr_t>(s.base) % 16) return false;
+    kb += s.K;
+  }
+  return kb == g.a.Ktot && reinterpret_cast<uintptr_t>(g.out) % 16 == 0 && reinterpret_cast<uintptr_t>(g.w) % 16 == 0 &&
+         (!g.res || reinterpret_cast<uintptr_t>(g.res) % 16 == 0);
+}
+
+template <int BM, int KP, int NTW>
+static void launch_ar(const GemmArgs& g, hipStream_t st) {
+  const int64_t np = g.wstride ? (g.M / g.HW) * ((g.HW + BM - 1) / BM) : (g.M + BM - 1) / BM;
+  constexpr size_t lds = (size_t)BM * KP * 2;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_ar_kernel<BM, KP, NTW, true>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_ar_kernel<BM, KP, NTW, false>), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  auto kern = g.res ? gemm_ar_kernel<BM, KP, NTW, true> : gemm_ar_kernel<BM, KP, NTW, false>;
+  hipLaunchKernelGGL(kern, dim3((unsigned)np), dim3(256), lds, st, g);
+}
+
+void launch_gemm_ar(const GemmArgs& g, hipStream_t st) {
+  switch (g.a.Ktot) {
+    case 256: launch_ar<128, 256, 2>(g, st); break;
+    case 512: launch_ar<64, 512, 4>(g, st); break;
+    case 640: launch_ar<64, 640, 4>(g, st); break;
+    default: launch_ar<32, 1280, 4>(g, st); break;
+  }
+}
+
 }  // namespace turtle

@@ -33,6 +33,8 @@ struct GemmArgs {
   int allow_panel;                 // panel kernel permitted (turtle_set_option "panel_gemm")
   int allow_lds;                   // LDS-pipelined kernel permitted (turtle_set_option "gemm_lds")
   int allow_pn;                    // resident-panel kernel permitted (turtle_set_option "gemm_pn")
+  int allow_ar;                    // A-resident per-panel kernel permitted (turtle_set_option "gemm_ar")
+  int allow_kt;                    // 2-D tiled deep-ring kernel permitted (turtle_set_option "gemm_kt")
   int dbg;                         // tools/kbench ablations of the pn kernel (0 in the product path)
   unsigned long long* stamps;      // tools/kbench s_memtime stamps of the pn kernel (null in the product path)
 };
@@ -41,6 +43,10 @@ bool gemm_lds_ok(const GemmArgs& g);                              // gemm2.hip (
 void launch_gemm_lds(const GemmArgs& g, hipStream_t st);
 bool gemm_pn_ok(const GemmArgs& g);                               // gemm3.hip (bf16)
 void launch_gemm_pn(const GemmArgs& g, hipStream_t st);
+bool gemm_ar_ok(const GemmArgs& g);                               // gemm3.hip (bf16)
+void launch_gemm_ar(const GemmArgs& g, hipStream_t st);
+bool gemm_kt_ok(const GemmArgs& g);                               // gemm5.hip (bf16)
+void launch_gemm_kt(const GemmArgs& g, hipStream_t st);
 
 enum DwMode { DW_PLAIN = 0, DW_GELU = 1, DW_GATE = 2 };
 struct DwArgs {

@@ -299,6 +299,8 @@ struct TurtleHandle {
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
   bool gemm_lds = true;                               // LDS-pipelined bf16 GEMM (gemm2.hip)
   bool gemm_pn = true;                                // resident-panel bf16 GEMM, K <= 512 (gemm3.hip)
+  bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
+  bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
   bool sab_tile = false;                              // query-tiled VALU SAB gather (sab.hip)
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
@@ -632,6 +634,7 @@ struct Runner {
     g.res = res; g.ldr = ldr; g.offr = offr;
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store;
     g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel; g.allow_lds = h->gemm_lds; g.allow_pn = h->gemm_pn;
+    g.allow_ar = h->gemm_ar; g.allow_kt = h->gemm_kt;
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
     // algorithmic traffic: A once (a 3x3 reads each input pixel once), W per weight set, out
     // (+ residual) once
@@ -1322,6 +1325,8 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "blaslt") h->blaslt = value != 0;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
+    else if (n == "gemm_ar") h->gemm_ar = value != 0;
+    else if (n == "gemm_kt") h->gemm_kt = value != 0;
     else if (n == "pwdw") h->pwdw = value != 0;
     else if (n == "sab_tile") h->sab_tile = value != 0;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
