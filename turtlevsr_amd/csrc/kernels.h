@@ -83,9 +83,10 @@ struct SabScoreArgs {
   float* topv;                     // [B*T][nsplit][N][5]
   int* topi;
   float* ballv;                    // [B*T][N][41] scores of the L1-ball keys (|di|+|dj| <= 4)
+  int dbg;                         // tools/sabbench ablations (0 in the product path)
 };
 template <typename T> void launch_sab_score(const SabScoreArgs& a, hipStream_t st);
-int sab_score_nsplit(int B, int T, int N);
+int sab_score_nsplit(int B, int T, int N, int d);
 
 constexpr int SAB_MAXC = 48;       // candidate slots per query (41 ball + 5 top-k, padded)
 struct SabPrepArgs {               // candidates + clipped softmax per (b, t, query)

@@ -38,6 +38,19 @@ struct Top5 {
     for (int k = 0; k < SAB_K; ++k) { v[k] = -INFINITY; i[k] = 0x7fffffff; }
   }
   TURTLE_DEV static bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia < ib); }
+  // branch-free insert (no-op unless x beats the 5th entry): one compare per slot and a shift
+  TURTLE_DEV void insert_nb(float x, int ix) {
+    bool c[SAB_K];
+#pragma unroll
+    for (int k = 0; k < SAB_K; ++k) c[k] = better(x, ix, v[k], i[k]);
+#pragma unroll
+    for (int k = SAB_K - 1; k >= 1; --k) {
+      v[k] = c[k - 1] ? v[k - 1] : (c[k] ? x : v[k]);
+      i[k] = c[k - 1] ? i[k - 1] : (c[k] ? ix : i[k]);
+    }
+    v[0] = c[0] ? x : v[0];
+    i[0] = c[0] ? ix : i[0];
+  }
   TURTLE_DEV void insert(float x, int ix) {
     if (!better(x, ix, v[SAB_K - 1], i[SAB_K - 1])) return;
     v[SAB_K - 1] = x; i[SAB_K - 1] = ix;
@@ -68,6 +81,38 @@ TURTLE_DEV void ball_offset(int slot, int& di, int& dj) {
   dj = c - (4 - (di < 0 ? -di : di));
 }
 
+// v[j] for a per-lane j < NS by a select tree on the bits of j. The selects are v_cndmask from
+// inline asm on a lane mask: written as C selects, hipcc turns the tree into a stack copy of v plus
+// an indexed scratch load.
+TURTLE_DEV float sel_lanes(uint64_t m, float f, float t) {   // lane bit set: t, else f
+  float r;
+  asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+  return r;
+}
+template <int NS>
+TURTLE_DEV float pick(const float (&v)[NS], int j) {
+  static_assert(NS == 8 || NS == 16, "pick width");
+  float h8[8], h4[4], h2[2];
+  int b = 0;
+  if constexpr (NS == 16) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(j & 1);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h8[k] = sel_lanes(m, v[2 * k], v[2 * k + 1]);
+    b = 1;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h8[k] = v[k];
+  }
+  const uint64_t m1 = __builtin_amdgcn_ballot_w64((j >> b) & 1);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) h4[k] = sel_lanes(m1, h8[2 * k], h8[2 * k + 1]);
+  const uint64_t m2 = __builtin_amdgcn_ballot_w64((j >> (b + 1)) & 1);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) h2[k] = sel_lanes(m2, h4[2 * k], h4[2 * k + 1]);
+  const uint64_t m3 = __builtin_amdgcn_ballot_w64((j >> (b + 2)) & 1);
+  return sel_lanes(m3, h2[0], h2[1]);
+}
+
 // exact m / tw for 0 <= m < 2^24 (float reciprocal + one correction each way)
 TURTLE_DEV int div_tw(int m, int tw, float inv) {
   int r = (int)((float)m * inv);
@@ -77,21 +122,22 @@ TURTLE_DEV int div_tw(int m, int tw, float inv) {
 }
 
 // ------------------------------------------------------------------------------------------
-// scores + top-5 + ball scores. Block = 64 queries (16 per wave) x one key range; key tiles of KT
-// rows are staged in a 2-slot LDS ring (register staging, one barrier per tile)
+// scores + top-5 + ball scores. Block = QG x 64 queries (QG groups of 16 per wave) x one key range;
+// key tiles of KT rows are staged in a 2-slot LDS ring (register staging, one barrier per tile).
+// QG = 2 would let every staged key fragment feed two query groups (half the L2 -> LDS key traffic).
 // ------------------------------------------------------------------------------------------
-template <typename T, int KT, int QK>
+template <typename T, int KT, int QK, int QG>
 __global__ __launch_bounds__(256) void sab_score_kernel(SabScoreArgs a) {
   using FR = typename Frag<T>::type;
-  constexpr int KF = Frag<T>::K, VEC = Vec<T>::N, ES = sizeof(T), MT = KT / 16;
+  constexpr int KF = Frag<T>::K, VEC = Vec<T>::N, ES = sizeof(T), MT = KT / 16, QB = 64 * QG;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ROW = a.d * ES + 16;
   char* sK0 = smem;
   char* sK1 = smem + KT * ROW;
-  float* mv = reinterpret_cast<float*>(smem + 2 * KT * ROW);   // [64][4][5]
-  int* mi = reinterpret_cast<int*>(mv + 64 * 4 * SAB_K);
+  float* mv = reinterpret_cast<float*>(smem + 2 * KT * ROW);   // [QB][4][5]
+  int* mi = reinterpret_cast<int*>(mv + QB * 4 * SAB_K);
 
-  const int nqt = (a.N + 63) / 64;
+  const int nqt = (a.N + QB - 1) / QB;
   int bid = blockIdx.x;
   const int ks = bid % a.nsplit;
   bid /= a.nsplit;
@@ -109,20 +155,27 @@ __global__ __launch_bounds__(256) void sab_score_kernel(SabScoreArgs a) {
   k += (int64_t)b * kbs;
   const float tau = *a.tau;
   const int d = a.d, nk = d / KF, N = a.N;
+  const float inv_tw = 1.f / (float)a.tw;
 
-  // this lane's query (B operand rows) and its fragments for every K step
-  const int nq = qt * 64 + wid * 16 + (lane & 15);
-  const bool qok = nq < N;
-  FR qf[QK];
-  {
-    const T* qr = q + (int64_t)min(nq, N - 1) * d;
+  // this lane's queries (B operand rows, one per group) and their fragments for every K step
+  FR qf[QG][QK];
+  int nqc[QG], nrow[QG], ncol[QG];
+  bool qok[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) {
+    const int nq = qt * QB + (wid * QG + g) * 16 + (lane & 15);
+    qok[g] = nq < N;
+    nqc[g] = min(nq, N - 1);
+    nrow[g] = div_tw(nqc[g], a.tw, inv_tw);
+    ncol[g] = nqc[g] - nrow[g] * a.tw;
+    const T* qr = q + (int64_t)nqc[g] * d;
 #pragma unroll
     for (int kk = 0; kk < QK; ++kk) {
       if constexpr (sizeof(T) == 2) {
         const int e = min(kk * KF + (lane >> 4) * 8, d - 8);
-        qf[kk] = __builtin_bit_cast(bf16x8, ld16(qr + e));
+        qf[g][kk] = __builtin_bit_cast(bf16x8, ld16(qr + e));
       } else {
-        qf[kk] = ld4f(qr + min(kk * KF + (lane >> 4), d - 1));
+        qf[g][kk] = ld4f(qr + min(kk * KF + (lane >> 4), d - 1));
       }
     }
   }
@@ -154,12 +207,11 @@ __global__ __launch_bounds__(256) void sab_score_kernel(SabScoreArgs a) {
   };
 
   // ball band of this block's queries (token rows), scalar
-  const float inv_tw = 1.f / (float)a.tw;
-  const int qrow_lo = (qt * 64) / a.tw, qrow_hi = min(qt * 64 + 63, N - 1) / a.tw;
-  const int nrow = div_tw(min(nq, N - 1), a.tw, inv_tw), ncol = min(nq, N - 1) - nrow * a.tw;
-  float* ballq = a.ballv + ((int64_t)bt * N + min(nq, N - 1)) * BALL;
+  const int qrow_lo = (qt * QB) / a.tw, qrow_hi = min(qt * QB + QB - 1, N - 1) / a.tw;
 
-  Top5 top; top.init();
+  Top5 top[QG];
+#pragma unroll
+  for (int g = 0; g < QG; ++g) top[g].init();
   if (tb < te) {
     load_tile(tb);
     store_tile(sK0);
@@ -168,45 +220,85 @@ __global__ __launch_bounds__(256) void sab_score_kernel(SabScoreArgs a) {
   __syncthreads();
   for (int it = tb; it < te; ++it) {
     const char* sK = ((it - tb) & 1) ? sK1 : sK0;
-    f32x4 acc[MT];
+    f32x4 acc[QG][MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int g = 0; g < QG; ++g)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[g][mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kk = 0; kk < QK; ++kk) {
-      if (kk < nk) {
+      if (kk < nk && !(a.dbg & 4)) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma(frag_at<T>(sK + mt * 16 * ROW, ROW, kk * KF, lane), qf[kk], acc[mt]);
+        for (int mt = 0; mt < MT; ++mt) {
+          const FR kf = frag_at<T>(sK + mt * 16 * ROW, ROW, kk * KF, lane);
+#pragma unroll
+          for (int g = 0; g < QG; ++g) acc[g][mt] = mfma(kf, qf[g][kk], acc[g][mt]);
+        }
       }
     }
     // next tile into the other slot (its last readers passed the previous barrier), then refill
     if (it + 1 < te) store_tile(((it - tb) & 1) ? sK0 : sK1);
     if (it + 2 < te) load_tile(it + 2);
-    // lane: query nq; keys it*KT + mt*16 + 4(l>>4) + r
+    // lane: query of group g; keys it*KT + mt*16 + 4(l>>4) + r
     const int m0 = it * KT;
     const int krow_lo = m0 / a.tw, krow_hi = min(m0 + KT - 1, N - 1) / a.tw;
-    const bool band = krow_hi >= qrow_lo - 4 && krow_lo <= qrow_hi + 4;
+    const bool band = krow_hi >= qrow_lo - 4 && krow_lo <= qrow_hi + 4 && !(a.dbg & 2);
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+    for (int g = 0; g < QG; ++g) {
+      // top-5: a cheap filter over the whole tile, then the candidates popped one per iteration
+      // (the wave iterates max-popcount times: a few once the lists have warmed up). The 4 lanes
+      // of a query (l, l^16, l^32, l^48) keep lists over disjoint key subsets; the query's final
+      // 5th score is >= each list's 5th, so the largest of the four filters all of them. The
+      // filter (>=) is a superset of the exact test with the index tie-break.
+      float thr = top[g].v[SAB_K - 1];
+      thr = fmaxf(thr, __shfl_xor(thr, 16, 64));
+      thr = fmaxf(thr, __shfl_xor(thr, 32, 64));
+      unsigned cand = 0;
+      float sv[MT * 4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + mt * 16 + (lane >> 4) * 4 + r;
-        const float s = acc[mt][r] * tau;
-        if (m < N) top.insert(s, m);
-        if (band && qok && m < N) {
-          const int mrow = div_tw(m, a.tw, inv_tw), mcol = m - mrow * a.tw;
-          const int di = mrow - nrow, dj = mcol - ncol;
-          if ((di < 0 ? -di : di) + (dj < 0 ? -dj : dj) <= 4) ballq[ball_slot(di, dj)] = s;
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + mt * 16 + (lane >> 4) * 4 + r;
+          sv[mt * 4 + r] = acc[g][mt][r] * tau;
+          cand |= (sv[mt * 4 + r] >= thr && m < N) ? 1u << (mt * 4 + r) : 0u;
         }
+      if (a.dbg & 1) cand = 0;
+      while (cand) {
+        const int j = __builtin_ctz(cand);
+        cand &= cand - 1;
+        top[g].insert_nb(pick<MT * 4>(sv, j), m0 + (j >> 2) * 16 + (lane >> 4) * 4 + (j & 3));
       }
+      if (band && qok[g]) {
+        float* ballq = a.ballv + ((int64_t)bt * N + nqc[g]) * BALL;
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + mt * 16 + (lane >> 4) * 4 + r;
+            if (m < N) {
+              const int mrow = div_tw(m, a.tw, inv_tw), mcol = m - mrow * a.tw;
+              const int di = mrow - nrow[g], dj = mcol - ncol[g];
+              if ((di < 0 ? -di : di) + (dj < 0 ? -dj : dj) <= 4) ballq[ball_slot(di, dj)] = sv[mt * 4 + r];
+            }
+          }
+      }
+    }
     __syncthreads();
   }
   // merge the 4 lane groups' lists of each query
-  const int ql = wid * 16 + (lane & 15);
 #pragma unroll
-  for (int x = 0; x < SAB_K; ++x) { mv[(ql * 4 + (lane >> 4)) * SAB_K + x] = top.v[x]; mi[(ql * 4 + (lane >> 4)) * SAB_K + x] = top.i[x]; }
+  for (int g = 0; g < QG; ++g) {
+    const int ql = (wid * QG + g) * 16 + (lane & 15);
+#pragma unroll
+    for (int x = 0; x < SAB_K; ++x) {
+      mv[(ql * 4 + (lane >> 4)) * SAB_K + x] = top[g].v[x];
+      mi[(ql * 4 + (lane >> 4)) * SAB_K + x] = top[g].i[x];
+    }
+  }
   __syncthreads();
-  if (tid < 64) {
-    const int n = qt * 64 + tid;
+  if (tid < QB) {
+    const int n = qt * QB + tid;
     Top5 m; m.init();
     for (int g = 0; g < 4; ++g)
       for (int x = 0; x < SAB_K; ++x) m.insert(mv[(tid * 4 + g) * SAB_K + x], mi[(tid * 4 + g) * SAB_K + x]);
@@ -217,33 +309,41 @@ __global__ __launch_bounds__(256) void sab_score_kernel(SabScoreArgs a) {
   }
 }
 
-int sab_score_nsplit(int B, int T, int N) {
-  const int blocks = B * T * ((N + 63) / 64);
-  int ns = (1024 + blocks - 1) / blocks;           // ~4 blocks per CU
+// QG = 2 measured slower on MI355X (tools/sabbench: the second group's registers cost a wave per
+// SIMD and the halved grid needs more key splits, i.e. more top-5 warm-ups); kept for tuning.
+static int sab_qg(int) { return 1; }
+
+int sab_score_nsplit(int B, int T, int N, int d) {
+  // as many key splits as keep the whole grid resident in one round: each split restarts the
+  // top-5 warm-up, a second round of blocks costs more than the split saves (tools/sabbench:
+  // d = 128 / T = 3 / N = 8160 best at 2 splits = 768 blocks = 3 per CU, d >= 256 at 1)
+  const int qb = 64 * sab_qg(d);
+  const int blocks = B * T * ((N + qb - 1) / qb);
+  const int cap = 256 * (d <= 128 ? 3 : 2);        // resident score blocks on MI355X (LDS / VGPRs)
   const int ntile = (N + 63) / 64;
-  return std::max(1, std::min(ns, std::min(8, ntile)));
+  return std::max(1, std::min(cap / std::max(1, blocks), std::min(8, ntile)));
 }
 
-template <typename T, int KT, int QK>
+template <typename T, int KT, int QK, int QG>
 static void launch_score_cfg(const SabScoreArgs& a, hipStream_t st) {
-  const size_t lds = 2 * (size_t)KT * (a.d * sizeof(T) + 16) + 64 * 4 * SAB_K * 8;
-  const int nqt = (a.N + 63) / 64;
+  const size_t lds = 2 * (size_t)KT * (a.d * sizeof(T) + 16) + 64 * QG * 4 * SAB_K * 8;
+  const int nqt = (a.N + 64 * QG - 1) / (64 * QG);
   static bool attr = false;                        // > 64 KB of dynamic LDS must be opted into
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_score_kernel<T, KT, QK>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_score_kernel<T, KT, QK, QG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((sab_score_kernel<T, KT, QK>), dim3((unsigned)(a.B * a.T * nqt * a.nsplit)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((sab_score_kernel<T, KT, QK, QG>), dim3((unsigned)(a.B * a.T * nqt * a.nsplit)), dim3(256), lds, st, a);
 }
 
 template <typename T>
 void launch_sab_score(const SabScoreArgs& a, hipStream_t st) {
   // d = 2c in {128, 256, 512} for the GoPro widths; K tiles of 64 keys (32 at d = 512: LDS ring)
   constexpr int KF = Frag<T>::K;
-  if (a.d <= 128) launch_score_cfg<T, 64, 128 / KF>(a, st);
-  else if (a.d <= 256) launch_score_cfg<T, 64, 256 / KF>(a, st);
-  else launch_score_cfg<T, 32, 512 / KF>(a, st);
+  if (a.d <= 128) launch_score_cfg<T, 64, 128 / KF, 1>(a, st);
+  else if (a.d <= 256) launch_score_cfg<T, 64, 256 / KF, 1>(a, st);
+  else launch_score_cfg<T, 32, 512 / KF, 1>(a, st);
 }
 
 // ------------------------------------------------------------------------------------------

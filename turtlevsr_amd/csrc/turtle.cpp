@@ -1035,7 +1035,7 @@ struct Runner {
     T* q2f = buf(P * d2);
     T* k2f = buf(P * d2);
     T* qtok = buf((int64_t)B * N * d2);
-    const int nsplit = sab_score_nsplit(B, NT, N);
+    const int nsplit = sab_score_nsplit(B, NT, N, d2);
     float* topv = fbuf((int64_t)B * NT * nsplit * N * 5);
     int* topi = reinterpret_cast<int*>(fbuf((int64_t)B * NT * nsplit * N * 5));
     float* ballv = fbuf((int64_t)B * NT * N * 41);
