@@ -362,6 +362,111 @@ void launch_weff(const WeffArgs& a, hipStream_t st) {
                      dim3(256), 0, st, a);
 }
 
+// attn_row + attn_weff in one launch: each W_eff block computes the softmax of every attention
+// row over all ncol columns from the reduced Gram (rows are <= 512 wide, ch <= 128) and keeps only
+// its 64 columns, staged straight into LDS for the projection fold. Same arithmetic order as
+// attn_row_kernel. Saves a launch and the A round trip through HBM per channel-attention block.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_weff_fused_kernel(AttnFinArgs f, WeffArgs a) {
+  __shared__ __attribute__((aligned(16))) float sA[WF_MAXCH][64];
+  __shared__ __attribute__((aligned(16))) float sW[WF_MAXCH][32];    // [i][o]
+  const int ch = a.ch, ncol = a.nseg * ch, stride = ch * ncol + ch + ncol;
+  const int o0 = blockIdx.x * 32, j0 = blockIdx.y * 64, bh = blockIdx.z;
+  const int b = bh / a.heads, h = bh % a.heads;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (int e = tid; e < 32 * ch; e += 256) {
+    const int oo = e / ch, i = e - oo * ch;
+    sW[i][oo] = o0 + oo < a.C ? a.wp[(int64_t)(o0 + oo) * a.C + h * ch + i] : 0.f;
+  }
+  const float* R = f.red + (int64_t)bh * stride;
+  // key-column scales kv (1/|k_j| on L2-normalised segments) of this lane's columns
+  float kv[AR_KC];
+#pragma unroll
+  for (int k = 0; k < AR_KC; ++k) {
+    const int jc = min(lane + 64 * k, ncol - 1);
+    kv[k] = ((f.norm_mask >> (jc / ch)) & 1) ? 1.f / fmaxf(sqrtf(R[ch * ncol + ch + jc]), 1e-12f) : 1.f;
+  }
+  const int jb = j0 / 64;                       // this block's columns are k = jb of every lane
+  const int kc = (ncol + 63) / 64;              // column vectors in use (uniform)
+  // 4 rows per wave per pass with all their loads in flight (the row loop is latency-bound)
+  constexpr int RG = 4;
+  for (int i0 = wid * RG; i0 < ch; i0 += 4 * RG) {
+    float lg[RG][AR_KC], qn[RG];
+#pragma unroll
+    for (int u = 0; u < RG; ++u) {
+      const int i = min(i0 + u, ch - 1);
+      qn[u] = R[ch * ncol + i];
+#pragma unroll
+      for (int k = 0; k < AR_KC; ++k)
+        lg[u][k] = k < kc ? R[i * ncol + min(lane + 64 * k, ncol - 1)] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < RG; ++u) {
+      const float q = f.tau[h] / fmaxf(sqrtf(qn[u]), 1e-12f);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < AR_KC; ++k) {
+        lg[u][k] = lane + 64 * k < ncol ? lg[u][k] * q * kv[k] : -INFINITY;
+        mx = fmaxf(mx, lg[u][k]);
+      }
+      mx = wave_max(mx);
+      float sum = 0.f, mine = 0.f;
+#pragma unroll
+      for (int k = 0; k < AR_KC; ++k) {
+        lg[u][k] = lane + 64 * k < ncol ? expf(lg[u][k] - mx) : 0.f;
+        sum += lg[u][k];
+        mine = k == jb ? lg[u][k] : mine;
+      }
+      const float inv = 1.f / wave_sum(sum);
+      if (i0 + u < ch) sA[i0 + u][lane] = mine * inv;     // 0 past ncol
+    }
+  }
+  if (blockIdx.x == 0 && wid == 0 && f.kinv && f.cur_seg >= 0) {
+    float mk = 0.f;
+#pragma unroll
+    for (int k = 0; k < AR_KC; ++k) mk = k == jb ? kv[k] : mk;
+    const int j = j0 + lane;
+    if (j >= f.cur_seg * ch && j < (f.cur_seg + 1) * ch) f.kinv[(int64_t)b * a.heads * ch + h * ch + (j - f.cur_seg * ch)] = mk;
+  }
+  __syncthreads();
+  const int jj = lane, og = wid * 8;
+  float acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = 0.f;
+  for (int i = 0; i < ch; ++i) {
+    const float av = sA[i][jj];
+    const float4 w0 = *reinterpret_cast<const float4*>(&sW[i][og]);
+    const float4 w1 = *reinterpret_cast<const float4*>(&sW[i][og + 4]);
+    acc[0] = fmaf(w0.x, av, acc[0]); acc[1] = fmaf(w0.y, av, acc[1]);
+    acc[2] = fmaf(w0.z, av, acc[2]); acc[3] = fmaf(w0.w, av, acc[3]);
+    acc[4] = fmaf(w1.x, av, acc[4]); acc[5] = fmaf(w1.y, av, acc[5]);
+    acc[6] = fmaf(w1.z, av, acc[6]); acc[7] = fmaf(w1.w, av, acc[7]);
+  }
+  const int col = j0 + jj;
+  if (col >= ncol) return;
+  const int sg = col / ch, j = col - sg * ch;
+  int64_t scol = a.seg_col[0];
+  int shs = a.seg_hstride[0];
+#pragma unroll
+  for (int q = 1; q < TURTLE_MAX_SEG; ++q)
+    if (sg == q) { scol = a.seg_col[q]; shs = a.seg_hstride[q]; }
+  T* W = reinterpret_cast<T*>(a.weff) + (int64_t)b * a.C * a.Keff + scol + (int64_t)h * shs + j;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (o0 + og + u < a.C) W[(int64_t)(o0 + og + u) * a.Keff] = from_f<T>(acc[u]);
+}
+
+template <typename T>
+void launch_attn_weff(const AttnFinArgs& f, const WeffArgs& a, hipStream_t st) {
+  const int ncol = f.nseg * f.ch, stride = f.ch * ncol + f.ch + ncol, nbh = f.B * f.heads;
+  hipLaunchKernelGGL(gram_sum_kernel, dim3((unsigned)((stride + 63) / 64), (unsigned)nbh), dim3(256), 0, st, f.part, f.red,
+                     f.nchunk, stride);
+  hipLaunchKernelGGL(attn_weff_fused_kernel<T>, dim3((unsigned)((a.C + 31) / 32), (unsigned)((ncol + 63) / 64), (unsigned)nbh),
+                     dim3(256), 0, st, f, a);
+}
+
+template void launch_attn_weff<float>(const AttnFinArgs&, const WeffArgs&, hipStream_t);
+template void launch_attn_weff<bf16>(const AttnFinArgs&, const WeffArgs&, hipStream_t);
 template void launch_gram<float>(const GramArgs&, hipStream_t);
 template void launch_gram<bf16>(const GramArgs&, hipStream_t);
 template void launch_weff<float>(const WeffArgs&, hipStream_t);

@@ -559,8 +559,11 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
     // measured per shape class (tools/kbench, MI355X): the 2-D tiled kernel for the resampling 3x3
     // convolutions and K >= 640 (incl. the five-source W_eff GEMM), the A-resident kernel for the
     // K = 256 residual projections, else the persistent panel kernel
+    // small frames (fewer than 32768 pixels: < 256 pn panels, i.e. a partly idle chip) also go to
+    // the 2-D tiled kernel, whose channel tiles multiply the grid
     const int K = g.a.Ktot;
-    if (((g.conv3 && g.N >= 256) || (!g.conv3 && K >= 640) || (!g.ln && K == 512 && g.N >= 512)) && gemm_kt_ok(g)) {
+    if (((g.conv3 && g.N >= 256) || (!g.conv3 && K >= 640) || (!g.ln && K == 512 && g.N >= 512) || g.M < 32768) &&
+        gemm_kt_ok(g)) {
       launch_gemm_kt(g, st);
       return;
     }

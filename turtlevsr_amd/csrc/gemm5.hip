@@ -350,11 +350,12 @@ static void launch_kt_cfg(const GemmArgs& g, hipStream_t st) {
 // tile choice (tools/kbench): 256 x 256 with 8 waves where N >= 256 fills the chip, else 128 x 128
 // with 4 waves (two blocks per CU); g.dbg & 0x30 forces a configuration for kbench
 void launch_gemm_kt(const GemmArgs& g, hipStream_t st) {
+  // the largest tile that still gives every CU a block (one round), else 128 x 128
   const int cfg = (g.dbg >> 4) & 3;
-  const int64_t tiles256 = ((g.M + 255) / 256) * ((g.N + 255) / 256);
-  const bool big = cfg ? cfg == 1 : (g.N >= 256 && tiles256 >= 256);
-  if (big) launch_kt_cfg<256, 256, 2, 4>(g, st);
-  else if (cfg == 3 || (!cfg && g.N >= 256)) launch_kt_cfg<128, 256, 2, 4>(g, st);
+  const int64_t t256 = ((g.M + 255) / 256) * ((g.N + 255) / 256), t128x256 = ((g.M + 127) / 128) * ((g.N + 255) / 256);
+  const int pick = cfg ? cfg : (g.N >= 256 && t256 >= 256) ? 1 : (g.N >= 256 && t128x256 >= 256) ? 3 : 2;
+  if (pick == 1) launch_kt_cfg<256, 256, 2, 4>(g, st);
+  else if (pick == 3) launch_kt_cfg<128, 256, 2, 4>(g, st);
   else launch_kt_cfg<128, 128, 2, 2>(g, st);
 }
 

@@ -146,6 +146,8 @@ struct WeffArgs {                  // W_eff[b][o][col] = sum_i Wp[o][h*ch+i] * A
   void* weff;                      // [B][C][Keff] storage type
 };
 template <typename T> void launch_weff(const WeffArgs& a, hipStream_t st);
+// Gram reduction + row softmax + W_eff fold in two launches (no A round trip)
+template <typename T> void launch_attn_weff(const AttnFinArgs& f, const WeffArgs& a, hipStream_t st);
 
 struct FhrCacheArgs {              // latent FHR cache roll: keep last Rnew rows of [old R ; cur ch]
   const void* old; int R;          // [B][P][heads][R] (R may be 0)

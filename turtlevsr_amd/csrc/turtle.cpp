@@ -301,6 +301,7 @@ struct TurtleHandle {
   bool gemm_pn = true;                                // resident-panel bf16 GEMM, K <= 512 (gemm3.hip)
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
+  bool attn_fuse = false;                             // row softmax folded into the W_eff kernel (attn.hip): slower so far
   bool sab_tile = false;                              // query-tiled VALU SAB gather (sab.hip)
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
@@ -811,15 +812,21 @@ struct Runner {
     AttnFinArgs f{};
     f.part = part; f.nchunk = nchunk; f.B = B; f.heads = b.heads; f.ch = ch; f.nseg = nseg;
     f.norm_mask = mask; f.tau = h->fptr(bw.tau); f.kinv = kinv; f.cur_seg = cur_seg; f.red = red; f.attn = attn;
-    tag("attn_rows nbh=%d ch=%d ncol=%d nchunk=%d", B * b.heads, ch, ncol, nchunk);
-    launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride, 0, [&] { launch_attn_finalize(f, st); });
     WeffArgs we{};
     we.attn = attn; we.wp = h->fptr(bw.wp); we.B = B; we.heads = b.heads; we.ch = ch; we.nseg = nseg; we.C = c;
     for (int s = 0; s < nseg; ++s) { we.seg_col[s] = segs[s].col; we.seg_hstride[s] = segs[s].colh; }
     we.Keff = vsrc.Ktot; we.weff = weff;
-    tag("weff B=%d C=%d heads=%d ncol=%d", B, c, b.heads, ncol);
-    launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot + 4.0 * B * b.heads * ch * ncol, 2.0 * B * c * (double)b.heads * ncol * ch,
-           [&] { launch_weff<T>(we, st); });
+    if (h->attn_fuse) {
+      tag("attn_weff nbh=%d ch=%d ncol=%d nchunk=%d C=%d", B * b.heads, ch, ncol, nchunk, c);
+      launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride + ES * (double)B * c * vsrc.Ktot,
+             2.0 * B * c * (double)b.heads * ncol * ch, [&] { launch_attn_weff<T>(f, we, st); });
+    } else {
+      tag("attn_rows nbh=%d ch=%d ncol=%d nchunk=%d", B * b.heads, ch, ncol, nchunk);
+      launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride, 0, [&] { launch_attn_finalize(f, st); });
+      tag("weff B=%d C=%d heads=%d ncol=%d", B, c, b.heads, ncol);
+      launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot + 4.0 * B * b.heads * ch * ncol, 2.0 * B * c * (double)b.heads * ncol * ch,
+             [&] { launch_weff<T>(we, st); });
+    }
     GemmW pw; pw.N = c; pw.K = vsrc.Ktot;
     gemm(pw, vsrc, (int64_t)B * HW, HW, Wimg, x, c, 0, x, c, 0, 0, STORE_NHWC, weff, (int64_t)c * vsrc.Ktot, 1, c,
          h->fptr(bw.po_bias));
@@ -1327,6 +1334,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
     else if (n == "gemm_ar") h->gemm_ar = value != 0;
     else if (n == "gemm_kt") h->gemm_kt = value != 0;
+    else if (n == "attn_fuse") h->attn_fuse = value != 0;
     else if (n == "pwdw") h->pwdw = value != 0;
     else if (n == "sab_tile") h->sab_tile = value != 0;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
