@@ -74,18 +74,10 @@ def f_ref(h, w):
 
 
 def source_hash():
-    """Hash of the HIP kernel sources + build script: ties committed PMC counters to the kernels
-    they were measured on."""
-    import hashlib
-    hs = hashlib.sha256()
-    base = os.path.join(REPO, "turtlevsr_amd")
-    for rel in sorted(os.listdir(os.path.join(base, "csrc"))) + ["../build.py"]:
-        path = os.path.join(base, "csrc", rel)
-        if os.path.isfile(path):
-            hs.update(rel.encode())
-            with open(path, "rb") as f:
-                hs.update(f.read())
-    return hs.hexdigest()[:16]
+    """Hash of the HIP kernel sources + build script (turtlevsr_amd/build.py): ties committed PMC
+    counters to the kernels they were measured on."""
+    from turtlevsr_amd.build import source_hash as sh
+    return sh()
 
 
 def cpu_model():

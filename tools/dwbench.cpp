@@ -37,7 +37,7 @@ int main(int argc, char** argv) {
       {136, 240, 1536, DW_PLAIN, "L4 qkv dw"},
       {544, 960, 384, DW_PLAIN, "L2 qkv dw"},
   };
-  const int variants[] = {1, 0};   // row sweep (default) vs per-pixel gather
+  const int variants[] = {1, 3, 0};   // row sweep (default), row sweep with the gate at 4 channels per lane, per-pixel gather
   hipStream_t st;
   CK(hipStreamCreate(&st));
   hipEvent_t e0, e1;

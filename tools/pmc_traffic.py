@@ -1,6 +1,6 @@
 """HBM traffic per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/prof_round.sh).
 
-    python tools/pmc_traffic.py gpurun_out/prof_<tag> 'TAG@@KERNEL_REGEX:GRID' ... > profiles/<round>_pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/prof_<tag> 'TAG@@KERNEL_REGEX[:GRID]' ... > profiles/pmc_traffic.json
 
 Per (kernel symbol, grid size) group: median FETCH_SIZE x 2 (gfx950 counts a wide 16-B/lane read
 at half its bytes: MI355X_MICROARCH.md, HBM section) + WRITE_SIZE, both reported in KB. A launch
@@ -38,14 +38,16 @@ def main():
     per_tag = {}
     for spec in sys.argv[2:]:
         tag, rest = spec.split("@@", 1)
-        rx, grid = rest.rsplit(":", 1)
-        hits = [k for k in groups if re.search(rx, k) and k.endswith(f"grid={grid}")]
+        rx, grid = rest.rsplit(":", 1) if re.search(r":\d+$", rest) else (rest, None)
+        hits = [k for k in groups if re.search(rx, k) and (grid is None or k.endswith(f"grid={grid}"))]
         if len(hits) == 1:
             g = groups[hits[0]]
             per_tag[tag] = dict(kernel=hits[0], hbm_bytes_per_launch=g["hbm_bytes"], fetch_bytes=g["fetch_bytes"],
                                 write_bytes=g["write_bytes"])
-    json.dump(dict(source=d, note="FETCH_SIZE doubled (gfx950 wide-read undercount); KB -> bytes", per_tag=per_tag,
-                   groups=groups), sys.stdout, indent=1)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from turtlevsr_amd.build import source_hash
+    json.dump(dict(source=d, source_hash=source_hash(), note="FETCH_SIZE doubled (gfx950 wide-read undercount); KB -> bytes",
+                   per_tag=per_tag, groups=groups), sys.stdout, indent=1)
 
 
 if __name__ == "__main__":

@@ -66,3 +66,17 @@ def build(force: bool = False, verbose: bool = True) -> str:
 
 if __name__ == "__main__":
     build(force="--force" in sys.argv)
+
+
+def source_hash() -> str:
+    """Hash of the HIP kernel sources + this build script: ties committed PMC counters
+    (profiles/pmc_traffic.json) to the kernels they were measured on."""
+    import hashlib
+    hs = hashlib.sha256()
+    for rel in sorted(os.listdir(CSRC)) + ["../build.py"]:
+        path = os.path.join(CSRC, rel)
+        if os.path.isfile(path):
+            hs.update(rel.encode())
+            with open(path, "rb") as f:
+                hs.update(f.read())
+    return hs.hexdigest()[:16]

@@ -504,7 +504,7 @@ __global__ __launch_bounds__(256, 2) void gemm_panel_kernel(GemmArgs g, int nspl
           float x = acc[mt][tn][e];
           if (g.ln) x = rs * (x - mu * vs[tn][e]) + vt[tn][e];
           x += vb[tn][e];
-          if (g.gelu) x = gelu_tanh(x);
+          if (g.gelu) x = gelu_bf16(x);
           const uint32_t rw = e < 2 ? rv[mt][tn].x : rv[mt][tn].y;
           v[e] = x * vc[tn][e] + __uint_as_float((e & 1) ? (rw & 0xffff0000u) : (rw << 16));
         }

@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256, 2) void gemm_lds_kernel(GemmArgs g) {
         float x = acc[tm][tn][e];
         if (g.ln) x = rs * (x - mu * fs[e]) + ft[e];
         x += fb[e];
-        if (g.gelu) x = gelu_tanh(x);
+        if (g.gelu) x = gelu_bf16(x);
         v[e] = x * fc[e];
       }
       typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));

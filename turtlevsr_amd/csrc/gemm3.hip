@@ -324,7 +324,7 @@ __global__ __launch_bounds__(512, 1) void gemm_pn_kernel(GemmArgs g, int npanel)
         }
         if (g.gelu) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(v[e]);
+          for (int e = 0; e < 8; ++e) v[e] = gelu_bf16(v[e]);
         }
         if (g.scale) {
           const f32x4 vc0 = *reinterpret_cast<const f32x4*>(e_c + cb), vc1 = *reinterpret_cast<const f32x4*>(e_c + cb + 4);

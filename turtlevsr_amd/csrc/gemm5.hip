@@ -281,7 +281,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * WN <= 4) ? 2 : 1) void gemm_kt_
         float x = acc[tm][2 * j + (e >> 2)][e & 3];
         if (g.ln) x = rs * (x - mu * fs[e]) + ft[e];
         x += fb[e];
-        if (g.gelu) x = gelu_tanh(x);
+        if (g.gelu) x = gelu_bf16(x);
         v[e] = x * fc[e];
       }
       if (res) {

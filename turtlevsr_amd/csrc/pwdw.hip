@@ -271,7 +271,7 @@ __global__ __launch_bounds__(512, 2) void pwdw_kernel(PwdwArgs a) {
     if (y < a.H && x < a.W) {
       Vec<bf16> o;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) o.v[e] = GATE ? gelu_tanh(d1[e]) * d2[e] : d1[e];
+      for (int e = 0; e < 8; ++e) o.v[e] = GATE ? gelu_bf16(d1[e]) * d2[e] : d1[e];
       const int oc = GATE ? sl * 64 + cv * 8 : sl * 128 + cv * 8;
       o.store(out + (((int64_t)img * a.H + y) * a.W + x) * a.ldo + a.offo + oc);
     }

@@ -29,23 +29,59 @@ TURTLE_DEV void unpack16<float>(const uint4& q, float (&v)[4]) {
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_dw[4];
 
+// raw channel vector of VW elements for the row-sweep depthwise: 16 bytes (bf16 x 8, fp32 x 4), or
+// 8 bytes (bf16 x 4: the gate's two halves in the register footprint of one plain vector)
+template <typename T, int VW> struct DwRaw;
+template <> struct DwRaw<bf16, 8> {
+  typedef uint4 raw;
+  static TURTLE_DEV raw load(const void* p) { return ld16(p); }
+  static TURTLE_DEV void unpack(const raw& q, float (&v)[8]) { unpack16<bf16>(q, v); }
+  static TURTLE_DEV void store(bf16* p, const float (&v)[8]) {
+    Vec<bf16> o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o.v[i] = v[i];
+    o.store(p);
+  }
+};
+template <> struct DwRaw<bf16, 4> {
+  typedef uint2 raw;
+  static TURTLE_DEV raw load(const void* p) { return ld8(p); }
+  static TURTLE_DEV void unpack(const raw& q, float (&v)[4]) {
+    v[0] = __uint_as_float(q.x << 16); v[1] = __uint_as_float(q.x & 0xffff0000u);
+    v[2] = __uint_as_float(q.y << 16); v[3] = __uint_as_float(q.y & 0xffff0000u);
+  }
+  static TURTLE_DEV void store(bf16* p, const float (&v)[4]) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<bf16x4*>(p) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+  }
+};
+template <> struct DwRaw<float, 4> {
+  typedef uint4 raw;
+  static TURTLE_DEV raw load(const void* p) { return ld16(p); }
+  static TURTLE_DEV void unpack(const raw& q, float (&v)[4]) { unpack16<float>(q, v); }
+  static TURTLE_DEV void store(float* p, const float (&v)[4]) { *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]); }
+};
+
 // Row-sweeping depthwise 3x3. A block owns a (32-column strip) x (DW_CC channel vectors) x (band of
 // RB rows) box of one image; thread = (column, channel vector). Walking down the band, each thread
 // keeps the 3x3 neighbourhood of its column as a rolling window of three rows in registers and
 // loads only the next row (3 vectors, the two side ones L1 hits of its neighbours' loads), one row
 // ahead of the math. Every input byte therefore leaves HBM about once (band halo 2/RB) instead of
 // the 3 row re-reads of a per-pixel gather. Tap weights of the block's channels sit in LDS (fp32).
+// VW = channels per lane: a 16-byte vector, or 4 for the bf16 gate (x1 and x2 vectors of 8 bytes:
+// 71 VGPRs, 7 waves per SIMD instead of 129 / 3; slower, kept for tools/dwbench).
 constexpr int DW_CC = 8;                                  // channel vectors per block
 constexpr int DW_SX = 256 / DW_CC;                        // columns per block
-template <typename T, int MODE>
+template <typename T, int MODE, int VW>
 __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstrip, int nchunk, int nband) {
-  constexpr int VEC = Vec<T>::N;
+  using RW = DwRaw<T, VW>;
+  typedef typename RW::raw raw;
   constexpr int NH = MODE == DW_GATE ? 2 : 1;             // gate: x1 and x2 halves
-  constexpr int CW = DW_CC * VEC;                         // channels per block
+  constexpr int CW = DW_CC * VW;                          // channels per block
   __shared__ __attribute__((aligned(16))) float sw[NH][9][CW];
   __shared__ __attribute__((aligned(16))) float sbias[NH][CW];
   const int tid = threadIdx.x;
-  const int CV = a.C / VEC;
+  const int CV = a.C / VW;
   const int Cw = NH * a.C;
   int lin = blockIdx.x;
   {
@@ -73,50 +109,50 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
   const int cvl = tid % DW_CC, xs = tid / DW_CC;
   const int x = strip * DW_SX + xs, cv = chunk * DW_CC + cvl;
   const bool live = x < a.W && cv < CV;
-  const int xc = min(x, a.W - 1), c0 = min(cv, CV - 1) * VEC;
+  const int xc = min(x, a.W - 1), c0 = min(cv, CV - 1) * VW;
   const int y0 = band * RB, y1 = min(a.H, y0 + RB);
   const T* in = reinterpret_cast<const T*>(a.in) + img * a.H * a.W * a.ldi + a.offi + c0;
   const bool okl = xc > 0, okr = xc + 1 < a.W;
   // one row of the window: columns x-1, x, x+1 (zero line outside the image)
-  auto load_row = [&](int y, uint4 (&r)[NH][3]) {
+  auto load_row = [&](int y, raw (&r)[NH][3]) {
     const bool oky = y >= 0 && y < a.H;
     const T* p = in + ((int64_t)(oky ? y : 0) * a.W + xc) * a.ldi;
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh) {
       const T* q = p + hh * a.C;
-      r[hh][0] = ld16(oky && okl ? reinterpret_cast<const void*>(q - a.ldi) : g_zero_dw);
-      r[hh][1] = ld16(oky ? reinterpret_cast<const void*>(q) : g_zero_dw);
-      r[hh][2] = ld16(oky && okr ? reinterpret_cast<const void*>(q + a.ldi) : g_zero_dw);
+      r[hh][0] = RW::load(oky && okl ? reinterpret_cast<const void*>(q - a.ldi) : g_zero_dw);
+      r[hh][1] = RW::load(oky ? reinterpret_cast<const void*>(q) : g_zero_dw);
+      r[hh][2] = RW::load(oky && okr ? reinterpret_cast<const void*>(q + a.ldi) : g_zero_dw);
     }
   };
-  uint4 w0[NH][3], w1[NH][3], w2[NH][3], nx[NH][3];
+  raw w0[NH][3], w1[NH][3], w2[NH][3], nx[NH][3];
   load_row(y0 - 1, w0);
   load_row(y0, w1);
   load_row(y0 + 1, w2);
   __syncthreads();
-  const int wc = cvl * VEC;
+  const int wc = cvl * VW;
   for (int y = y0; y < y1; ++y) {
     if (y + 1 < y1) load_row(y + 2, nx);                  // next row in flight during the math
     // re-read the tap weights from LDS every row (opaque offset): hoisted, they would hold
     // 72-144 VGPRs for the whole sweep
     int wcy = wc;
     asm volatile("" : "+v"(wcy));
-    float acc[NH][VEC];
+    float acc[NH][VW];
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh) {
 #pragma unroll
-      for (int i0 = 0; i0 < VEC; i0 += 4) {
+      for (int i0 = 0; i0 < VW; i0 += 4) {
         const float4 bb = *reinterpret_cast<const float4*>(&sbias[hh][wcy + i0]);
         acc[hh][i0] = bb.x; acc[hh][i0 + 1] = bb.y; acc[hh][i0 + 2] = bb.z; acc[hh][i0 + 3] = bb.w;
       }
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
-        const uint4 q = tap < 3 ? w0[hh][tap] : tap < 6 ? w1[hh][tap - 3] : w2[hh][tap - 6];
-        float v[VEC];
-        unpack16<T>(q, v);
+        const raw q = tap < 3 ? w0[hh][tap] : tap < 6 ? w1[hh][tap - 3] : w2[hh][tap - 6];
+        float v[VW];
+        RW::unpack(q, v);
         const float* wt = &sw[hh][tap][wcy];
 #pragma unroll
-        for (int i0 = 0; i0 < VEC; i0 += 4) {
+        for (int i0 = 0; i0 < VW; i0 += 4) {
           const float4 ww = *reinterpret_cast<const float4*>(wt + i0);
           acc[hh][i0] = fmaf(ww.x, v[i0], acc[hh][i0]);
           acc[hh][i0 + 1] = fmaf(ww.y, v[i0 + 1], acc[hh][i0 + 1]);
@@ -126,17 +162,17 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
         // one tap's weights / unpacked values live at a time (the scheduler would otherwise
         // hoist all 9 taps' LDS reads and unpacks: 200+ VGPRs, one wave per SIMD)
 #pragma unroll
-        for (int i = 0; i < VEC; ++i) asm volatile("" : "+v"(acc[hh][i]));
+        for (int i = 0; i < VW; ++i) asm volatile("" : "+v"(acc[hh][i]));
       }
     }
     if (live) {
-      Vec<T> o;
+      float o[VW];
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) {
+      for (int i = 0; i < VW; ++i) {
         float r = acc[0][i];
         if (MODE == DW_GELU) r = gelu_t<T>(r);
         else if (MODE == DW_GATE) r = gelu_t<T>(r) * acc[NH - 1][i];
-        o.v[i] = r;
+        o[i] = r;
       }
       const int64_t pix = (img * a.H + y) * a.W + x;
       int64_t dst;
@@ -147,7 +183,7 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
       } else {
         dst = pix * a.ldo + a.offo + c0;
       }
-      o.store(reinterpret_cast<T*>(a.out) + dst);
+      RW::store(reinterpret_cast<T*>(a.out) + dst, o);
     }
 #pragma unroll
     for (int hh = 0; hh < NH; ++hh)
@@ -237,20 +273,29 @@ __global__ __launch_bounds__(256) void dw_kernel(DwArgs a) {
   o.store(reinterpret_cast<T*>(a.out) + dst);
 }
 
+template <typename T, int MODE, int VW>
+static void launch_dw_rows(const DwArgs& a, hipStream_t st) {
+  const int CV = a.C / VW;
+  const int nstrip = (a.W + DW_SX - 1) / DW_SX, nchunk = (CV + DW_CC - 1) / DW_CC;
+  // band height: tall bands (halo 2/RB) while the grid still has >= ~8 blocks per CU
+  int RB = 32;
+  auto nblk = [&](int rb) { return (int64_t)a.nimg * nchunk * nstrip * ((a.H + rb - 1) / rb); };
+  while (RB > 4 && nblk(RB) < 2048) RB /= 2;
+  const int nband = (a.H + RB - 1) / RB;
+  hipLaunchKernelGGL((dw_rows_kernel<T, MODE, VW>), dim3((unsigned)nblk(RB)), dim3(256), 0, st, a, RB, nstrip, nchunk, nband);
+}
+
 template <typename T>
 void launch_dw(const DwArgs& a, hipStream_t st) {
   if (a.rows) {
-    const int CV = a.C / Vec<T>::N;
-    const int nstrip = (a.W + DW_SX - 1) / DW_SX, nchunk = (CV + DW_CC - 1) / DW_CC;
-    // band height: tall bands (halo 2/RB) while the grid still has >= ~8 blocks per CU
-    int RB = 32;
-    auto nblk = [&](int rb) { return (int64_t)a.nimg * nchunk * nstrip * ((a.H + rb - 1) / rb); };
-    while (RB > 4 && nblk(RB) < 2048) RB /= 2;
-    const int nband = (a.H + RB - 1) / RB;
-    const dim3 grid((unsigned)nblk(RB));
-    if (a.mode == DW_GATE) hipLaunchKernelGGL((dw_rows_kernel<T, DW_GATE>), grid, dim3(256), 0, st, a, RB, nstrip, nchunk, nband);
-    else if (a.mode == DW_GELU) hipLaunchKernelGGL((dw_rows_kernel<T, DW_GELU>), grid, dim3(256), 0, st, a, RB, nstrip, nchunk, nband);
-    else hipLaunchKernelGGL((dw_rows_kernel<T, DW_PLAIN>), grid, dim3(256), 0, st, a, RB, nstrip, nchunk, nband);
+    constexpr int V = Vec<T>::N;
+    // a.rows == 3: the bf16 gate at 4 channels per lane (tools/dwbench; measured slower on MI355X:
+    // L3 gate 172 -> 227 us despite 7 instead of 3 waves per SIMD - the 8-byte loads cost more than
+    // the occupancy buys)
+    if (a.mode == DW_GATE && sizeof(T) == 2 && a.rows == 3 && a.C % 4 == 0) launch_dw_rows<T, DW_GATE, 4>(a, st);
+    else if (a.mode == DW_GATE) launch_dw_rows<T, DW_GATE, V>(a, st);
+    else if (a.mode == DW_GELU) launch_dw_rows<T, DW_GELU, V>(a, st);
+    else launch_dw_rows<T, DW_PLAIN, V>(a, st);
     return;
   }
   const int64_t total = (int64_t)a.nimg * a.H * a.W * (a.C / Vec<T>::N);

@@ -1,7 +1,8 @@
 """Parameter holders with the reference's module paths, so ``state_dict()`` has the same 633 keys.
 
-These modules hold ``nn.Parameter`` tensors only; they compute nothing. The forward lives in
-the HIP library (``hip_forward.py``). Module / parameter names and registration order follow the
+These modules hold ``nn.Parameter`` tensors only; they compute nothing. The inference forward
+lives in the HIP library (``turtlevsr_amd/model.py`` drives ``libturtle_hip.so`` through
+``_lib.py``); the training graph over the same tree is ``turtlevsr_amd/train.py``. Module / parameter names and registration order follow the
 reference constructors so ``load_state_dict(torch.load(p)['params'], strict=True)`` of a reference
 checkpoint works unchanged (base_model.py:261-286, inference.py:248-255):
 
