@@ -219,3 +219,28 @@ def test_hip_vs_oracle_through_tiled_harness():
         assert float((a - b).abs().max()) <= 1e-4
     for a, b in zip(r_hip.psnr, r_ref.psnr):
         assert abs(a - b) <= 0.05 or (math.isinf(a) and math.isinf(b))
+
+
+@pytest.mark.gpu
+def test_hip_vs_oracle_published_tiled_protocol():
+    """The reference's published evaluation protocol on the HIP path (basicsr/inference.py:590-609,
+    172-246): GoPro widths, tile 320, overlap 192, per-tile caches carried through HOST memory
+    between frames (:227-237). 3 frames of 352 x 480 = 2 x 3 tiles per frame. fp32 HIP vs the
+    oracle through the same harness: restored frames to 2e-4, uint8 PSNR within 0.01 dB."""
+    from golden_io import load
+    from turtlevsr_amd.model import TurtleHIP
+    _, meta = load("clip_gopro_64")
+    m_ref, sd = _oracle_model(meta)
+    hip = TurtleHIP(meta["opt"], dtype="fp32")
+    hip.load_state_dict(sd, strict=True)
+    hip = hip.cuda().eval()
+    torch.manual_seed(4)
+    frames = [torch.rand(3, 352, 480) for _ in range(3)]
+    with torch.no_grad():
+        r_ref = run_video(frames, frames, m_ref, tile=320, tile_overlap=192, keep_outputs=True)
+        r_hip = run_video([f.cuda() for f in frames], frames, hip, tile=320, tile_overlap=192, keep_outputs=True,
+                          cache_device="cpu")
+    for a, b in zip(r_hip.outputs, r_ref.outputs):
+        assert float((a.cpu() - b).abs().max()) <= 2e-4
+    for a, b in zip(r_hip.psnr, r_ref.psnr):
+        assert abs(a - b) <= 0.01 or (math.isinf(a) and math.isinf(b))

@@ -80,7 +80,10 @@ struct F2L {
 
 // MODE, input width CM (= GEMM2 width), tile rows R (multiple of 3), waves NW, hidden channels per
 // pass HPM (0: dw-only), max GEMM1 width N1M, minimum waves per SIMD WPE (register budget)
-template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE>
+// TPB tiles per block (TPB > 1: a block walks a run of consecutive tiles; the next tile's haloed
+// input is fetched into registers while the current one computes, and the per-channel tables are
+// loaded once per block instead of once per tile)
+template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE, int TPB = 1>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void fused2_kernel(FusedArgs a) {
   using L = F2L<CM, R, HPM, N1M, MODE == F_GATEOUT ? NW * R * 512 : 0>;
   constexpr int KS = CM / 32;                       // GEMM1 K steps
@@ -97,38 +100,20 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const int px = lane & 15, grp = lane >> 4;
   const int N1 = a.N1;
 
-  // ---- tile (XCD-aware: consecutive tiles on one XCD share halo rows in its L2) ----
+  // ---- tiles (XCD-aware: consecutive tiles on one XCD share halo rows in its L2) ----
   const int tx_n = (a.W + F2_TX - 1) / F2_TX, ty_n = (a.H + R - 1) / R;
+  const int ntiles = a.nimg * tx_n * ty_n;
   int lin = blockIdx.x;
   {
     const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
     lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;
   }
-  const int img = lin / (tx_n * ty_n);
-  const int trem = lin - img * tx_n * ty_n;
-  const int y0 = (trem / tx_n) * R, x0 = (trem % tx_n) * F2_TX;
+  const int t_begin = lin * TPB, t_end = min(ntiles, t_begin + TPB);
   const bf16* W1 = reinterpret_cast<const bf16*>(a.w1);
   const float* zf = reinterpret_cast<const float*>(g_zero_f2);
 
-  // ---- raw haloed input tile + per-channel tables (taps, LN / bias vectors) -> LDS ----
+  // ---- per-channel tables (taps, LN / bias vectors) -> LDS, once per block ----
   {
-    const bf16* X = reinterpret_cast<const bf16*>(a.x);
-    constexpr int CV = CM / 8;                       // 16-byte chunks per pixel
-    constexpr int NV = (L::NXP * CV + NT - 1) / NT;
-    uint4 v[NV];
-    int o[NV];
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-      const int e = tid + NT * i;
-      const int p = e / CV, k = (e - p * CV) * 8;
-      const int hr = p >> 4, hp = p & 15;
-      const int y = y0 - 1 + hr, x = x0 - 1 + hp;
-      const bool live = p < L::NXP;
-      const bool ok = live && y >= 0 && y < a.H && x >= 0 && x < a.W;
-      const int64_t off = (((int64_t)img * a.H + (ok ? y : 0)) * a.W + (ok ? x : 0)) * a.ldx + a.offx + k;
-      v[i] = ld16(ok ? reinterpret_cast<const void*>(X + off) : g_zero_f2);
-      o[i] = live ? p * L::XP + k * 2 : -1;
-    }
     // taps: bf16 pairs [5][N1] (lo = tap 2i, hi = tap 2i + 1), straight copy
     const uint32_t* tg = a.dww2;
     for (int e = tid * 4; e < 5 * N1; e += NT * 4)
@@ -139,10 +124,38 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       const float dv = a.dwb ? a.dwb[c] : 0.f;
       sVec[c] = sv; sVec[N1M + c] = tv; sVec[2 * N1M + c] = dv;
     }
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-      if (o[i] >= 0) *reinterpret_cast<uint4*>(sX + o[i]) = v[i];
   }
+  // ---- raw haloed input tile: registers (vx) -> LDS; the LDS slot of a chunk depends on tid only ----
+  constexpr int CV = CM / 8;                         // 16-byte chunks per pixel
+  constexpr int NV = (L::NXP * CV + NT - 1) / NT;
+  uint4 vx[NV];
+  auto fetch_x = [&](int tile) {
+    const bf16* X = reinterpret_cast<const bf16*>(a.x);
+    const int timg = tile / (tx_n * ty_n), trem = tile - timg * tx_n * ty_n;
+    const int ty0 = (trem / tx_n) * R, tx0 = (trem % tx_n) * F2_TX;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int e = tid + NT * i;
+      const int p = e / CV, k = (e - p * CV) * 8;
+      const int hr = p >> 4, hp = p & 15;
+      const int y = ty0 - 1 + hr, x = tx0 - 1 + hp;
+      const bool ok = p < L::NXP && y >= 0 && y < a.H && x >= 0 && x < a.W;
+      const int64_t off = (((int64_t)timg * a.H + (ok ? y : 0)) * a.W + (ok ? x : 0)) * a.ldx + a.offx + k;
+      vx[i] = ld16(ok ? reinterpret_cast<const void*>(X + off) : g_zero_f2);
+    }
+  };
+  if (t_begin < t_end) fetch_x(t_begin);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+  const int img = tile / (tx_n * ty_n);
+  const int trem = tile - img * tx_n * ty_n;
+  const int y0 = (trem / tx_n) * R, x0 = (trem % tx_n) * F2_TX;
+  if (tile > t_begin) __syncthreads();               // every wave is done with the previous tile's LDS
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int e = tid + NT * i, p = e / CV, k = (e - p * CV) * 8;
+    if (p < L::NXP) *reinterpret_cast<uint4*>(sX + p * L::XP + k * 2) = vx[i];
+  }
+  if (tile + 1 < t_end) fetch_x(tile + 1);           // in flight during this tile's walks
   __syncthreads();
   // ---- LayerNorm statistics per haloed pixel (2 threads per pixel, shifted sums) ----
   for (int e = tid; e < 2 * L::NXP; e += NT) {
@@ -443,19 +456,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       }
     }
   }
+  }   // tile loop
 }
 
 // (MODE, C) -> (tile rows, waves, hidden per pass); units per pass chosen so every wave of a pass
 // gets the same number of units
-template <int MODE, int CM, int R, int NW, int HPM, int WPE>
+template <int MODE, int CM, int R, int NW, int HPM, int WPE, int TPB = 1>
 static void f2_launch(const FusedArgs& a0, hipStream_t st) {
   FusedArgs a = a0;
   a.up = HPM / 16;
   // widest GEMM1 the per-channel tables hold: 2 int(2.5 C) (gate), 2C (ReducedAttn), 6C (CHM
   // [qk | v | qkv]); at C = 256 the dw-only tables stop at 3C (qkv, kv) to fit 2 blocks per CU
   constexpr int N1M = (MODE == F_GATE || MODE == F_GATEOUT) ? 5 * CM : (MODE == F_GELU ? 2 * CM : (CM >= 256 ? 3 * CM : 6 * CM));
-  const int64_t blocks = (int64_t)a.nimg * ((a.H + R - 1) / R) * ((a.W + F2_TX - 1) / F2_TX);
-  hipLaunchKernelGGL((fused2_kernel<MODE, CM, R, NW, HPM, N1M, WPE>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, a);
+  const int64_t tiles = (int64_t)a.nimg * ((a.H + R - 1) / R) * ((a.W + F2_TX - 1) / F2_TX);
+  const int64_t blocks = (tiles + TPB - 1) / TPB;
+  hipLaunchKernelGGL((fused2_kernel<MODE, CM, R, NW, HPM, N1M, WPE, TPB>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, a);
 }
 
 bool fused2_ok(const FusedArgs& a) {
@@ -499,6 +514,9 @@ void launch_fused2(const FusedArgs& a, hipStream_t st) {
     if (a.C == 64) {
       if (v == 1) f2_launch<F_GATE, 64, 6, 4, 160, 3>(a, st);
       else if (v == 2) f2_launch<F_GATE, 64, 3, 4, 64, 3>(a, st);
+      // 4 tiles per block with the next tile prefetched: 942 -> 964 us (tools/f2bench), the per-tile
+      // prologue is not what bounds it; 5 waves x 2 units in one pass: 1491 us
+      else if (v == 3) f2_launch<F_GATE, 64, 9, 4, 64, 3, 4>(a, st);
       else f2_launch<F_GATE, 64, 9, 4, 64, 3>(a, st);
     } else {
       if (v == 1) f2_launch<F_GATE, 128, 3, 4, 64, 2>(a, st);
