@@ -149,9 +149,9 @@ int main(int argc, char** argv) {
     };
     if (only_v < 0 && has_ref) run("fused", [&] { launch_fused<bf16>(ab, 0); });
     if (fused2_ok(ab)) {
-      for (int v = 0; v < 4; ++v) {
+      for (int v = 0; v < 6; ++v) {
         if (only_v >= 0 && v != only_v) continue;
-        if (v >= 3 && !(ab.mode == F_GATE && ab.C == 64)) continue;
+        if (ab.C == 256 && v >= 3) continue;
         FusedArgs c = ab; c.dbg = v;
         char nm[16]; snprintf(nm, sizeof nm, "fused2.%d", v);
         run(nm, [&] { launch_fused2(c, 0); });

@@ -491,7 +491,8 @@ bool fused2_ok(const FusedArgs& a) {
 // minimum waves per SIMD WPE. `a.dbg` (tools/f2bench only; 0 in the product path) selects an
 // alternative configuration for the same shape.
 void launch_fused2(const FusedArgs& a, hipStream_t st) {
-  // defaults (v = 0) are the fastest measured per shape family on MI355X (tools/f2bench, 1080p)
+  // defaults (v = 0) are the fastest measured per shape family on MI355X (tools/f2bench, 1080p);
+  // v = 1..5 are the alternatives of the last sweep (profiles/r02h_f2bench_sweep.log)
   const int v = a.dbg;
   if (a.mode == F_GATEOUT) {
     if (v == 1) f2_launch<F_GATEOUT, 256, 6, 8, 0, 2>(a, st);
@@ -502,36 +503,63 @@ void launch_fused2(const FusedArgs& a, hipStream_t st) {
     else f2_launch<F_DWONLY, 256, 3, 4, 0, 2>(a, st);
   } else if (a.mode == F_DWONLY) {
     if (a.C == 64) {
-      if (v == 1) f2_launch<F_DWONLY, 64, 6, 4, 0, 4>(a, st);
-      else if (v == 2) f2_launch<F_DWONLY, 64, 9, 4, 0, 4>(a, st);
-      else f2_launch<F_DWONLY, 64, 15, 4, 0, 4>(a, st);
+      switch (v) {
+        case 1: f2_launch<F_DWONLY, 64, 15, 4, 0, 4>(a, st); break;
+        case 2: f2_launch<F_DWONLY, 64, 9, 4, 0, 4>(a, st); break;
+        case 3: f2_launch<F_DWONLY, 64, 18, 4, 0, 4>(a, st); break;
+        case 4: f2_launch<F_DWONLY, 64, 21, 4, 0, 3>(a, st); break;
+        case 5: f2_launch<F_DWONLY, 64, 15, 4, 0, 4, 2>(a, st); break;
+        default: f2_launch<F_DWONLY, 64, 12, 4, 0, 4>(a, st);
+      }
     } else {
-      if (v == 1) f2_launch<F_DWONLY, 128, 3, 4, 0, 4>(a, st);
-      else if (v == 2) f2_launch<F_DWONLY, 128, 6, 4, 0, 4>(a, st);
-      else f2_launch<F_DWONLY, 128, 9, 4, 0, 3>(a, st);
+      switch (v) {
+        case 1: f2_launch<F_DWONLY, 128, 6, 4, 0, 4>(a, st); break;
+        case 2: f2_launch<F_DWONLY, 128, 12, 4, 0, 3>(a, st); break;
+        case 3: f2_launch<F_DWONLY, 128, 6, 4, 0, 3>(a, st); break;
+        case 4: f2_launch<F_DWONLY, 128, 15, 4, 0, 2>(a, st); break;
+        case 5: f2_launch<F_DWONLY, 128, 9, 4, 0, 3>(a, st); break;
+        default: f2_launch<F_DWONLY, 128, 9, 4, 0, 4>(a, st);
+      }
     }
   } else if (a.mode == F_GATE) {
     if (a.C == 64) {
-      if (v == 1) f2_launch<F_GATE, 64, 6, 4, 160, 3>(a, st);
-      else if (v == 2) f2_launch<F_GATE, 64, 3, 4, 64, 3>(a, st);
-      // 4 tiles per block with the next tile prefetched: 942 -> 964 us (tools/f2bench), the per-tile
-      // prologue is not what bounds it; 5 waves x 2 units in one pass: 1491 us
-      else if (v == 3) f2_launch<F_GATE, 64, 9, 4, 64, 3, 4>(a, st);
-      else f2_launch<F_GATE, 64, 9, 4, 64, 3>(a, st);
+      switch (v) {
+        case 1: f2_launch<F_GATE, 64, 9, 4, 64, 3>(a, st); break;
+        case 2: f2_launch<F_GATE, 64, 12, 4, 64, 2>(a, st); break;
+        case 3: f2_launch<F_GATE, 64, 9, 4, 64, 3, 4>(a, st); break;   // 4 tiles per block, next tile prefetched
+        case 4: f2_launch<F_GATE, 64, 6, 4, 64, 4>(a, st); break;
+        case 5: f2_launch<F_GATE, 64, 3, 4, 64, 4>(a, st); break;
+        default: f2_launch<F_GATE, 64, 6, 4, 64, 3>(a, st);           // 46 KB: 3 blocks per CU
+      }
     } else {
-      if (v == 1) f2_launch<F_GATE, 128, 3, 4, 64, 2>(a, st);
-      else if (v == 2) f2_launch<F_GATE, 128, 3, 4, 128, 2>(a, st);
-      else f2_launch<F_GATE, 128, 6, 4, 64, 2>(a, st);
+      switch (v) {
+        case 1: f2_launch<F_GATE, 128, 3, 4, 64, 3>(a, st); break;
+        case 2: f2_launch<F_GATE, 128, 3, 4, 128, 2>(a, st); break;
+        case 3: f2_launch<F_GATE, 128, 6, 4, 64, 3>(a, st); break;
+        case 4: f2_launch<F_GATE, 128, 9, 4, 64, 2>(a, st); break;
+        case 5: f2_launch<F_GATE, 128, 3, 4, 64, 2>(a, st); break;
+        default: f2_launch<F_GATE, 128, 6, 4, 64, 2>(a, st);
+      }
     }
   } else {
     if (a.C == 64) {
-      if (v == 1) f2_launch<F_GELU, 64, 9, 4, 64, 3>(a, st);
-      else if (v == 2) f2_launch<F_GELU, 64, 3, 4, 64, 4>(a, st);
-      else f2_launch<F_GELU, 64, 6, 4, 128, 3>(a, st);
+      switch (v) {
+        case 1: f2_launch<F_GELU, 64, 9, 4, 64, 3>(a, st); break;
+        case 2: f2_launch<F_GELU, 64, 6, 4, 64, 3>(a, st); break;
+        case 3: f2_launch<F_GELU, 64, 6, 4, 64, 4>(a, st); break;
+        case 4: f2_launch<F_GELU, 64, 9, 4, 128, 2>(a, st); break;
+        case 5: f2_launch<F_GELU, 64, 3, 4, 64, 4>(a, st); break;
+        default: f2_launch<F_GELU, 64, 6, 4, 128, 3>(a, st);
+      }
     } else {
-      if (v == 1) f2_launch<F_GELU, 128, 3, 4, 64, 2>(a, st);
-      else if (v == 2) f2_launch<F_GELU, 128, 3, 4, 128, 2>(a, st);
-      else f2_launch<F_GELU, 128, 6, 4, 64, 2>(a, st);
+      switch (v) {
+        case 1: f2_launch<F_GELU, 128, 3, 4, 64, 3>(a, st); break;
+        case 2: f2_launch<F_GELU, 128, 3, 4, 128, 2>(a, st); break;
+        case 3: f2_launch<F_GELU, 128, 6, 4, 64, 3>(a, st); break;
+        case 4: f2_launch<F_GELU, 128, 6, 4, 64, 2>(a, st); break;
+        case 5: f2_launch<F_GELU, 128, 3, 4, 64, 4>(a, st); break;
+        default: f2_launch<F_GELU, 128, 9, 4, 64, 2>(a, st);
+      }
     }
   }
 }
