@@ -149,9 +149,10 @@ int main(int argc, char** argv) {
     };
     if (only_v < 0 && has_ref) run("fused", [&] { launch_fused<bf16>(ab, 0); });
     if (fused2_ok(ab)) {
-      for (int v = 0; v < 6; ++v) {
+      for (int v = 0; v < 7; ++v) {
         if (only_v >= 0 && v != only_v) continue;
         if (ab.C == 256 && v >= 3) continue;
+        if (v == 6 && !(ab.mode == F_GATE && ab.C == 64)) continue;
         FusedArgs c = ab; c.dbg = v;
         char nm[16]; snprintf(nm, sizeof nm, "fused2.%d", v);
         run(nm, [&] { launch_fused2(c, 0); });

@@ -18,6 +18,6 @@ python3 tools/pmc_traffic.py $OUT \
   'fused2 mode=1 nimg=1 H=1088 W=1920 C=64 N1=128 N2=64 ln=1 ndst=0@@fused2_kernel<1, 64,' \
   'fused2 mode=1 nimg=1 H=544 W=960 C=128 N1=256 N2=128 ln=1 ndst=0@@fused2_kernel<1, 128,' \
   'dw nimg=1 H=272 W=480 C=640 mode=2 tok=0@@dw_rows_kernel:652800' \
-  'dw nimg=1 H=272 W=480 C=768 mode=0 tok=0@@dw_rows_kernel:1044480' \
+  'dw nimg=1 H=272 W=480 C=768 mode=0 tok=0@@dw_rows_kernel:783360' \
   > $OUT/pmc_traffic.json
 rc=$?; python3 -c "import json; d=json.load(open('$OUT/pmc_traffic.json')); print(d['source_hash'], json.dumps(d['per_tag'], indent=0)[:1500])"; exit $rc

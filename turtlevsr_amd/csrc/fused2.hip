@@ -83,9 +83,11 @@ struct F2L {
 // TPB tiles per block (TPB > 1: a block walks a run of consecutive tiles; the next tile's haloed
 // input is fetched into registers while the current one computes, and the per-channel tables are
 // loaded once per block instead of once per tile)
-template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE, int TPB = 1>
+// TG: per-channel tables (taps, LN / bias vectors) read from global memory (L2) at the start of each
+// walk instead of staged in LDS: 32 * N1M fewer LDS bytes per block, i.e. more blocks per CU
+template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE, int TPB = 1, bool TG = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void fused2_kernel(FusedArgs a) {
-  using L = F2L<CM, R, HPM, N1M, MODE == F_GATEOUT ? NW * R * 512 : 0>;
+  using L = F2L<CM, R, HPM, TG ? 0 : N1M, MODE == F_GATEOUT ? NW * R * 512 : 0>;
   constexpr int KS = CM / 32;                       // GEMM1 K steps
   constexpr int NT = NW * 64;
   __shared__ __attribute__((aligned(16))) char smem[L::BYTES];
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const float* zf = reinterpret_cast<const float*>(g_zero_f2);
 
   // ---- per-channel tables (taps, LN / bias vectors) -> LDS, once per block ----
-  {
+  if constexpr (!TG) {
     // taps: bf16 pairs [5][N1] (lo = tap 2i, hi = tap 2i + 1), straight copy
     const uint32_t* tg = a.dww2;
     for (int e = tid * 4; e < 5 * N1; e += NT * 4)
@@ -195,13 +197,25 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   // LN / bias -> window -> depthwise row `emit(orow, d)` (d = the lane's 4 channels r0 + 4 grp ..).
   auto walk = [&](int r0, const bf16x8 (&wf)[KS], auto&& emit) {
     const int ch = r0 + grp * 4;
-    const f32x4 s4 = *reinterpret_cast<const f32x4*>(sVec + ch);
-    const f32x4 tb = *reinterpret_cast<const f32x4*>(sVec + N1M + ch);
-    const f32x4 db = *reinterpret_cast<const f32x4*>(sVec + 2 * N1M + ch);
+    f32x4 s4, tb, db;
+    uint4 tp[5];
+    if constexpr (TG) {                            // unconditional loads (zero line for absent vectors)
+      s4 = ld_f4(a.ln && a.ln_s ? a.ln_s + ch : zf);
+      tb = ld_f4(a.ln && a.ln_t ? a.ln_t + ch : zf) + ld_f4(a.b1 ? a.b1 + ch : zf);
+      db = ld_f4(a.dwb ? a.dwb + ch : zf);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) tp[i] = ld16(a.dww2 + i * N1 + ch);
+    } else {
+      s4 = *reinterpret_cast<const f32x4*>(sVec + ch);
+      tb = *reinterpret_cast<const f32x4*>(sVec + N1M + ch);
+      db = *reinterpret_cast<const f32x4*>(sVec + 2 * N1M + ch);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) tp[i] = *reinterpret_cast<const uint4*>(sTap + i * N1 + ch);
+    }
     f32x4 wt[9];
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
-      const uint4 p = *reinterpret_cast<const uint4*>(sTap + i * N1 + ch);
+      const uint4 p = tp[i];
       const uint32_t u[4] = {p.x, p.y, p.z, p.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -461,7 +475,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
 // (MODE, C) -> (tile rows, waves, hidden per pass); units per pass chosen so every wave of a pass
 // gets the same number of units
-template <int MODE, int CM, int R, int NW, int HPM, int WPE, int TPB = 1>
+template <int MODE, int CM, int R, int NW, int HPM, int WPE, int TPB = 1, bool TG = false>
 static void f2_launch(const FusedArgs& a0, hipStream_t st) {
   FusedArgs a = a0;
   a.up = HPM / 16;
@@ -470,7 +484,7 @@ static void f2_launch(const FusedArgs& a0, hipStream_t st) {
   constexpr int N1M = (MODE == F_GATE || MODE == F_GATEOUT) ? 5 * CM : (MODE == F_GELU ? 2 * CM : (CM >= 256 ? 3 * CM : 6 * CM));
   const int64_t tiles = (int64_t)a.nimg * ((a.H + R - 1) / R) * ((a.W + F2_TX - 1) / F2_TX);
   const int64_t blocks = (tiles + TPB - 1) / TPB;
-  hipLaunchKernelGGL((fused2_kernel<MODE, CM, R, NW, HPM, N1M, WPE, TPB>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, a);
+  hipLaunchKernelGGL((fused2_kernel<MODE, CM, R, NW, HPM, N1M, WPE, TPB, TG>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, a);
 }
 
 bool fused2_ok(const FusedArgs& a) {
@@ -527,6 +541,7 @@ void launch_fused2(const FusedArgs& a, hipStream_t st) {
         case 1: f2_launch<F_GATE, 64, 9, 4, 64, 3>(a, st); break;
         case 2: f2_launch<F_GATE, 64, 12, 4, 64, 2>(a, st); break;
         case 3: f2_launch<F_GATE, 64, 9, 4, 64, 3, 4>(a, st); break;   // 4 tiles per block, next tile prefetched
+        case 6: f2_launch<F_GATE, 64, 6, 4, 64, 3, 1, true>(a, st); break;   // tables from L2 (spills: 924 us)
         case 4: f2_launch<F_GATE, 64, 6, 4, 64, 4>(a, st); break;
         case 5: f2_launch<F_GATE, 64, 3, 4, 64, 4>(a, st); break;
         default: f2_launch<F_GATE, 64, 6, 4, 64, 3>(a, st);           // 46 KB: 3 blocks per CU
