@@ -222,6 +222,23 @@ struct PwdwArgs {                  // pwdw.hip: [LN ->] pw (C -> N1) -> dw3x3 [-
 bool pwdw_ok(const PwdwArgs& a);
 void launch_pwdw(const PwdwArgs& a, hipStream_t st);
 
+struct DwGemmArgs {                // dwgemm.hip: out = res + b + W [gelu(dw(x1)) * dw(x2) | dw(x)], bf16
+  const void* in; int64_t ldi; int offi;   // hidden map, pixel-major [nimg][H][W][ldi]; x1 at offi, x2 at offi + K
+  const void* dww16; const float* dwb;     // [9][NH*K] bf16 tap-major, [NH*K] fp32 or null
+  int gate;                        // 1: GatedFeedForward gate (NH = 2), 0: plain depthwise
+  int nimg, H, W, K;               // K = GEMM depth = depthwise output channels
+  const void* w; int64_t ldw; int64_t wstride; int wdiv;   // [N][ldw] bf16; per-image sets if wstride
+  int N;
+  const float* bias;               // [N] or null
+  const void* res; int64_t ldr; int offr;
+  void* out; int64_t ldo; int offo;
+  const float* zeros;              // >= 16 zero floats
+  int dbg;                         // tools/dgbench ablations (0 in the product path)
+};
+bool dwgemm_ok(const DwGemmArgs& g);
+int64_t dwgemm_blocks(const DwGemmArgs& g);
+void launch_dwgemm(const DwGemmArgs& g, hipStream_t st);
+
 void launch_cast_f32(const float* src, void* dst, int64_t n, int to_bf16, hipStream_t st);
 
 // t0 StateAlignBlock (turtle_arch.py:459-533), t0.hip

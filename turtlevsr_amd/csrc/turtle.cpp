@@ -205,7 +205,7 @@ struct GemmW {
   size_t tb = NONE;   // LN GEMMs: W b_ln + bias (the vendor path's bias after an explicit LN prologue)
   int N = 0, K = 0; bool ln = false;
 };
-struct DwW { size_t w = NONE, bias = NONE, w2 = NONE; int C = 0; };   // w2: bf16 tap pairs [5][C] (u32)
+struct DwW { size_t w = NONE, bias = NONE, w2 = NONE, w16 = NONE; int C = 0; };   // w2: bf16 tap pairs [5][C] (u32); w16: bf16 [9][C]
 struct BlockW {
   GemmW a_in, a_out, q2, k2, kv, f_in, f_out, t0_kpw;   // t0_kpw: W_k of the t0 aligner (pos term)
   DwW t0_kdw;                                           // t0 k-half depthwise taps without bias
@@ -255,6 +255,14 @@ struct Packer {
     return u32(o);
   }
   // storage-typed matrix; returns offset and writes back the rounded values (for LN rowsums)
+  // depthwise 3x3 table [9][C] as bf16 (the dwgemm kernel's block-diagonal MFMA operand)
+  size_t bf16tab(const std::vector<double>& w9) {
+    size_t o = align();
+    host.resize(o + w9.size() * 2);
+    uint16_t* p = reinterpret_cast<uint16_t*>(host.data() + o);
+    for (size_t i = 0; i < w9.size(); ++i) p[i] = bf16_bits(w9[i]);
+    return o;
+  }
   size_t stor(std::vector<double>& v) {
     size_t o = align();
     if (bf16) {
@@ -306,6 +314,8 @@ struct TurtleHandle {
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
+  bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
+  int dwgemm_min_blocks = 384;                        // one 160 KB block per CU: below ~1.5 rounds (latent level) dw + GEMM is faster
   bool blaslt = getenv("TURTLE_NO_BLASLT") == nullptr; // hipBLASLt for the plain projections it wins (blas.cpp)
   BlasCtx* blas = nullptr;                            // created on the first bf16 forward
   bool blas_failed = false;                           // creation failed once: never retried
@@ -370,7 +380,7 @@ static DwW pack_dw(TurtleHandle* h, Packer& pk, const std::string& n, int c0, in
   for (int c = 0; c < C; ++c)
     for (int t = 0; t < taps; ++t) o[(size_t)t * C + c] = w[(size_t)(c0 + c) * taps + t];
   DwW d; d.C = C; d.w = pk.f32(o);
-  if (taps == 9) d.w2 = pk.dw_pairs(o, C);
+  if (taps == 9) { d.w2 = pk.dw_pairs(o, C); d.w16 = pk.bf16tab(o); }
   if (with_bias && has(h, n + ".bias")) {
     const auto& b = W(h, n + ".bias");
     d.bias = pk.f32(std::vector<double>(b.begin() + c0, b.begin() + c0 + C));
@@ -398,6 +408,7 @@ static DwW pack_dw_cat(TurtleHandle* h, Packer& pk, const std::vector<std::strin
   }
   DwW d; d.C = Ct; d.w = pk.f32(o);
   d.w2 = pk.dw_pairs(o, Ct);
+  d.w16 = pk.bf16tab(o);
   if (any_bias) d.bias = pk.f32(bias);
   return d;
 }
@@ -774,6 +785,28 @@ struct Runner {
     tag("pwdw gate=%d nimg=%d H=%d W=%d C=%d N1=%d", gate, nimg, H, Wd, C, w1.N);
     launch(TURTLE_K_FUSED, ES * px * (C + hid), 2.0 * px * C * w1.N + 18.0 * px * w1.N, [&] { launch_pwdw(p, st); });
   }
+  // out (+)= W [gelu(dw(x1)) * dw(x2) | dw(x)] + bias (+ res) with the depthwise computed in the
+  // GEMM's operand prologue (dwgemm.hip); returns false (nothing launched) where not eligible
+  bool dwgemm(const DwW& dwp, int gate, const T* in, int64_t ldi, int offi, int nimg, int H, int Wd, int K,
+              const void* wptr, int64_t ldw, int64_t wstride, int N, const float* bias, const T* res, int64_t ldr,
+              T* out, int64_t ldo) {
+    if (ES != 2 || !h->dwgemm || dwp.C != (gate ? 2 * K : K)) return false;
+    DwGemmArgs a{};
+    a.in = in; a.ldi = ldi; a.offi = offi; a.dww16 = h->ptr(dwp.w16); a.dwb = h->fptr(dwp.bias); a.gate = gate;
+    a.nimg = nimg; a.H = H; a.W = Wd; a.K = K;
+    a.w = wptr; a.ldw = ldw; a.wstride = wstride; a.wdiv = 1; a.N = N; a.bias = bias;
+    a.res = res; a.ldr = ldr; a.offr = 0; a.out = out; a.ldo = ldo; a.offo = 0;
+    a.zeros = h->fptr(h->mw.zeros);
+    if (dwgemm_blocks(a) < h->dwgemm_min_blocks) return false;
+    if (dry()) return true;
+    if (!dwgemm_ok(a)) return false;
+    const double px = (double)nimg * H * Wd, cin = gate ? 2.0 * K : K;
+    const double nset = wstride ? nimg : 1.0;
+    tag("dwgemm gate=%d nimg=%d H=%d W=%d K=%d N=%d", gate, nimg, H, Wd, K, N);
+    launch(TURTLE_K_GEMM, ES * (px * cin + nset * (double)N * K + px * N * (res ? 2 : 1)),
+           2.0 * px * N * K + 18.0 * px * cin, [&] { launch_dwgemm(a, st); });
+    return true;
+  }
   static FusedDst dst_map(void* p, int64_t ld, int off, int cbeg, int cend) {
     return FusedDst{p, ld, off, cbeg, cend, cend - cbeg, 0, 0};
   }
@@ -877,10 +910,13 @@ struct Runner {
         gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
       } else {
         T* t1 = buf(P * 2 * hd);
-        T* t2 = buf(P * hd);
+        T* t2 = buf(P * hd);   // dw + gate output of the unfolded path
         gemm(bw.f_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * hd, 0);
-        dw(bw.f_dw, t1, 2 * hd, 0, t2, hd, 0, B, H, Wd, DW_GATE);
-        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
+        if (!dwgemm(bw.f_dw, 1, t1, 2 * hd, 0, B, H, Wd, hd, h->ptr(bw.f_out.w), hd, 0, c, h->fptr(bw.f_out.bias),
+                    x, c, x, c)) {
+          dw(bw.f_dw, t1, 2 * hd, 0, t2, hd, 0, B, H, Wd, DW_GATE);
+          gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
+        }
       }
     } else {
       T* t1 = buf(P * 2 * c);
@@ -1330,6 +1366,8 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "panel_gemm") h->panel = value != 0;
     else if (n == "dw_rows") h->dw_rows = value != 0;
     else if (n == "blaslt") h->blaslt = value != 0;
+    else if (n == "dwgemm") h->dwgemm = value != 0;
+    else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
     else if (n == "gemm_ar") h->gemm_ar = value != 0;
