@@ -239,6 +239,16 @@ bool dwgemm_ok(const DwGemmArgs& g);
 int64_t dwgemm_blocks(const DwGemmArgs& g);
 void launch_dwgemm(const DwGemmArgs& g, hipStream_t st);
 
+struct FfnArgs {                   // ffn.hip: out = x + g2 * (W2 gelu(LN-folded W1 x) + b2), bf16, C in {64, 128}
+  const void* x; void* out;        // [M][C] pixel-major; out may alias x
+  int64_t M; int C;
+  const void* w1f; const void* w2f;   // W1' [2C][C] / W2 [C][2C] in MFMA A-fragment order (turtle.cpp pack_ffn_frags)
+  const float* s1; const float* t1;   // [2C] rowsum(W1'), W1 b_ln + b1 (null: 0)
+  const float* b2; const float* g2;   // [C] conv5 bias, gamma (null: 0 / 1)
+};
+bool ffn_ok(const FfnArgs& a);
+void launch_ffn(const FfnArgs& a, hipStream_t st);
+
 void launch_cast_f32(const float* src, void* dst, int64_t n, int to_bf16, hipStream_t st);
 
 // t0 StateAlignBlock (turtle_arch.py:459-533), t0.hip

@@ -210,6 +210,8 @@ struct BlockW {
   GemmW a_in, a_out, q2, k2, kv, f_in, f_out, t0_kpw;   // t0_kpw: W_k of the t0 aligner (pos term)
   DwW t0_kdw;                                           // t0 k-half depthwise taps without bias
   DwW a_dw, sab_qk_dw, sab_v_dw, fhr_dw, kv_dw, f_dw, chm_dw6;
+  DwW a_dw_qk, a_dw_v;
+  size_t ffn_w1f = NONE, ffn_w2f = NONE;                // FeedForward conv4' / conv5 in MFMA fragment order (ffn.hip)                                  // channel attention: qkv_dwconv split (q,k | v) for the dwgemm v path
   size_t q2_win = NONE, q2_winb = NONE, k2_win = NONE, k2_winb = NONE, sab_tau = NONE;
   size_t wp = NONE, po_bias = NONE, tau = NONE;   // channel-attention projection (fp32) + temperature
 };
@@ -315,6 +317,8 @@ struct TurtleHandle {
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
+  bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
+  bool dwgemm_attn = true;                            // channel attention: v's depthwise inside the W_eff GEMM (dwgemm.hip)
   int dwgemm_min_blocks = 384;                        // one 160 KB block per CU: below ~1.5 rounds (latent level) dw + GEMM is faster
   bool blaslt = getenv("TURTLE_NO_BLASLT") == nullptr; // hipBLASLt for the plain projections it wins (blas.cpp)
   BlasCtx* blas = nullptr;                            // created on the first bf16 forward
@@ -428,6 +432,38 @@ static GemmW pack_conv3(TurtleHandle* h, Packer& pk, const std::string& n, int C
   return g;
 }
 
+// FeedForward weights for ffn.hip: the bf16 matrices already packed at host offsets w1 ([2C][C],
+// LN-folded) and w2 ([C][2C]) re-laid as 16x16x32 MFMA A fragments (1 KB: lane l, 8 bf16 at l * 16).
+// W1 fragment (hc, s, ks): row l & 15 = 4 g' + e' -> hidden 32 hc + 8 g' + 4 s + e', k = 32 ks + 8 (l >> 4) + j;
+// W2 fragment (hc, t): row -> output 32 (t >> 1) + 8 g' + 4 (t & 1) + e', k = 32 hc + 8 (l >> 4) + j
+static void pack_ffn_frags(Packer& pk, size_t w1, size_t w2, int C, size_t& o1, size_t& o2) {
+  const int H = 2 * C, KS1 = C / 32, HC = H / 32, T2 = C / 16;
+  std::vector<uint16_t> a((size_t)H * C), b((size_t)C * H), fa(a.size()), fb(b.size());
+  std::memcpy(a.data(), pk.host.data() + w1, a.size() * 2);
+  std::memcpy(b.data(), pk.host.data() + w2, b.size() * 2);
+  for (int hc = 0; hc < HC; ++hc)
+    for (int s = 0; s < 2; ++s)
+      for (int ks = 0; ks < KS1; ++ks)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const int m = l & 15, hrow = 32 * hc + 8 * (m >> 2) + 4 * s + (m & 3), k = 32 * ks + 8 * (l >> 4) + j;
+            fa[((((size_t)(hc * 2 + s) * KS1 + ks) * 64 + l) * 8) + j] = a[(size_t)hrow * C + k];
+          }
+  for (int hc = 0; hc < HC; ++hc)
+    for (int t = 0; t < T2; ++t)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 8; ++j) {
+          const int m = l & 15, orow = 32 * (t >> 1) + 8 * (m >> 2) + 4 * (t & 1) + (m & 3), k = 32 * hc + 8 * (l >> 4) + j;
+          fb[(((size_t)(hc * T2 + t) * 64 + l) * 8) + j] = b[(size_t)orow * H + k];
+        }
+  o1 = pk.align();
+  pk.host.resize(o1 + fa.size() * 2);
+  std::memcpy(pk.host.data() + o1, fa.data(), fa.size() * 2);
+  o2 = pk.align();
+  pk.host.resize(o2 + fb.size() * 2);
+  std::memcpy(pk.host.data() + o2, fb.data(), fb.size() * 2);
+}
+
 static void pack_all(TurtleHandle* h) {
   Arch& A = h->arch;
   Packer pk; pk.bf16 = h->bf16();
@@ -464,6 +500,8 @@ static void pack_all(TurtleHandle* h) {
       } else if (b.attn == TURTLE_ATTN_CHANNEL || b.attn == TURTLE_ATTN_FHR) {
         bw.a_in = pack_gemm(h, pk, dvec(W(h, a + ".qkv.weight")), 3 * c, c, n1, opt_bias(h, a + ".qkv.bias"));
         bw.a_dw = pack_dw(h, pk, a + ".qkv_dwconv", 0, 3 * c);
+        bw.a_dw_qk = pack_dw(h, pk, a + ".qkv_dwconv", 0, 2 * c);
+        bw.a_dw_v = pack_dw(h, pk, a + ".qkv_dwconv", 2 * c, c);
         bw.wp = pk.f32(dvec(W(h, a + ".project_out.weight")));
         if (has(h, a + ".project_out.bias")) bw.po_bias = pk.f32(dvec(W(h, a + ".project_out.bias")));
         bw.tau = pk.f32(dvec(W(h, a + ".temperature")));
@@ -537,6 +575,7 @@ static void pack_all(TurtleHandle* h) {
         bw.f_in = pack_gemm(h, pk, dvec(W(h, f + ".conv4.weight")), 2 * c, c, n2, dvec(W(h, f + ".conv4.bias")));
         bw.f_out = pack_gemm(h, pk, dvec(W(h, f + ".conv5.weight")), c, 2 * c, "", dvec(W(h, f + ".conv5.bias")));
         bw.f_out.scale = pk.f32(dvec(W(h, f + ".gamma")));
+        if (pk.bf16 && (c == 64 || c == 128)) pack_ffn_frags(pk, bw.f_in.w, bw.f_out.w, c, bw.ffn_w1f, bw.ffn_w2f);
       }
       bws.push_back(bw);
     }
@@ -800,12 +839,39 @@ struct Runner {
     if (dwgemm_blocks(a) < h->dwgemm_min_blocks) return false;
     if (dry()) return true;
     if (!dwgemm_ok(a)) return false;
+    return dwgemm_launch(a);
+  }
+  // shape-only eligibility of the channel-attention v path (decided before qkv is produced, and the
+  // same in the sizing dry run): alignment is guaranteed by the arena (256 B) and widths % 32
+  bool can_dwgemm_v(int c, int nimg, int H, int Wd) const {
+    if (ES != 2 || !h->dwgemm || !h->dwgemm_attn || c % 32 || c > 512) return false;
+    if ((int64_t)H * Wd * 3 * c >= ((int64_t)1 << 31)) return false;   // dwgemm_ok: 32-bit input offsets
+    DwGemmArgs a{};
+    a.nimg = nimg; a.H = H; a.W = Wd; a.N = c;
+    return dwgemm_blocks(a) >= h->dwgemm_min_blocks;
+  }
+  bool dwgemm_launch(DwGemmArgs& a) {
+    const int gate = a.gate, K = a.K, N = a.N, nimg = a.nimg, H = a.H, Wd = a.W;
+    const bool res = a.res != nullptr;
+    const int64_t wstride = a.wstride;
     const double px = (double)nimg * H * Wd, cin = gate ? 2.0 * K : K;
     const double nset = wstride ? nimg : 1.0;
     tag("dwgemm gate=%d nimg=%d H=%d W=%d K=%d N=%d", gate, nimg, H, Wd, K, N);
     launch(TURTLE_K_GEMM, ES * (px * cin + nset * (double)N * K + px * N * (res ? 2 : 1)),
            2.0 * px * N * K + 18.0 * px * cin, [&] { launch_dwgemm(a, st); });
     return true;
+  }
+  // FeedForward in one kernel (ffn.hip): bf16, widths 64 / 128 (shape-only, same in the dry run)
+  bool can_ffn(int c) const { return ES == 2 && h->ffn && (c == 64 || c == 128); }
+  void ffn(const BlockW& bw, T* x, int64_t P, int c) {
+    if (dry()) return;
+    FfnArgs f{};
+    f.x = x; f.out = x; f.M = P; f.C = c;
+    f.w1f = h->ptr(bw.ffn_w1f); f.w2f = h->ptr(bw.ffn_w2f);
+    f.s1 = h->fptr(bw.f_in.s); f.t1 = h->fptr(bw.f_in.tb); f.b2 = h->fptr(bw.f_out.bias); f.g2 = h->fptr(bw.f_out.scale);
+    if (!bw.f_in.ln || !ffn_ok(f)) TFAIL(TURTLE_EINVAL, "ffn: FeedForward weights not packed for the fused kernel");
+    tag("ffn M=%lld C=%d", (long long)P, c);
+    launch(TURTLE_K_FUSED, ES * 2.0 * P * c, 2.0 * P * (2.0 * c * c * 2), [&] { launch_ffn(f, st); });
   }
   static FusedDst dst_map(void* p, int64_t ld, int off, int cbeg, int cend) {
     return FusedDst{p, ld, off, cbeg, cend, cend - cbeg, 0, 0};
@@ -815,7 +881,8 @@ struct Runner {
 
   // channel attention core: Gram over (q, key segments), softmax, W_eff, then out = x + W_eff [v srcs]
   void chan_attn(const BlockW& bw, const Blk& b, const T* q, int64_t ldq, int qoff, const std::vector<Seg>& segs,
-                 const SrcList& vsrc, int HW, int Wimg, T* x, float* kinv, int cur_seg) {
+                 const SrcList& vsrc, int HW, int Wimg, T* x, float* kinv, int cur_seg,
+                 const DwW* vdw = nullptr, const T* vraw = nullptr, int64_t ldv = 0, int offv = 0) {
     const int c = b.dim, ch = c / b.heads, nseg = (int)segs.size(), ncol = nseg * ch;
     if (ncol > 512 || nseg > TURTLE_MAX_SEG) TFAIL(TURTLE_EINVAL, "channel attention: more than 512 key columns");
     // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each, whole
@@ -860,6 +927,13 @@ struct Runner {
       launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot + 4.0 * B * b.heads * ch * ncol, 2.0 * B * c * (double)b.heads * ncol * ch,
              [&] { launch_weff<T>(we, st); });
     }
+    if (vdw) {
+      // v's depthwise folded into the W_eff GEMM's operand prologue (dwgemm.hip): out = x + W_eff dw(v) + b
+      if (!dwgemm(*vdw, 0, vraw, ldv, offv, B, HW / Wimg, Wimg, c, weff, c, (int64_t)c * c, c, h->fptr(bw.po_bias), x, c,
+                  x, c))
+        TFAIL(TURTLE_EINVAL, "channel attention: dwgemm v path not eligible");
+      return;
+    }
     GemmW pw; pw.N = c; pw.K = vsrc.Ktot;
     gemm(pw, vsrc, (int64_t)B * HW, HW, Wimg, x, c, 0, x, c, 0, 0, STORE_NHWC, weff, (int64_t)c * vsrc.Ktot, 1, c,
          h->fptr(bw.po_bias));
@@ -884,10 +958,20 @@ struct Runner {
       }
     } else if (b.attn == TURTLE_ATTN_CHANNEL || (b.attn == TURTLE_ATTN_FHR && b.cache_slot < 0)) {
       T* t2 = buf(P * 3 * c);
-      qkv_dw(bw, x, c, t2, B, H, Wd);
       const int ch = c / b.heads;
       std::vector<Seg> segs{{t2, 3 * c, c, ch, 1, 0, 1, 0, ch}};
-      chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t2, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1);
+      if (!can_fuse(c, F_DWONLY, 3 * c, 0) && !can_fused2_wide(c, F_DWONLY, 3 * c, 0) && !can_pwdw(c, 3 * c, false) &&
+          can_dwgemm_v(c, B, H, Wd)) {
+        // qkv GEMM, depthwise of q,k only; v's depthwise runs inside the W_eff GEMM (dwgemm.hip)
+        T* t1 = buf(P * 3 * c);
+        gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
+        dw(bw.a_dw_qk, t1, 3 * c, 0, t2, 3 * c, 0, B, H, Wd, DW_PLAIN);
+        chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t1, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1, &bw.a_dw_v, t1, 3 * c,
+                  2 * c);
+      } else {
+        qkv_dw(bw, x, c, t2, B, H, Wd);
+        chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t2, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1);
+      }
     } else if (b.attn == TURTLE_ATTN_FHR) {
       fhr(b, bw, x, H, Wd);
     } else if (b.attn == TURTLE_ATTN_CHM) {
@@ -918,6 +1002,8 @@ struct Runner {
           gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
         }
       }
+    } else if (can_ffn(c)) {
+      ffn(bw, x, P, c);
     } else {
       T* t1 = buf(P * 2 * c);
       gemm(bw.f_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * c, 0, nullptr, 0, 0, /*gelu*/ 1);
@@ -1367,6 +1453,8 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "dw_rows") h->dw_rows = value != 0;
     else if (n == "blaslt") h->blaslt = value != 0;
     else if (n == "dwgemm") h->dwgemm = value != 0;
+    else if (n == "dwgemm_attn") h->dwgemm_attn = value != 0;
+    else if (n == "ffn") h->ffn = value != 0;
     else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
