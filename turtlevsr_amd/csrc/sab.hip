@@ -653,12 +653,16 @@ constexpr int SM_T = 8, SM_S = 16;                 // query tile / key square si
 constexpr int SM_E = 64;                           // D elements per chunk
 constexpr int SM_RV = SM_E * 2 + 16;               // staged V row bytes (padded)
 constexpr int SM_RO = SM_E + 4;                    // output staging row (floats)
-constexpr int SM_LDS = 2 * 256 * SM_RV + 64 * SM_RO * 4 + 64 * SAB_K * 8;
+// DB: V chunk double-buffered in LDS and the tail rows prefetched one chunk ahead (1 block per CU,
+// one wave per SIMD); !DB: one V buffer (the register staging is the second stage), tail rows
+// fetched at the top of their own chunk, <= 256 registers: two blocks per CU
+template <bool DB> constexpr int sm_lds() { return (DB ? 2 : 1) * 256 * SM_RV + 64 * SM_RO * 4 + 64 * SAB_K * 8; }
 
-__global__ __launch_bounds__(256, 1) void sab_av_mfma_kernel(SabGatherArgs a, int nsplit) {
+template <bool DB>
+__global__ __launch_bounds__(256, DB ? 1 : 2) void sab_av_mfma_kernel(SabGatherArgs a, int nsplit) {
   extern __shared__ __attribute__((aligned(16))) char sm[];
-  char* sV = sm;                                   // [2][256][SM_RV]
-  float* sO = reinterpret_cast<float*>(sm + 2 * 256 * SM_RV);   // [64][SM_RO]
+  char* sV = sm;                                   // [1 or 2][256][SM_RV]
+  float* sO = reinterpret_cast<float*>(sm + (DB ? 2 : 1) * 256 * SM_RV);   // [64][SM_RO]
   int* sTi = reinterpret_cast<int*>(sO + 64 * SM_RO);           // [64][5] tail keys
   float* sTw = reinterpret_cast<float*>(sTi + 64 * SAB_K);      // [64][5] tail weights
   const int D = a.ws * a.ws * a.C, nch = D / SM_E;
@@ -762,7 +766,7 @@ __global__ __launch_bounds__(256, 1) void sab_av_mfma_kernel(SabGatherArgs a, in
   // tail rows of this thread's query / element group, fetched one chunk ahead (their L2 latency
   // was the critical path of a chunk)
   const int tq = tid >> 2, teg = (tid & 3) * 16;
-  uint4 tcur[2 * SAB_K], tnext[2 * SAB_K];
+  uint4 tcur[2 * SAB_K], tnext[DB ? 2 * SAB_K : 1];
   auto load_tail = [&](int chn, uint4 (&r)[2 * SAB_K]) {
 #pragma unroll
     for (int x = 0; x < SAB_K; ++x) {
@@ -773,15 +777,16 @@ __global__ __launch_bounds__(256, 1) void sab_av_mfma_kernel(SabGatherArgs a, in
   };
   if (ch_beg < ch_end) {
     load_v(ch_beg);
-    load_tail(ch_beg, tcur);
+    if constexpr (DB) load_tail(ch_beg, tcur);
     store_v(0);
   }
   __syncthreads();
   for (int chn = ch_beg; chn < ch_end; ++chn) {
-    const int buf = (chn - ch_beg) & 1;
+    const int buf = DB ? (chn - ch_beg) & 1 : 0;
+    if constexpr (!DB) load_tail(chn, tcur);      // lands during this chunk's MFMAs
     if (chn + 1 < ch_end) {
       load_v(chn + 1);
-      load_tail(chn + 1, tnext);
+      if constexpr (DB) load_tail(chn + 1, tnext);
     }
     // MFMA: wave w owns elements w*16 .. +15 of the chunk, all 64 queries
     f32x4 acc[4];
@@ -802,7 +807,10 @@ __global__ __launch_bounds__(256, 1) void sab_av_mfma_kernel(SabGatherArgs a, in
     for (int qt = 0; qt < 4; ++qt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) sO[(qt * 16 + g16 * 4 + i) * SM_RO + wid * 16 + li] = acc[qt][i];
-    __syncthreads();
+    __syncthreads();                               // (!DB: every wave's V reads of this chunk are done)
+    if constexpr (!DB) {
+      if (chn + 1 < ch_end) store_v(0);
+    }
     // tail + store: thread = (query tid / 4, 16 elements (tid % 4) * 16)
     {
       const int ql = tq, eg = teg;
@@ -831,10 +839,12 @@ __global__ __launch_bounds__(256, 1) void sab_av_mfma_kernel(SabGatherArgs a, in
         s1.store(dst + 8);
       }
     }
-    if (chn + 1 < ch_end) {
-      store_v(buf ^ 1);
+    if constexpr (DB) {
+      if (chn + 1 < ch_end) {
+        store_v(buf ^ 1);
 #pragma unroll
-      for (int x = 0; x < 2 * SAB_K; ++x) tcur[x] = tnext[x];
+        for (int x = 0; x < 2 * SAB_K; ++x) tcur[x] = tnext[x];
+      }
     }
     __syncthreads();
   }
@@ -852,10 +862,12 @@ void launch_sab_av_mfma(const SabGatherArgs& a, hipStream_t st) {
   const int nsplit = std::max(1, std::min(nch, (1024 + tiles - 1) / tiles));
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_av_mfma_kernel), hipFuncAttributeMaxDynamicSharedMemorySize, SM_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_av_mfma_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize, sm_lds<true>());
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_av_mfma_kernel<false>), hipFuncAttributeMaxDynamicSharedMemorySize, sm_lds<false>());
     attr = true;
   }
-  hipLaunchKernelGGL(sab_av_mfma_kernel, dim3((unsigned)(tiles * nsplit)), dim3(256), SM_LDS, st, a, nsplit);
+  if (a.db) hipLaunchKernelGGL(sab_av_mfma_kernel<true>, dim3((unsigned)(tiles * nsplit)), dim3(256), sm_lds<true>(), st, a, nsplit);
+  else hipLaunchKernelGGL(sab_av_mfma_kernel<false>, dim3((unsigned)(tiles * nsplit)), dim3(256), sm_lds<false>(), st, a, nsplit);
 }
 
 template void launch_sab_score<float>(const SabScoreArgs&, hipStream_t);

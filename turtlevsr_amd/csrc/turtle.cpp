@@ -314,6 +314,7 @@ struct TurtleHandle {
   bool attn_fuse = false;                             // row softmax folded into the W_eff kernel (attn.hip): slower so far
   bool sab_tile = false;                              // query-tiled VALU SAB gather (sab.hip)
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
+  bool sab_db = false;                                // SAB A.v: double-buffered 1-block/CU variant (else 2 blocks / CU)
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
@@ -1216,7 +1217,7 @@ struct Runner {
       sa.tau = h->fptr(bw.sab_tau); sa.topv = topv; sa.topi = topi; sa.ballv = ballv;
       SabGatherArgs ga{};
       ga.B = B; ga.T = NT; ga.N = N; ga.th = th; ga.tw = tw; ga.ws = ws; ga.C = c;
-      ga.cnt = ccnt; ga.ci = cidx; ga.cw = cwt; ga.ballw = ballv; ga.out = xs;
+      ga.cnt = ccnt; ga.ci = cidx; ga.cw = cwt; ga.ballw = ballv; ga.out = xs; ga.db = h->sab_db ? 1 : 0;
       for (int t = 0; t < NT; ++t) {
         if (t < Tin) {
           sa.k[t] = kin + (int64_t)t * N * d2; sa.k_bstride[t] = (int64_t)Tin * N * d2;
@@ -1455,6 +1456,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "dwgemm") h->dwgemm = value != 0;
     else if (n == "dwgemm_attn") h->dwgemm_attn = value != 0;
     else if (n == "ffn") h->ffn = value != 0;
+    else if (n == "sab_db") h->sab_db = value != 0;
     else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
