@@ -178,6 +178,20 @@ TURTLE_DEV float gelu_bf16(float x) {
   return gelu_fast(x);
 #endif
 }
+// two tanh-form GELUs with the polynomial / scaling steps as packed f32 pairs (v_pk_mul / v_pk_fma,
+// identical roundings to gelu_tanh per element); the bf16 kernels' GELU when TURTLE_BF16_GELU_TANH
+TURTLE_DEV f32x2 gelu_tanh2(f32x2 x) {
+  const f32x2 u = x * __builtin_elementwise_fma(f32x2{-0.10294324f, -0.10294324f}, x * x, f32x2{-2.3022082f, -2.3022082f});
+  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(u.x), __builtin_amdgcn_exp2f(u.y)} + f32x2{1.f, 1.f};
+  return x * f32x2{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+}
+TURTLE_DEV f32x2 gelu_bf16_2(f32x2 x) {
+#if TURTLE_BF16_GELU_TANH
+  return gelu_tanh2(x);
+#else
+  return f32x2{gelu_fast(x.x), gelu_fast(x.y)};
+#endif
+}
 // GELU of a kernel computing in storage type T: gelu_bf16 for bf16 storage, libm erf for fp32
 template <typename T>
 TURTLE_DEV float gelu_t(float x) {

@@ -238,8 +238,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       const int yg = y0 - 1 + hr;
       const float m = (yg >= 0 && yg < a.H) ? colok : 0.f;
       const float rs = m * st.y, c0 = -st.x * st.y * m;
+      // packed f32 pairs (v_pk_mul / v_pk_fma: two lanes' values per VALU issue, same roundings)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) w[q] = fmaf(rs, acc[q], fmaf(c0, s4[q], m * tb[q]));
+      for (int h = 0; h < 2; ++h) {
+        const f32x2 r = __builtin_elementwise_fma(f32x2{rs, rs}, f32x2{acc[2 * h], acc[2 * h + 1]},
+                                                  __builtin_elementwise_fma(f32x2{c0, c0}, f32x2{s4[2 * h], s4[2 * h + 1]},
+                                                                            f32x2{m, m} * f32x2{tb[2 * h], tb[2 * h + 1]}));
+        w[2 * h] = r.x; w[2 * h + 1] = r.y;
+      }
       // pin the row here in the asm order: its first DPP read (as row y+1 of the next depthwise
       // row) comes >= 24 VALU instructions later (the DPP read-after-VALU-write hazard needs 2)
 #pragma unroll
@@ -284,7 +290,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
           for (int q = 0; q < 4; ++q) fmac_shr1(d[q], w[q], wt[t0][q]);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) d[q] = fmaf(wt[t0 + 1][q], w[q], d[q]);
+          for (int h = 0; h < 2; ++h) {   // centre tap: packed pairs
+            const f32x2 r = __builtin_elementwise_fma(f32x2{wt[t0 + 1][2 * h], wt[t0 + 1][2 * h + 1]}, f32x2{w[2 * h], w[2 * h + 1]},
+                                                      f32x2{d[2 * h], d[2 * h + 1]});
+            d[2 * h] = r.x; d[2 * h + 1] = r.y;
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) fmac_shl1(d[q], w[q], wt[t0 + 2][q]);
         };
@@ -357,7 +367,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       walk(u * 16, wa, [&](int orow, const f32x4& d) {
         bf16x4 g;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) g[q] = (bf16)gelu_t<bf16>(d[q]);
+        for (int h = 0; h < 2; ++h) {
+              const f32x2 r = gelu_bf16_2(f32x2{d[2 * h], d[2 * h + 1]});
+              g[2 * h] = (bf16)r.x; g[2 * h + 1] = (bf16)r.y;
+            }
         *reinterpret_cast<bf16x4*>(park + orow * 512) = g;
       });
       if (u + NW < nunit) load_w1(wa, (u + NW) * 16);
@@ -368,7 +381,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         if (!out_lane || y >= a.H) return;
         bf16x4 g;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) g[q] = (bf16)((float)g1[q] * d[q]);
+        for (int h = 0; h < 2; ++h) {
+              const f32x2 r = f32x2{(float)g1[2 * h], (float)g1[2 * h + 1]} * f32x2{d[2 * h], d[2 * h + 1]};
+              g[2 * h] = (bf16)r.x; g[2 * h + 1] = (bf16)r.y;
+            }
         *reinterpret_cast<bf16x4*>(dp + ((int64_t)img * a.H + y) * a.W * D.ld + colpart) = g;
       });
     }
@@ -415,7 +431,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
           auto emit_x1 = [&](int orow, const f32x4& d) {         // x1 / plain: park gelu(d)
             bf16x4 g;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) g[q] = (bf16)gelu_t<bf16>(d[q]);
+            for (int h = 0; h < 2; ++h) {
+              const f32x2 r = gelu_bf16_2(f32x2{d[2 * h], d[2 * h + 1]});
+              g[2 * h] = (bf16)r.x; g[2 * h + 1] = (bf16)r.y;
+            }
             *reinterpret_cast<bf16x4*>(gcol + (orow * 16 + px) * L::GP) = g;
           };
           auto emit_x2 = [&](int orow, const f32x4& d) {         // x2: G = gelu(x1) * x2
@@ -423,7 +442,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             const bf16x4 g1 = *p;
             bf16x4 g;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) g[q] = (bf16)((float)g1[q] * d[q]);
+            for (int h = 0; h < 2; ++h) {
+              const f32x2 r = f32x2{(float)g1[2 * h], (float)g1[2 * h + 1]} * f32x2{d[2 * h], d[2 * h + 1]};
+              g[2 * h] = (bf16)r.x; g[2 * h + 1] = (bf16)r.y;
+            }
             *p = g;
           };
           if constexpr (h == 0) walk(walk_r0(u, 0), wa, emit_x1);
