@@ -218,8 +218,9 @@ __global__ __launch_bounds__(DG_NT, 1) void dwgemm_kernel(DwGemmArgs g) {
       uint32_t pk[2];
 #pragma unroll
       for (int e2 = 0; e2 < 2; ++e2) {
-        float r0 = d[cb][0][2 * e2], r1 = d[cb][0][2 * e2 + 1];
-        if constexpr (NH == 2) { r0 = gelu_bf16(r0) * d[cb][1][2 * e2]; r1 = gelu_bf16(r1) * d[cb][1][2 * e2 + 1]; }
+        f32x2 r = f32x2{d[cb][0][2 * e2], d[cb][0][2 * e2 + 1]};
+        if constexpr (NH == 2) r = gelu_bf16_2(r) * f32x2{d[cb][1][2 * e2], d[cb][1][2 * e2 + 1]};   // packed pairs
+        const float r0 = r.x, r1 = r.y;
         const uint32_t lo = __builtin_bit_cast(unsigned short, (bf16)r0);
         const uint32_t hi = __builtin_bit_cast(unsigned short, (bf16)r1);
         pk[e2] = lo | (hi << 16);

@@ -158,13 +158,20 @@ __global__ __launch_bounds__(512, FFN<C>::BPC) void ffn_kernel(FfnArgs a) {
       bf16x8v hf[2];
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        const float nm = -mu[n];
+        // packed f32 pairs (v_pk_fma / v_pk_mul): two hidden channels per VALU issue
+        const f32x2 nm = f32x2{-mu[n], -mu[n]}, r2 = f32x2{rs[n], rs[n]};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float v0 = fmaf(rs[n], fmaf(nm, s_lo[i], acc1[n][0][i]), t_lo[i]);
-          const float v1 = fmaf(rs[n], fmaf(nm, s_hi[i], acc1[n][1][i]), t_hi[i]);
-          hf[n][i] = (bf16)gelu_bf16(v0);
-          hf[n][4 + i] = (bf16)gelu_bf16(v1);
+        for (int s = 0; s < 2; ++s) {
+          const f32x4 sv = s ? s_hi : s_lo, tv = s ? t_hi : t_lo;
+#pragma unroll
+          for (int i = 0; i < 4; i += 2) {
+            const f32x2 v = __builtin_elementwise_fma(
+                r2, __builtin_elementwise_fma(nm, f32x2{sv[i], sv[i + 1]}, f32x2{acc1[n][s][i], acc1[n][s][i + 1]}),
+                f32x2{tv[i], tv[i + 1]});
+            const f32x2 gv = gelu_bf16_2(v);
+            hf[n][4 * s + i] = (bf16)gv.x;
+            hf[n][4 * s + i + 1] = (bf16)gv.y;
+          }
         }
       }
       // GEMM2 K step hc

@@ -152,12 +152,11 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
         RW::unpack(q, v);
         const float* wt = &sw[hh][tap][wcy];
 #pragma unroll
-        for (int i0 = 0; i0 < VW; i0 += 4) {
+        for (int i0 = 0; i0 < VW; i0 += 4) {   // packed f32 pairs (v_pk_fma_f32)
           const float4 ww = *reinterpret_cast<const float4*>(wt + i0);
-          acc[hh][i0] = fmaf(ww.x, v[i0], acc[hh][i0]);
-          acc[hh][i0 + 1] = fmaf(ww.y, v[i0 + 1], acc[hh][i0 + 1]);
-          acc[hh][i0 + 2] = fmaf(ww.z, v[i0 + 2], acc[hh][i0 + 2]);
-          acc[hh][i0 + 3] = fmaf(ww.w, v[i0 + 3], acc[hh][i0 + 3]);
+          const f32x2 a0 = __builtin_elementwise_fma(f32x2{ww.x, ww.y}, f32x2{v[i0], v[i0 + 1]}, f32x2{acc[hh][i0], acc[hh][i0 + 1]});
+          const f32x2 a1 = __builtin_elementwise_fma(f32x2{ww.z, ww.w}, f32x2{v[i0 + 2], v[i0 + 3]}, f32x2{acc[hh][i0 + 2], acc[hh][i0 + 3]});
+          acc[hh][i0] = a0.x; acc[hh][i0 + 1] = a0.y; acc[hh][i0 + 2] = a1.x; acc[hh][i0 + 3] = a1.y;
         }
         // one tap's weights / unpacked values live at a time (the scheduler would otherwise
         // hoist all 9 taps' LDS reads and unpacks: 200+ VGPRs, one wave per SIMD)
@@ -167,12 +166,21 @@ __global__ __launch_bounds__(256) void dw_rows_kernel(DwArgs a, int RB, int nstr
     }
     if (live) {
       float o[VW];
+      if constexpr (sizeof(T) == 2 && MODE != DW_PLAIN) {   // bf16 GELU / gate as packed pairs
 #pragma unroll
-      for (int i = 0; i < VW; ++i) {
-        float r = acc[0][i];
-        if (MODE == DW_GELU) r = gelu_t<T>(r);
-        else if (MODE == DW_GATE) r = gelu_t<T>(r) * acc[NH - 1][i];
-        o[i] = r;
+        for (int i = 0; i < VW; i += 2) {
+          f32x2 r = gelu_bf16_2(f32x2{acc[0][i], acc[0][i + 1]});
+          if (MODE == DW_GATE) r = r * f32x2{acc[NH - 1][i], acc[NH - 1][i + 1]};
+          o[i] = r.x; o[i + 1] = r.y;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < VW; ++i) {
+          float r = acc[0][i];
+          if (MODE == DW_GELU) r = gelu_t<T>(r);
+          else if (MODE == DW_GATE) r = gelu_t<T>(r) * acc[NH - 1][i];
+          o[i] = r;
+        }
       }
       const int64_t pix = (img * a.H + y) * a.W + x;
       int64_t dst;
