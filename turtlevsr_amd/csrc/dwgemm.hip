@@ -121,8 +121,15 @@ __global__ __launch_bounds__(DG_NT, 1) void dwgemm_kernel(DwGemmArgs g) {
       const int c = dg_xpos<NH>(p, pos);                  // involution: position <-> chunk
       const int yy = y0 - 1 + r, xx = x0 - 1 + p;
       if (yy >= 0 && yy < g.H && xx >= 0 && xx < g.W) {
-        ptr = reinterpret_cast<const char*>(in + (yy * g.W + xx) * (int)g.ldi + (c >> 1) * K + (c & 1) * 8);
-        inc = DG_KC * 2;
+        if (g.cb_px) {                                    // channel-blocked: x2 blocks follow the K / 16 x1 blocks
+          const int64_t pix = ((int64_t)img * g.H + yy) * g.W + xx;
+          ptr = reinterpret_cast<const char*>(reinterpret_cast<const bf16*>(g.in) + (((int64_t)(c >> 1) * (K / DG_KC) * g.cb_px + pix) << 4) +
+                                              (c & 1) * 8);
+          inc = (int)(g.cb_px * DG_KC * 2);
+        } else {
+          ptr = reinterpret_cast<const char*>(in + (yy * g.W + xx) * (int)g.ldi + (c >> 1) * K + (c & 1) * 8);
+          inc = DG_KC * 2;
+        }
       }
     } else if (b < L::B_OFF) {
       const int q = (b - L::T_OFF) >> 4, hh = q / 18, tap = (q % 18) >> 1, piece = q & 1;
@@ -330,7 +337,9 @@ __global__ __launch_bounds__(DG_NT, 1) void dwgemm_kernel(DwGemmArgs g) {
 // Eligible: 16-byte aligned rows, K % 32 == 0 (whole K-step pairs), N % 8 == 0
 bool dwgemm_ok(const DwGemmArgs& g) {
   if ((int64_t)g.N * g.ldw >= (int64_t)1 << 31) return false;   // 32-bit weight / input offsets
-  if ((int64_t)g.H * g.W * g.ldi >= (int64_t)1 << 31) return false;
+  if (!g.cb_px && (int64_t)g.H * g.W * g.ldi >= (int64_t)1 << 31) return false;
+  if (g.cb_px && ((int64_t)(g.K / DG_KC + 3) * g.cb_px * DG_KC * 2 >= (int64_t)1 << 31 || g.cb_px < (int64_t)g.nimg * g.H * g.W))
+    return false;                                 // per-step byte increments stay 32-bit
   if (g.K % (2 * DG_KC) || g.N % 8 || g.K <= 0 || g.N <= 0 || g.H <= 0 || g.W <= 0) return false;
   if (g.ldi % 8 || g.offi % 8 || g.ldw % 8 || g.ldo % 8 || g.offo % 8 || g.wstride % 8) return false;
   if (g.res && (g.ldr % 8 || g.offr % 8 || reinterpret_cast<uintptr_t>(g.res) % 16)) return false;

@@ -555,6 +555,11 @@ static void launch_cfg(const GemmArgs& g, hipStream_t st) {
 
 template <typename T>
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
+  if (g.store_mode == STORE_CB16) {                // produced only for the pn kernel (turtle.cpp)
+    if (sizeof(T) != 2 || !gemm_pn_ok(g)) abort();
+    launch_gemm_pn(g, st);
+    return;
+  }
   if constexpr (sizeof(T) == 2) {
     // measured per shape class (tools/kbench, MI355X): the 2-D tiled kernel for the resampling 3x3
     // convolutions and K >= 640 (incl. the five-source W_eff GEMM), the A-resident kernel for the

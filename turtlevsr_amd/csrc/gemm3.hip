@@ -344,7 +344,12 @@ __global__ __launch_bounds__(512, 1) void gemm_pn_kernel(GemmArgs g, int npanel)
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
         // rows past the panel end hold copies of its last row: same value, same address
-        if (!(g.dbg & 1)) pn_gstore(pob + (min(wm * (BM / WM) + mt * 16 + fr, mlast) * (int)g.ldo + cb), o);
+        const int prow = min(wm * (BM / WM) + mt * 16 + fr, mlast);
+        if (g.store_mode == STORE_CB16) {   // channel-blocked: 16-channel block cb >> 4, 32-byte pixel rows
+          if (!(g.dbg & 1)) pn_gstore(reinterpret_cast<bf16*>(g.out) + (((int64_t)(cb >> 4) * g.cb_px + P.m0 + prow) << 4) + (cb & 15), o);
+        } else if (!(g.dbg & 1)) {
+          pn_gstore(pob + (prow * (int)g.ldo + cb), o);
+        }
       }
       PN_STAMP();
     }
@@ -362,7 +367,12 @@ static size_t pn_lds_bytes(int bm, int kp, int N, bool scale) {
 static int pn_wn(int N, bool res) { return (N % 256 == 0 && !res) ? 8 : (N % 128 == 0 ? 4 : 2); }
 
 bool gemm_pn_ok(const GemmArgs& g) {
-  if (!g.allow_pn || g.conv3 || g.store_mode != STORE_NHWC) return false;
+  if (!g.allow_pn || g.conv3) return false;
+  if (g.store_mode == STORE_CB16) {
+    if (g.res || g.offo || g.N % 16 || g.cb_px != g.M || g.scale) return false;
+  } else if (g.store_mode != STORE_NHWC) {
+    return false;
+  }
   const int K = g.a.Ktot;
   if (K != 64 && K != 128 && K != 256 && K != 384 && K != 512) return false;
   if (g.N % 64 || g.N > 8192 || g.ldw % 8 || g.ldo % 8 || g.offo % 8) return false;

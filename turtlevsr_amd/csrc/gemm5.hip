@@ -320,7 +320,7 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * WN <= 4) ? 2 : 1) void gemm_kt_
 // Eligible: bf16, 16-byte aligned operand rows, N % 8 == 0 (PixelShuffle: N / 4 % 8), K tiles never
 // straddle sources / taps (all but the last source K % 32 == 0, conv3 cin % 32 == 0).
 bool gemm_kt_ok(const GemmArgs& g) {
-  if (!g.allow_kt || g.N % 8 || g.ldo % 8 || g.offo % 8 || g.ldw % 8) return false;
+  if (!g.allow_kt || g.store_mode == STORE_CB16 || g.N % 8 || g.ldo % 8 || g.offo % 8 || g.ldw % 8) return false;
   if (g.res && (g.ldr % 8 || g.offr % 8)) return false;
   if (g.store_mode == STORE_SHUFFLE && (g.N / 4) % 8) return false;
   if (reinterpret_cast<uintptr_t>(g.out) % 16 || reinterpret_cast<uintptr_t>(g.w) % 16 ||

@@ -4,7 +4,9 @@
 
 namespace turtle {
 
-enum StoreMode { STORE_NHWC = 0, STORE_SHUFFLE = 1, STORE_UNSHUFFLE = 2 };
+// STORE_CB16: channel-blocked [C / 16][pixels][16] (cb_px pixels per block): the hidden map of a
+// GatedFeedForward whose depthwise + gate runs in dwgemm.hip reads one K step as contiguous rows
+enum StoreMode { STORE_NHWC = 0, STORE_SHUFFLE = 1, STORE_UNSHUFFLE = 2, STORE_CB16 = 3 };
 
 struct GemmArgs {
   SrcList a;                       // A sources, K-concatenated
@@ -37,6 +39,7 @@ struct GemmArgs {
   int allow_kt;                    // 2-D tiled deep-ring kernel permitted (turtle_set_option "gemm_kt")
   int dbg;                         // tools/kbench ablations of the pn kernel (0 in the product path)
   unsigned long long* stamps;      // tools/kbench s_memtime stamps of the pn kernel (null in the product path)
+  int64_t cb_px;                   // STORE_CB16: pixels per 16-channel block (= M)
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
 bool gemm_lds_ok(const GemmArgs& g);                              // gemm2.hip (bf16)
@@ -234,6 +237,7 @@ struct DwGemmArgs {                // dwgemm.hip: out = res + b + W [gelu(dw(x1)
   const void* res; int64_t ldr; int offr;
   void* out; int64_t ldo; int offo;
   const float* zeros;              // >= 16 zero floats
+  int64_t cb_px;                   // > 0: `in` is channel-blocked [C / 16][cb_px][16] (STORE_CB16), ldi / offi unused
   int dbg;                         // tools/dgbench ablations (0 in the product path)
 };
 bool dwgemm_ok(const DwGemmArgs& g);

@@ -319,6 +319,7 @@ struct TurtleHandle {
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
+  bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
   bool dwgemm_attn = true;                            // channel attention: v's depthwise inside the W_eff GEMM (dwgemm.hip)
   int dwgemm_min_blocks = 384;                        // one 160 KB block per CU: below ~1.5 rounds (latent level) dw + GEMM is faster
   bool blaslt = getenv("TURTLE_NO_BLASLT") == nullptr; // hipBLASLt for the plain projections it wins (blas.cpp)
@@ -684,9 +685,12 @@ struct Runner {
     g.ln = w.ln; g.ln_s = h->fptr(w.s); g.ln_t = h->fptr(w.t);
     g.bias = bias ? bias : h->fptr(w.bias); g.scale = h->fptr(w.scale); g.gelu = gelu;
     g.res = res; g.ldr = ldr; g.offr = offr;
-    g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store;
+    g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store; g.cb_px = store == STORE_CB16 ? M : 0;
     g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel; g.allow_lds = h->gemm_lds; g.allow_pn = h->gemm_pn;
     g.allow_ar = h->gemm_ar; g.allow_kt = h->gemm_kt;
+    if (store == STORE_CB16 && (ES != 2 || !gemm_pn_ok(g)))
+      TFAIL(TURTLE_EINVAL, "channel-blocked store needs the pn GEMM (M " + std::to_string(M) + " N " + std::to_string(g.N) +
+                               " K " + std::to_string(a.Ktot) + " HW " + std::to_string(HW) + ")");
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
     // algorithmic traffic: A once (a 3x3 reads each input pixel once), W per weight set, out
     // (+ residual) once
@@ -829,14 +833,14 @@ struct Runner {
   // GEMM's operand prologue (dwgemm.hip); returns false (nothing launched) where not eligible
   bool dwgemm(const DwW& dwp, int gate, const T* in, int64_t ldi, int offi, int nimg, int H, int Wd, int K,
               const void* wptr, int64_t ldw, int64_t wstride, int N, const float* bias, const T* res, int64_t ldr,
-              T* out, int64_t ldo) {
+              T* out, int64_t ldo, int64_t cb_px = 0) {
     if (ES != 2 || !h->dwgemm || dwp.C != (gate ? 2 * K : K)) return false;
     DwGemmArgs a{};
     a.in = in; a.ldi = ldi; a.offi = offi; a.dww16 = h->ptr(dwp.w16); a.dwb = h->fptr(dwp.bias); a.gate = gate;
     a.nimg = nimg; a.H = H; a.W = Wd; a.K = K;
     a.w = wptr; a.ldw = ldw; a.wstride = wstride; a.wdiv = 1; a.N = N; a.bias = bias;
     a.res = res; a.ldr = ldr; a.offr = 0; a.out = out; a.ldo = ldo; a.offo = 0;
-    a.zeros = h->fptr(h->mw.zeros);
+    a.zeros = h->fptr(h->mw.zeros); a.cb_px = cb_px;
     if (dwgemm_blocks(a) < h->dwgemm_min_blocks) return false;
     if (dry()) return true;
     if (!dwgemm_ok(a)) return false;
@@ -850,6 +854,20 @@ struct Runner {
     DwGemmArgs a{};
     a.nimg = nimg; a.H = H; a.W = Wd; a.N = c;
     return dwgemm_blocks(a) >= h->dwgemm_min_blocks;
+  }
+  // shape-only: the GatedFeedForward hidden map channel-blocked between the pn GEMM and dwgemm
+  bool can_dwgemm_cb(int c, int hd, int nimg, int H, int Wd) const {
+    if (ES != 2 || !h->dwgemm || !h->dwgemm_cb || !h->gemm_pn || hd % 32 || hd > 2048) return false;
+    if (c != 64 && c != 128 && c != 256 && c != 384 && c != 512) return false;
+    const int64_t P = (int64_t)nimg * H * Wd;
+    if ((2 * hd) % 64 || (int64_t)H * Wd < 128 || (int64_t)(hd / 16 + 3) * P * 32 >= ((int64_t)1 << 31)) return false;
+    DwGemmArgs a{};
+    a.nimg = nimg; a.H = H; a.W = Wd; a.N = c;
+    if (dwgemm_blocks(a) < h->dwgemm_min_blocks) return false;
+    GemmArgs g{};                                  // the project_in GEMM as gemm() will build it
+    g.a = src1(nullptr, c, 0, c); g.M = P; g.N = 2 * hd; g.HW = H * Wd; g.Wimg = Wd; g.ldw = c; g.ln = 1;
+    g.ldo = 2 * hd; g.store_mode = STORE_CB16; g.cb_px = P; g.allow_pn = h->gemm_pn;
+    return gemm_pn_ok(g);
   }
   bool dwgemm_launch(DwGemmArgs& a) {
     const int gate = a.gate, K = a.K, N = a.N, nimg = a.nimg, H = a.H, Wd = a.W;
@@ -993,6 +1011,13 @@ struct Runner {
         T* t2 = buf(P * hd);
         pwdw(bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, 1, t2, hd, 0);
         gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
+      } else if (can_dwgemm_cb(c, hd, B, H, Wd)) {
+        // project_in stores the hidden map channel-blocked ([2 hd / 16][P][16]): each dwgemm K step
+        // then reads contiguous 32-byte pixel rows
+        T* t1 = buf(P * 2 * hd);
+        gemm(bw.f_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * hd, 0, nullptr, 0, 0, 0, STORE_CB16);
+        if (!dwgemm(bw.f_dw, 1, t1, 0, 0, B, H, Wd, hd, h->ptr(bw.f_out.w), hd, 0, c, h->fptr(bw.f_out.bias), x, c, x, c, P))
+          TFAIL(TURTLE_EINVAL, "GatedFeedForward: channel-blocked dwgemm not eligible");
       } else {
         T* t1 = buf(P * 2 * hd);
         T* t2 = buf(P * hd);   // dw + gate output of the unfolded path
@@ -1455,6 +1480,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "blaslt") h->blaslt = value != 0;
     else if (n == "dwgemm") h->dwgemm = value != 0;
     else if (n == "dwgemm_attn") h->dwgemm_attn = value != 0;
+    else if (n == "dwgemm_cb") h->dwgemm_cb = value != 0;
     else if (n == "ffn") h->ffn = value != 0;
     else if (n == "sab_db") h->sab_db = value != 0;
     else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;
