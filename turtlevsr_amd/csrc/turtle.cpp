@@ -318,6 +318,7 @@ struct TurtleHandle {
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
+  int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 1024;   // Gram pixel splits: blocks over all (b, head)
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
   bool dwgemm_attn = true;                            // channel attention: v's depthwise inside the W_eff GEMM (dwgemm.hip)
@@ -906,7 +907,7 @@ struct Runner {
     if (ncol > 512 || nseg > TURTLE_MAX_SEG) TFAIL(TURTLE_EINVAL, "channel attention: more than 512 key columns");
     // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each, whole
     // 128-pixel steps of the bf16 Gram
-    int nchunk = std::max(1, std::min((HW + 255) / 256, std::max(1, 1024 / (B * b.heads))));
+    int nchunk = std::max(1, std::min((HW + 255) / 256, std::max(1, h->gram_blocks / (B * b.heads))));
     int chunk = (HW + nchunk - 1) / nchunk;
     chunk = (chunk + 127) / 128 * 128;
     nchunk = (HW + chunk - 1) / chunk;
