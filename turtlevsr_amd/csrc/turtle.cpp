@@ -318,7 +318,7 @@ struct TurtleHandle {
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
-  int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 1024;   // Gram pixel splits: blocks over all (b, head)
+  int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
   bool dwgemm_attn = true;                            // channel attention: v's depthwise inside the W_eff GEMM (dwgemm.hip)
