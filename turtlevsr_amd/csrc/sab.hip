@@ -370,6 +370,8 @@ __global__ __launch_bounds__(256) void sab_prep_kernel(SabPrepArgs a) {
   }
   sv[w][lane] = v;
   si[w][lane] = ix;
+  // slots no entry ranks into (non-finite scores tie) stay "no key", never stale LDS
+  if (lane < SAB_K) { t5v[w][lane] = -INFINITY; t5i[w][lane] = -1; }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
   int rank = 0;
@@ -396,7 +398,8 @@ __global__ __launch_bounds__(256) void sab_prep_kernel(SabPrepArgs a) {
     const int x = lane - BALL;
     const int mm = t5i[w][x];
     const int mr = mm / a.tw, mc = mm - mr * a.tw;
-    if (abs(mr - ti) + abs(mc - tj) > 4) { m = mm; mul = 1; s = t5v[w][x]; }
+    // only real keys reach the gather (a NaN frame must give NaN output, not an out-of-range read)
+    if (mm >= 0 && mm < a.N && abs(mr - ti) + abs(mc - tj) > 4) { m = mm; mul = 1; s = t5v[w][x]; }
   }
   // 3) clipped softmax over the candidates whose logit s*mult is not exactly zero
   float l = -INFINITY;
