@@ -182,6 +182,7 @@ struct EndArgs {                   // ending 3x3 Cin->Cimg + bias + current fram
   const float* inp; int64_t in_bstride, in_fstride;
   int B, Cimg, Hin, Win, Hp, Wp, Hout, Wout, sr;
   float* out;                      // [B][Cimg][Hout][Wout]
+  const void* wfrag;               // bf16 MFMA A fragments of w (turtle.cpp pack_all), matrix-core kernel
 };
 template <typename T> void launch_ending(const EndArgs& a, hipStream_t st);
 bool stem_end_mfma_ok(int cin_end, int cin_stem, int cout_stem);   // bf16 matrix-core stem / ending

@@ -678,6 +678,61 @@ __global__ __launch_bounds__(256) void ending_mfma_kernel(EndArgs a) {
   }
 }
 
+// Tiled form of the same ending: a block owns 4 rows x 64 columns of output, stages the haloed
+// (6 x 66 pixels x CIN) input once in LDS with coalesced 16-byte loads (1.5x halo instead of every
+// tap's 16-byte vector coming from L2: 9x), and each wave runs its row as 4 runs of 16 pixels with
+// the MFMA B operands read from LDS (pixel rows padded to CIN * 2 + 16 bytes: conflict-free
+// ds_read_b128 for 16 consecutive pixels).
+constexpr int ET_R = 4, ET_C = 64;
+template <int CIN>
+__global__ __launch_bounds__(256) void ending_tile_kernel(EndArgs a) {
+  constexpr int KS = 9 * CIN / 32, PB = CIN * 2 + 16, TW = ET_C + 2, NPX = (ET_R + 2) * TW, CV = CIN / 8;
+  __shared__ __attribute__((aligned(16))) char sx[NPX * PB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int tpr = (a.Wp + ET_C - 1) / ET_C, tpc = (a.Hp + ET_R - 1) / ET_R;
+  const int bx = blockIdx.x % tpr, rest = blockIdx.x / tpr, by = rest % tpc, b = rest / tpc;
+  const int x0 = bx * ET_C, y0 = by * ET_R;
+  const bf16* X = reinterpret_cast<const bf16*>(a.x);
+  // haloed tile -> LDS (zero outside the padded image)
+  for (int e = tid; e < NPX * CV; e += 256) {
+    const int p = e / CV, k = e - p * CV, r = p / TW, c = p - r * TW;
+    const int yy = y0 - 1 + r, xx = x0 - 1 + c;
+    const bool ok = yy >= 0 && yy < a.Hp && xx >= 0 && xx < a.Wp;
+    const uint4 v = ld16(ok ? reinterpret_cast<const void*>(X + (((int64_t)b * a.Hp + yy) * a.Wp + xx) * CIN + k * 8) : g_zero_end);
+    *reinterpret_cast<uint4*>(sx + p * PB + k * 16) = v;
+  }
+  bf16x8 wf[KS];                                   // pre-packed A fragments: one 16-byte load each
+#pragma unroll
+  for (int s = 0; s < KS; ++s) wf[s] = __builtin_bit_cast(bf16x8, ld16(reinterpret_cast<const bf16*>(a.wfrag) + (s * 64 + lane) * 8));
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = i < a.Cimg ? a.bias[i] : 0.f;
+  StemArgs s{};
+  s.inp = a.inp; s.in_bstride = a.in_bstride; s.in_fstride = a.in_fstride;
+  s.Cimg = a.Cimg; s.Hin = a.Hin; s.Win = a.Win; s.sr = a.sr;
+  __syncthreads();
+  const int y = y0 + wid;                          // wave = output row
+#pragma unroll
+  for (int run = 0; run < ET_C / 16; ++run) {
+    const int xl = run * 16 + li;                  // output column in the tile
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int k0 = st * 32 + g * 8, tap = k0 / CIN, c = k0 - tap * CIN;
+      const int r = wid + tap / 3, cc = xl + tap % 3;   // haloed tile coordinates of the tap
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(sx + (r * TW + cc) * PB + c * 2);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[st], bv, acc, 0, 0, 0);
+    }
+    const int x = x0 + xl;
+    if (g == 0 && y < a.Hout && x < a.Wout) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (i < a.Cimg)
+          a.out[(((int64_t)b * a.Cimg + i) * a.Hout + y) * a.Wout + x] = acc[i] + bias[i] + frame_px(s, b, 1, i, y, x);
+    }
+  }
+}
+
 template <int CIN>   // frame channels (Cimg, or 2 Cimg with use_both_input); K = 9 CIN padded to 32 KS
 __global__ __launch_bounds__(256) void stem_mfma_kernel(StemArgs a) {
   constexpr int KS = (9 * CIN + 31) / 32;
@@ -753,7 +808,9 @@ bool stem_end_mfma_ok(int cin_end, int cin_stem, int cout_stem) {
 }
 
 void launch_ending_mfma(const EndArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(ending_mfma_kernel<64>, dim3(2048), dim3(256), 0, st, a);
+  if (!a.wfrag || a.Cin != 64) abort();            // packed by turtle.cpp for the 64-channel ending
+  const int64_t tiles = (int64_t)a.B * ((a.Hp + ET_R - 1) / ET_R) * ((a.Wp + ET_C - 1) / ET_C);
+  hipLaunchKernelGGL(ending_tile_kernel<64>, dim3((unsigned)tiles), dim3(256), 0, st, a);
 }
 
 void launch_stem_mfma(const StemArgs& a, hipStream_t st) {

@@ -217,6 +217,7 @@ struct BlockW {
 };
 struct ModelW {
   size_t stem_w = NONE, stem_b = NONE, end_w = NONE, end_b = NONE;
+  size_t end_wf = NONE;                      // ending 3x3 as bf16 MFMA A fragments [9 Cin / 32][64 lanes][8] (spatial.hip)
   size_t zeros = NONE, ones = NONE;          // constant vectors for branch-free kernel operands
   GemmW down[3], up[3], reduce[3];
   std::vector<std::vector<BlockW>> blocks;   // [level][block]
@@ -475,6 +476,22 @@ static void pack_all(TurtleHandle* h) {
   M.stem_w = pk.f32(dvec(W(h, "input_projection.weight")));
   if (has(h, "input_projection.bias")) M.stem_b = pk.f32(dvec(W(h, "input_projection.bias")));
   M.end_w = pk.f32(dvec(W(h, "ending.weight")));
+  {
+    // A fragment s, lane l: output channel l & 15 (< Cimg, else 0), k = 32 s + 8 (l >> 4) + j -> (tap, ci)
+    const auto& ew = W(h, "ending.weight");
+    const int cin = d, cimg = (int)(ew.size() / ((size_t)cin * 9));
+    if (cin % 32 == 0 && cimg <= 16) {
+      const int ks = 9 * cin / 32;
+      std::vector<double> f((size_t)ks * 64 * 8, 0.0);
+      for (int s = 0; s < ks; ++s)
+        for (int l = 0; l < 64; ++l)
+          for (int j = 0; j < 8; ++j) {
+            const int k = s * 32 + (l >> 4) * 8 + j, tap = k / cin, ci = k - tap * cin, co = l & 15;
+            if (co < cimg) f[((size_t)s * 64 + l) * 8 + j] = ew[((size_t)co * cin + ci) * 9 + tap];
+          }
+      M.end_wf = pk.bf16tab(f);
+    }
+  }
   M.end_b = pk.f32(dvec(W(h, "ending.bias")));
   const char* downs[3] = {"down1_2.body.0", "down2_3.body.0", "down3_4.body.0"};
   const char* ups[3] = {"up4_3.body.0", "up3_2.body.0", "up2_1.body.0"};
@@ -1377,6 +1394,7 @@ struct Runner {
     if (!dry()) {
       EndArgs e{};
       e.x = d1; e.Cin = d; e.w = h->fptr(h->mw.end_w); e.bias = h->fptr(h->mw.end_b);
+      e.wfrag = h->ptr(h->mw.end_wf);
       e.inp = inp; e.in_bstride = (int64_t)2 * A.cfg.n_colors * Hin * Win; e.in_fstride = (int64_t)A.cfg.n_colors * Hin * Win;
       e.B = B; e.Cimg = A.cfg.n_colors; e.Hin = Hin; e.Win = Win; e.Hp = Hp; e.Wp = Wp; e.Hout = Hout; e.Wout = Wout;
       e.sr = A.cfg.super_resolution; e.out = out;
