@@ -262,6 +262,8 @@ def main():
     ap.add_argument("--no-psnr", action="store_true")
     ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--profile-all", action="store_true", help="print every kernel class's time")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="kernel-selection switch (turtle_set_option), repeatable; A/B runs only")
     ap.add_argument("--train", action="store_true",
                     help="config 5: one DDP training step per `step` (8 x 5-frame 256x256 clips per GPU, bf16 autocast, AdamW)")
     ap.add_argument("--train-batch", type=int, default=8)
@@ -286,6 +288,9 @@ def main():
     opt = load_opt()
 
     model = build_model(opt, args.dtype, dev, args.sr)
+    for kv in args.opt:
+        name, value = kv.split("=", 1)
+        model.set_option(name, int(value))
     if args.sr:
         if h % 4 or w % 4:
             raise SystemExit(f"--sr needs an output size divisible by 4, got {w}x{h}")

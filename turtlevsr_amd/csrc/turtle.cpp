@@ -1034,7 +1034,9 @@ struct Runner {
         // then reads contiguous 32-byte pixel rows
         T* t1 = buf(P * 2 * hd);
         gemm(bw.f_in, src1(x, c, 0, c), P, HW, Wd, t1, 2 * hd, 0, nullptr, 0, 0, 0, STORE_CB16);
-        if (!dwgemm(bw.f_dw, 1, t1, 0, 0, B, H, Wd, hd, h->ptr(bw.f_out.w), hd, 0, c, h->fptr(bw.f_out.bias), x, c, x, c, P))
+        // (the sizing dry run may hold no packed weights: nothing to check or launch there)
+        if (!dry() && !dwgemm(bw.f_dw, 1, t1, 0, 0, B, H, Wd, hd, h->ptr(bw.f_out.w), hd, 0, c, h->fptr(bw.f_out.bias), x, c,
+                              x, c, P))
           TFAIL(TURTLE_EINVAL, "GatedFeedForward: channel-blocked dwgemm not eligible");
       } else {
         T* t1 = buf(P * 2 * hd);
