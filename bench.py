@@ -117,22 +117,53 @@ def clip_frames(h, w, seed, dev, n=5, batch=1):
     return [torch.stack([clip[:, max(j - 1, 0)], clip[:, j]], dim=1).contiguous() for j in range(n)]
 
 
-def cpu_baseline(opt, threads):
-    """Oracle fp32 on a 256x256 steady-state frame (3 priming frames untimed, 2 timed): s/frame."""
+def cpu_share_threads():
+    """Host threads for the CPU baseline: the GPU box's CPU share per GPU (OMP_NUM_THREADS, 16 on the
+    pool's 1-GPU boxes), capped by the cores present."""
+    n = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(n, os.cpu_count() or 1))
+
+
+def _grow_cache(t, n_tokens, p4):
+    """A cache tensor of the small priming run, re-shaped to the bench frame size (same layout:
+    FHR slots [B, heads, rows, P4], SAB slots [B, T, 1, N, d]) and filled with synthetic values."""
+    if t is None:
+        return None
+    shape = list(t.shape)
+    if t.dim() == 4:
+        shape[3] = p4
+    else:
+        shape[3] = n_tokens
+    g = torch.Generator().manual_seed(7 + t.dim() + shape[-1])
+    return torch.rand(shape, generator=g) - 0.5
+
+
+def cpu_baseline(opt, h, w, threads, sr=False):
+    """The reference's CPU path (oracle/turtle_ref.py: fp32 torch CPU restatement, dense SAB like
+    the reference) MEASURED on one steady-state frame at the bench resolution: the history caches
+    are full (T = ntc frames at every cached level; their shapes come from 4 priming frames at
+    64x64, re-sized to this frame, synthetic contents - the cost does not depend on them).
+    Returns seconds per frame."""
     from oracle import turtle_ref as R
     torch.set_num_threads(threads)
     m = TurtleHIP(opt)
     shapes = {k: tuple(v.shape) for k, v in m.state_dict().items()}
     sd = {k: torch.from_numpy(v) for k, v in synthetic_state_dict(shapes, 0).items()}
-    frames = clip_frames(256, 256, 11, "cpu")
+    small = clip_frames(64, 64, 11, "cpu")
     kc = vc = None
-    for j in range(3):
-        _, kc, vc = R.turtle_forward(sd, opt, frames[j], kc, vc)
-    t0 = time.perf_counter()
-    for j in range(3, 5):
-        _, kc, vc = R.turtle_forward(sd, opt, frames[j], kc, vc)
-    dt = (time.perf_counter() - t0) / 2
-    return dt
+    with torch.no_grad():
+        for j in range(4):
+            _, kc, vc = R.turtle_forward(sd, opt, small[j], kc, vc)
+        ho, wo = (4 * h, 4 * w) if sr else (h, w)
+        hp, wp = (ho + 31) // 32 * 32, (wo + 31) // 32 * 32
+        kb = [_grow_cache(t, hp * wp // 256, hp * wp // 64) for t in kc]
+        vb = [_grow_cache(t, hp * wp // 256, hp * wp // 64) for t in vc]
+        frame = clip_frames(h, w, 12, "cpu", n=2)[1]
+        print(f"[bench] cpu baseline: one steady-state {wo}x{ho} oracle frame on {threads} threads ...",
+              file=sys.stderr, flush=True)
+        t0 = time.perf_counter()
+        R.turtle_forward(sd, opt, frame, kb, vb, sr=sr)
+        return time.perf_counter() - t0
 
 
 def launch_groups(dump):
@@ -248,18 +279,90 @@ def train_bench(args, world, rank, dev):
         dist.destroy_process_group()
 
 
-def main():
+SCALE_RES, SCALE_BATCH = "256", 8       # north-star scaling workload: 256x256 5-frame clips, 8 per GPU
+
+
+def time_frames(model, frames, steps, warmup, graph, roofline_on, world):
+    """Prime the caches (3 frames), W warmup frames (every launch event-timed when roofline_on),
+    then K timed frames between barriers; returns (elapsed_s, wprof, wgroups, nwarm, tgroups)."""
+    state = dict(kc=None, vc=None, j=0)
+    runner = GraphedTurtle(model, *frames[0].shape[:1], *frames[0].shape[-2:]) if graph else None
+
+    def step():
+        if runner is not None:
+            out, state["kc"], state["vc"] = runner(frames[state["j"] % len(frames)])
+        else:
+            out, state["kc"], state["vc"] = model(frames[state["j"] % len(frames)], state["kc"], state["vc"])
+        state["j"] += 1
+        return out
+
+    with torch.no_grad():
+        for _ in range(3):           # prime the history caches (steady state: full caches)
+            step()
+        # warmup, profiled: every launch bracketed by HIP events -> whole-frame breakdown by kernel
+        # class / launch shape, and the dominant launch shape (most GPU time)
+        wdump = os.path.join("/tmp", f"turtle_bench_warm_{os.getpid()}.tsv")
+        if os.path.exists(wdump):
+            os.remove(wdump)
+        nwarm = max(warmup, 1)
+        if roofline_on:
+            os.environ["TURTLE_PROF_DUMP"] = wdump
+            model.profile_begin("all")
+        for _ in range(nwarm):
+            step()
+        torch.cuda.synchronize()
+        wprof = model.profile_end() if roofline_on else {}
+        wgroups = launch_groups(wdump)
+        dom = max(wgroups, key=lambda k: wgroups[k]["ms"]) if wgroups else None
+        if world > 1:
+            dist.barrier()
+        # timed region: HIP events only around the dominant shape's launches (per-launch events
+        # on all ~400 launches of a frame would add ~3 ms of stream bubbles to the frame time)
+        dump = os.path.join("/tmp", f"turtle_bench_launches_{os.getpid()}.tsv")
+        if os.path.exists(dump):
+            os.remove(dump)
+        if dom is not None:
+            os.environ["TURTLE_PROF_DUMP"] = dump
+            model.profile_begin("all", tag=dom)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if dom is not None:
+            model.profile_end()
+        os.environ.pop("TURTLE_PROF_DUMP", None)
+    tgroups = launch_groups(dump)
+    keep = os.environ.get("TURTLE_BENCH_DUMP")     # keep the warmup frames' per-launch records
+    if keep and os.path.exists(wdump):
+        shutil.copyfile(wdump, keep)
+    for f in (dump, wdump):
+        if os.path.exists(f):
+            os.remove(f)
+    return elapsed, wprof, wgroups, nwarm, tgroups
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--res", default="1080p", choices=list(RES))
+    ap.add_argument("--res", default=None, choices=list(RES),
+                    help="default: 1080p on one GPU; with --gpus N > 1 the north-star scaling workload "
+                         f"({SCALE_RES}x{SCALE_RES} 5-frame clips, {SCALE_BATCH} per GPU, graph replay)")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--batch", type=int, default=1, help="clips per GPU restored together (B of [B,2,3,H,W])")
+    ap.add_argument("--batch", type=int, default=None, help="clips per GPU restored together (B of [B,2,3,H,W])")
     ap.add_argument("--sr", action="store_true", help="TurtleSuper_t1 4x SR: LR input = res/4, output at res")
     ap.add_argument("--graph", action="store_true", help="steady-state frames replayed as captured HIP graphs (turtlevsr_amd/graph.py)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-psnr", action="store_true")
+    ap.add_argument("--no-scaling-point", action="store_true",
+                    help="skip the N=1 measurement of the scaling workload on the default 1-GPU line")
     ap.add_argument("--no-roofline", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--profile-all", action="store_true", help="print every kernel class's time")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
@@ -267,9 +370,31 @@ def main():
     ap.add_argument("--train", action="store_true",
                     help="config 5: one DDP training step per `step` (8 x 5-frame 256x256 clips per GPU, bf16 autocast, AdamW)")
     ap.add_argument("--train-batch", type=int, default=8)
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
+    default_line, _ = resolve_workload(args)
+    return args, default_line
+
+
+def resolve_workload(args):
+    """Workload of a run: with no --res / --batch, one GPU measures the headline configuration
+    (1080p, B = 1, eager: BASELINE.json's metric) and `--gpus N > 1` the north-star scaling
+    workload (256x256 5-frame clips, SCALE_BATCH per GPU, graph replay), which the default 1-GPU
+    line also measures once as `scaling_workload_n1`. Returns (default 1-GPU line?, scaling run?)."""
+    default_line = args.res is None and args.batch is None and not args.sr and not args.train and not args.graph
+    scaling_run = args.res is None and args.gpus > 1 and not args.train and not args.sr
+    if args.res is None:
+        args.res = SCALE_RES if scaling_run else "1080p"
+    if args.batch is None:
+        args.batch = SCALE_BATCH if scaling_run else 1
+    if scaling_run:
+        args.graph = True
     if args.graph:
         args.no_roofline = True      # per-launch profiling events cannot live inside a captured graph
+    return default_line and args.gpus == 1, scaling_run
+
+
+def main():
+    args, default_line = parse_args()
 
     # one process per GPU: spawn the workers here, before this process touches the GPU, unless an
     # external launcher (torch.distributed.run) already did; its WORLD_SIZE must match --gpus
@@ -297,69 +422,11 @@ def main():
         frames = clip_frames(h // 4, w // 4, clip_seed(rank), dev, batch=args.batch)
     else:
         frames = clip_frames(h, w, clip_seed(rank), dev, batch=args.batch)
-    kc = vc = None
-    j = 0
-
-    runner = GraphedTurtle(model, *frames[0].shape[:1], *frames[0].shape[-2:]) if args.graph else None
-
-    def step():
-        nonlocal kc, vc, j
-        if runner is not None:
-            out, kc, vc = runner(frames[j % len(frames)])
-        else:
-            out, kc, vc = model(frames[j % len(frames)], kc, vc)
-        j += 1
-        return out
-
-    with torch.no_grad():
-        for _ in range(3):           # prime the history caches (steady state: full caches)
-            step()
-        # warmup, profiled: every launch bracketed by HIP events -> whole-frame breakdown by kernel
-        # class / launch shape, and the dominant launch shape (most GPU time)
-        wdump = os.path.join("/tmp", f"turtle_bench_warm_{os.getpid()}.tsv")
-        if os.path.exists(wdump):
-            os.remove(wdump)
-        nwarm = max(args.warmup, 1)
-        if not args.no_roofline:
-            os.environ["TURTLE_PROF_DUMP"] = wdump
-            model.profile_begin("all")
-        for _ in range(nwarm):
-            step()
-        torch.cuda.synchronize()
-        wprof = model.profile_end() if not args.no_roofline else {}
-        wgroups = launch_groups(wdump)
-        dom = max(wgroups, key=lambda k: wgroups[k]["ms"]) if wgroups else None
-        if world > 1:
-            dist.barrier()
-        # timed region: HIP events only around the dominant shape's launches (per-launch events
-        # on all ~400 launches of a frame would add ~3 ms of stream bubbles to the frame time)
-        dump = os.path.join("/tmp", f"turtle_bench_launches_{os.getpid()}.tsv")
-        if os.path.exists(dump):
-            os.remove(dump)
-        if dom is not None:
-            os.environ["TURTLE_PROF_DUMP"] = dump
-            model.profile_begin("all", tag=dom)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        if dom is not None:
-            model.profile_end()
-        os.environ.pop("TURTLE_PROF_DUMP", None)
+    elapsed, wprof, wgroups, nwarm, tgroups = time_frames(model, frames, args.steps, args.warmup, args.graph,
+                                                          not args.no_roofline, world)
     rep = replica_throughput(elapsed, args.steps * args.batch, dev)
     tmax, fps = rep.t_max, rep.value
-
-    roof = roofline(wprof, wgroups, nwarm, launch_groups(dump), args.steps, args.dtype)
-    keep = os.environ.get("TURTLE_BENCH_DUMP")     # keep the warmup frames' per-launch records
-    if keep and os.path.exists(wdump):
-        shutil.copyfile(wdump, keep)
-    for f in (dump, wdump):
-        if os.path.exists(f):
-            os.remove(f)
+    roof = roofline(wprof, wgroups, nwarm, tgroups, args.steps, args.dtype)
 
     psnr = dpsnr = None
     if not args.no_psnr and rank == 0 and args.dtype == "bf16":
@@ -394,17 +461,31 @@ def main():
             dpsnr = round(max(deltas), 5)
         del ref
 
+    # the scaling workload at N = 1 (the default line only): the point the driver's N > 1 runs of
+    # `--gpus N` (which default to that workload) are compared with
+    scale_pt = None
+    if default_line and world == 1 and rank == 0 and not args.no_scaling_point:
+        del model
+        torch.cuda.empty_cache()
+        sh, sw = RES[SCALE_RES]
+        sm = build_model(opt, args.dtype, dev)
+        sframes = clip_frames(sh, sw, clip_seed(rank), dev, batch=SCALE_BATCH)
+        s_el, *_ = time_frames(sm, sframes, max(args.steps, 10), 3, True, False, 1)
+        scale_pt = dict(value=round(max(args.steps, 10) * SCALE_BATCH / s_el, 3), unit="frames/s", n_gpus=1,
+                        workload=f"Turtle_t1 GoPro deblur, {sw}x{sh} causal 5-frame clips, B={SCALE_BATCH} per GPU, "
+                                 "caches full, HIP graph replay (the `--gpus N > 1` default workload)")
+        del sm
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        dt = cpu_baseline(opt, threads)
-        scale = f_ref(256, 256) / f_ref(h, w)     # (SR: the network runs at the output size)
-        cpu = dict(value=round(scale / dt, 6), unit="frames/s", cores=threads, kind="port",
-                   measured_s_per_frame_256=round(dt, 3), cpu_model=cpu_model(), nproc=os.cpu_count(),
+        threads = cpu_share_threads()
+        dt = cpu_baseline(opt, h // 4 if args.sr else h, w // 4 if args.sr else w, threads, sr=args.sr)
+        cpu = dict(value=round(1.0 / dt, 6), unit="frames/s", cores=threads, kind="port", measured=True,
+                   s_per_frame=round(dt, 2), cpu_model=cpu_model(), nproc=os.cpu_count(),
                    torch_threads=torch.get_num_threads(),
-                   sample=f"oracle/turtle_ref.py fp32 (dense SAB, as the reference) on 2 steady-state 256x256 GoPro "
-                          f"frames after 3 priming frames: {dt:.2f} s/frame on {threads} threads; scaled to "
-                          f"{w}x{h} by the reference FLOP ratio F_ref(256^2)/F_ref = {scale:.5f}")
+                   sample=f"oracle/turtle_ref.py fp32 (dense SAB, as the reference), ONE steady-state {w}x{h} frame "
+                          f"(history caches full: T = ntc at every cached level), B=1, timed on {threads} host threads "
+                          f"(the box's CPU share per GPU): {dt:.1f} s/frame; not extrapolated")
 
     line = {
         "metric": "restored frames/sec @1080p (1/2/4/8 GPU) + PSNR delta vs ref"
@@ -422,7 +503,7 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic frames (uniform [0,1)), synthetic random-init GoPro weights",
         "config": {"workload": (f"TurtleSuper_t1 GoPro-arch 4x SR, {w // 4}x{h // 4} -> {w}x{h}" if args.sr
-                                else f"Turtle_t1 GoPro deblur, {w}x{h}") + f", causal 5-frame clip, B={args.batch}, caches full",
+                                else f"Turtle_t1 GoPro deblur, {w}x{h}") + f", causal 5-frame clip, B={args.batch} per GPU, caches full",
                    "model": "Turtle_t1 (GoPro arch, 59.08M params)", "global_batch": world * args.batch, "seq_len": 5,
                    "parallelism": f"replicas x{world}",
                    "execution": "HIP graph replay (2 captured graphs, ping-pong caches)" if args.graph else "eager launches"},
@@ -432,6 +513,8 @@ def main():
         "psnr_delta_vs_fp32_db": dpsnr,
         "alg_tflops": round(f_alg(h, w) * fps / 1e12, 2),
     }
+    if scale_pt is not None:
+        line["scaling_workload_n1"] = scale_pt
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1,15 +1,17 @@
 /* libturtle_hip training-path kernels (turtlevsr_amd/csrc/train_ops.hip).
  *
  * The training step (config 5, video_restoration_model.py:78-108) runs the Turtle_t1 graph under
- * torch autograd on the GPU; these entry points are the hand-written forward / backward kernels of
- * the ops whose aten lowering is the slow part of that graph, bound by turtlevsr_amd/train_ops.py
- * as torch.autograd.Functions. Tensors are NCHW, contiguous, device pointers; `dtype` 0 = fp32,
- * 1 = bf16 activations (weights and weight gradients fp32); `stream` is a hipStream_t. Weight /
- * bias gradient buffers are accumulated into (atomics): zero them first. Return 0 or an error
- * (negative: bad argument; positive: hipError_t).
+ * torch autograd on the GPU with channels-last (NHWC) activations; these entry points are the
+ * hand-written forward / backward kernels of its ops, bound by turtlevsr_amd/train_ops.py as
+ * torch.autograd.Functions. Activations are pixel rows: element (p, c) at base[p * ld + c], base
+ * 16-byte aligned, ld * element size a multiple of 16 B. `dtype` 0 = fp32, 1 = bf16, 2 = fp16
+ * (the GEMM entry points take 0 / 1); weights and weight gradients fp32 unless stated. `stream` is
+ * a hipStream_t. Gradient buffers documented as "accumulated" are added into (atomics): zero them
+ * first. Return 0 or an error (negative: bad argument; positive: hipError_t).
  */
 #ifndef TURTLE_TRAIN_H
 #define TURTLE_TRAIN_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -17,26 +19,51 @@ extern "C" {
 #endif
 
 /* LayerNorm over channels per pixel (turtle_t1_arch.py:67-112, WithBias_LayerNorm / BiasFree_LayerNorm):
- * x, y [N][C][HW]; w, b [C]; saves mu, rstd [N*HW] for the backward. */
-int turtle_train_ln_fwd(const void* x, const float* w, const float* b, void* y, float* mu, float* rstd, int64_t N, int C,
-                        int64_t HW, int biasfree, int dtype, void* stream);
-/* dx [N][C][HW]; dw, db [C] accumulated (db unused for BiasFree) */
-int turtle_train_ln_bwd(const void* x, const float* w, const float* mu, const float* rstd, const void* dy, void* dx,
-                        float* dw, float* db, int64_t N, int C, int64_t HW, int biasfree, int dtype, void* stream);
+ * x [P][ldx] -> y [P][ldy] (C channels, C % 8 == 0, C <= 2048); w, b [C]; saves mu, rstd [P]. */
+int turtle_train_ln_fwd(const void* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy, float* mu, float* rstd,
+                        int64_t P, int C, int biasfree, int dtype, void* stream);
+/* dx [P][lddx]; dw, db [C] accumulated (db unused for BiasFree) */
+int turtle_train_ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy,
+                        int64_t lddy, void* dx, int64_t lddx, float* dw, float* db, int64_t P, int C, int biasfree, int dtype,
+                        void* stream);
 
 /* depthwise 3x3, stride 1, pad 1, groups = C (nn.Conv2d(C, C, 3, padding=1, groups=C), e.g.
- * turtle_t1_arch.py:167-169, 237, 716-722): w [C][9], b [C] or NULL. flip = 1 convolves with the
- * taps rotated by 180 degrees (the input gradient: dx = dw3x3_flip(dy), b = NULL). N*C <= 65535. */
-int turtle_train_dw3x3_fwd(const void* x, const float* w, const float* b, void* y, int64_t N, int C, int H, int W, int flip,
-                           int dtype, void* stream);
-/* dw [C][9], db [C] (or NULL) accumulated from x and dy */
-int turtle_train_dw3x3_wgrad(const void* x, const void* dy, float* dw, float* db, int64_t N, int C, int H, int W, int dtype,
-                             void* stream);
+ * turtle_t1_arch.py:167-169, 237, 716-722): x [N][H][W][ldx] -> y [N][H][W][ldy]; w9 tap-major
+ * [9][C] (tap = 3 dy + dx), b [C] or NULL. flip = 1 uses the taps rotated by 180 degrees (the input
+ * gradient: dx = dw3x3_flip(dy), b = NULL). */
+int turtle_train_dw3x3_fwd(const void* x, int64_t ldx, const float* w9, const float* b, void* y, int64_t ldy, int64_t N, int C,
+                           int H, int W, int flip, int dtype, void* stream);
+/* dw9 [9][C], db [C] (or NULL) accumulated from x and dy */
+int turtle_train_dw3x3_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* dw9, float* db, int64_t N, int C,
+                             int H, int W, int dtype, void* stream);
 
-/* GatedFeedForward gate (turtle_t1_arch.py:176): x [N][2h][HW] -> y [N][h][HW] = gelu(x[:h]) * x[h:]
- * (exact erf GELU); backward dx [N][2h][HW] from x and dy. */
-int turtle_train_gate_fwd(const void* x, void* y, int64_t N, int h, int64_t HW, int dtype, void* stream);
-int turtle_train_gate_bwd(const void* x, const void* dy, void* dx, int64_t N, int h, int64_t HW, int dtype, void* stream);
+/* GatedFeedForward gate (turtle_t1_arch.py:176): x [P][ldx] (x1 = channels [0, h), x2 = [h, 2h))
+ * -> y [P][ldy] = gelu(x1) * x2 (exact erf GELU); backward dx [P][lddx] (2h channels) from x, dy. */
+int turtle_train_gate_fwd(const void* x, int64_t ldx, void* y, int64_t ldy, int64_t P, int h, int dtype, void* stream);
+int turtle_train_gate_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx, int64_t P, int h,
+                          int dtype, void* stream);
+
+/* column sums db[n] += sum_p dy[p][n] (a 1x1 convolution's bias gradient), N % 8 == 0 */
+int turtle_train_colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, int dtype, void* stream);
+
+/* pointwise GEMM (a 1x1 convolution, nn.Conv2d(K, N, 1) on NHWC rows; also its input gradient with
+ * W transposed, and the channel-attention A.v with per-image weights):
+ *   y[p][n] = sum_k x[p][k] w[img(p)][n][k] + bias[n]
+ * w [N][K] in the activation dtype; wstride = 0: one weight set, else set i at w + i * wstride
+ * elements for the i-th run of img_px pixels. bias fp32 [N] or NULL. K % 8 == N % 8 == 0. Runs on
+ * the inference GEMM family (gemm*.hip). */
+int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride, int64_t img_px, const float* bias, void* y,
+                      int64_t ldy, int64_t P, int K, int N, int dtype, void* stream);
+
+/* reduction GEMM over pixels (a 1x1 convolution's weight gradient dW = dY^T X; the channel
+ * attention Gram q^T k over HW, turtle_t1_arch.py:694-697, and its backward):
+ *   c[img][n][k] (+)= sum_{p in img} a[p][n] b[p][k]
+ * img_px = 0: one product over all P pixels; else one per run of img_px pixels (P % img_px == 0).
+ * c fp32 [nimg][N][K]; accumulate = 1 adds into c. Needs a workspace of
+ * turtle_train_rgemm_workspace(P, N, K, img_px) bytes. Deterministic (fixed reduction order). */
+size_t turtle_train_rgemm_workspace(int64_t P, int N, int K, int64_t img_px);
+int turtle_train_rgemm(const void* a, int64_t lda, const void* b, int64_t ldb, float* c, int64_t P, int N, int K, int64_t img_px,
+                       int accumulate, int dtype, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,7 @@ import torch.nn.functional as F
 
 
 class AtenOps:
+    channels_last = False
     @staticmethod
     def layer_norm(x, w, b, biasfree):
         mu = x.mean(dim=1, keepdim=True)
@@ -23,3 +24,16 @@ class AtenOps:
     def gelu_gate(x):
         h = x.shape[1] // 2
         return F.gelu(x[:, :h]) * x[:, h:]
+
+    @staticmethod
+    def conv1x1(x, w, b):
+        if w.dim() == 4:
+            return F.conv2d(x, w, b)
+        y = torch.einsum("bkhw,bnk->bnhw", x, w)        # one weight set per image
+        return y if b is None else y + b.view(1, -1, 1, 1)
+
+    @staticmethod
+    def gram(q, k, heads):
+        b, c, h, w = q.shape
+        qh, kh = q.reshape(b, heads, c // heads, h * w), k.reshape(b, heads, c // heads, h * w)
+        return qh @ kh.transpose(-2, -1)

@@ -7,19 +7,24 @@
   3). Gate: PSNR(HIP, oracle) >= 80 dB and the PSNR-vs-clean of the HIP output within 1e-3 dB of
   the oracle's (the north-star's fp32 "1e-3 PSNR" bar), per frame; the bf16 build's uint8 PSNR vs
   clean (the reference protocol, inference.py:324-325 + calc_PSNR 52-61) within 0.01 dB of the
-  fp32 build's (the north-star's bf16 bar).
+  fp32 build's (the north-star's bf16 bar). The same bf16 bar at the headline 1920x1080 size on
+  the bench's own denoising clip and weights (test_1080p_bf16_psnr_delta_bench_protocol).
 * Config 4 (Turtle_SR_MVSR 4x, 1080p output, bf16): TurtleSuper_t1 at GoPro widths on a
   480x270 LR frame -> 1920x1080: bf16 >= 58 dB vs the HIP fp32 build at full size; fp32 HIP vs the
   oracle (turtlesuper_t1_arch.py:976-977, 1049-1071) at 128x72 -> 512x288, PSNR >= 80 dB.
 Weights: the deterministic synthetic GoPro-width state dict of the golden clips (parity is
 weight-agnostic; trained checkpoints are not available offline).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
 
 from golden_io import load, synth_sd
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 pytestmark = pytest.mark.gpu
 
@@ -85,6 +90,34 @@ def test_davis_540p_fp32_psnr_delta():
         d16 = abs(psnr_u8(o16[j], clean[:, j]) - psnr_u8(o, clean[:, j]))
         print(f"frame {j}: uint8 PSNR vs clean fp32 {psnr_u8(o, clean[:, j]):.4f} dB, bf16 delta {d16:.5f} dB")
         assert d16 <= 0.01, (j, d16)
+
+
+@pytest.mark.timeout(600)
+def test_1080p_bf16_psnr_delta_bench_protocol():
+    """North-star PSNR bar at the headline configuration: the bench's own denoising clip
+    (bench.denoise_clip: smooth clean frames + N(0, 25/255), 1920x1080, 4 causal frames, GoPro arch
+    and the bench's synthetic weights) through the fp32 and bf16 builds; uint8 PSNR vs the clean
+    frames (tensor2img + calc_PSNR, inference.py:52-61, 324-325) must agree within 0.01 dB on every
+    frame (two clips)."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    dev = torch.device("cuda", 0)
+    opt = bench.load_opt()
+    m32, m16 = bench.build_model(opt, "fp32", dev), bench.build_model(opt, "bf16", dev)
+    worst = 0.0
+    for seed in (3, 5):
+        clean, noisy = bench.denoise_clip(4, 1080, 1920, 1, dev, seed=seed)
+        k32 = v32 = k16 = v16 = None
+        with torch.no_grad():
+            for j in range(4):
+                x = torch.stack([noisy[:, max(j - 1, 0)], noisy[:, j]], dim=1).contiguous()
+                o32, k32, v32 = m32(x, k32, v32)
+                o16, k16, v16 = m16(x, k16, v16)
+                d = abs(psnr_u8(o16, clean[:, j]) - psnr_u8(o32, clean[:, j]))
+                print(f"seed {seed} frame {j}: uint8 PSNR fp32 {psnr_u8(o32, clean[:, j]):.4f} dB, bf16 delta {d:.5f} dB")
+                worst = max(worst, d)
+    assert worst <= 0.01, worst
 
 
 def test_sr_1080p_bf16_vs_fp32():

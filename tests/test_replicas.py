@@ -5,6 +5,7 @@ these tests run that aggregation in two real processes (gloo, 127.0.0.1) with un
 times and frame counts, and the clip assignment / seeding it relies on."""
 import os
 import socket
+import sys
 
 import pytest
 import torch.distributed as dist
@@ -92,3 +93,18 @@ def test_launcher_spawns_one_worker_per_gpu_gloo():
 def test_launcher_refuses_mismatched_world():
     rc, lines, err = _probe(["2"], env={"WORLD_SIZE": "4", "RANK": "0"})
     assert rc != 0 and not lines and "WORLD_SIZE=4" in err
+
+
+def test_launcher_stops_the_group_when_a_worker_fails():
+    """One shared deadline for the whole group; a worker failing (here rank 1, before any
+    rendezvous) ends its siblings at once and its exit code is returned."""
+    import time
+    from turtlevsr_amd.replicas import launch_workers
+    code = "import os, sys, time; r = int(os.environ['RANK']); sys.exit(3) if r == 1 else time.sleep(60)"
+    t0 = time.monotonic()
+    assert launch_workers(3, [sys.executable, "-c", code]) == 3
+    assert time.monotonic() - t0 < 30
+    t0 = time.monotonic()
+    assert launch_workers(2, [sys.executable, "-c", "import time; time.sleep(60)"], timeout=1.0) == 124
+    assert time.monotonic() - t0 < 30
+    assert launch_workers(2, [sys.executable, "-c", "pass"]) == 0

@@ -62,6 +62,81 @@ def test_graph_gradients_match_reference(name):
     assert _check_grads(net, g, rtol=2e-3, atol=2e-6) == meta["n_params"]
 
 
+def optimize_parameters(net_g, optimizer_g, scaler, lq, gt, amp_dtype=None):
+    """The body of VideoRestorationModel.optimize_parameters (video_restoration_model.py:78-107),
+    restated: autocast forward over the clip with un-detached caches, frame-averaged L1,
+    + 0 * sum(p), scaled backward, unscale, AdamW step, scaler update. The reference runs
+    torch.cuda.amp.autocast() (fp16) on lq.half() inputs (feed_data, :73-76)."""
+    loss = torch.nn.L1Loss()
+    optimizer_g.zero_grad()
+    dev = lq.device.type
+    with torch.autocast(device_type=dev, dtype=amp_dtype or torch.float32, enabled=amp_dtype is not None):
+        l_pix = 0
+        frame_num = lq.shape[1]
+        k_cache, v_cache = None, None
+        for j in range(frame_num):
+            target_g_images = gt[:, j, :, :, :]
+            current_input = lq[:, j, :, :, :].unsqueeze(1)
+            pre_input = lq[:, j if j == 0 else j - 1, :, :, :].unsqueeze(1)
+            inp = torch.concat([pre_input, current_input], dim=1)
+            out_g, k_cache, v_cache = net_g(inp, k_cache, v_cache)
+            l_pix += loss(out_g, target_g_images)
+    l_pix /= frame_num
+    l_total = l_pix + 0 * sum(p.sum() for p in net_g.parameters())
+    scaler.scale(l_total).backward()
+    scaler.unscale_(optimizer_g)
+    scaler.step(optimizer_g)
+    scaler.update()
+    return float(l_pix.detach())
+
+
+def _dropin(meta, dev, ops=None):
+    """The module the reference's model wrapper builds: import_module('basicsr.models.archs.' +
+    opt['model'].lower()).make_model(opt) (video_restoration_model.py:18-21), in train mode (:42)."""
+    from importlib import import_module
+    net = import_module("basicsr.models.archs.turtle_t1_arch").make_model(meta["opt"])
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    net.load_state_dict(synth_sd(shapes, meta["seed"]), strict=True)
+    if ops is not None:
+        net.graph_ops = ops
+    return net.to(dev).train()
+
+
+def _adamw(net):
+    return torch.optim.AdamW([p for p in net.parameters() if p.requires_grad], lr=4e-4, betas=(0.9, 0.99), weight_decay=0)
+
+
+@pytest.mark.parametrize("name", ["train_tiny", "train_tiny_hetero"])
+def test_dropin_module_trains_under_reference_loop(name):
+    """make_model(opt)'s module in train mode is differentiable: the reference's optimize_parameters
+    body gives the reference's loss and gradients (ATen op set on CPU), and AdamW moves the weights."""
+    torch.set_num_threads(8)
+    g, meta = load(name)
+    net = _dropin(meta, "cpu", AtenOps)
+    before = {k: p.detach().clone() for k, p in net.named_parameters()}
+    lq, gt = _data(meta)
+    l = optimize_parameters(net, _adamw(net), torch.amp.GradScaler("cpu", enabled=False), lq, gt)
+    assert l == pytest.approx(float(g["loss"]), rel=1e-5)
+    assert _check_grads(net, g, rtol=2e-3, atol=2e-6) == meta["n_params"]
+    moved = sum(int(not torch.equal(before[k], p.detach())) for k, p in net.named_parameters())
+    assert moved > 0.9 * meta["n_params"]
+
+
+def test_dropin_module_inference_modes_stay_on_hip():
+    """eval() (validation, inference.py:253) or no_grad never builds the graph: on CPU the HIP
+    inference path refuses, so nothing silently falls back to ATen."""
+    _, meta = load("train_tiny")
+    net = _dropin(meta, "cpu", AtenOps)
+    x = torch.rand(1, 2, 3, 64, 64)
+    with pytest.raises(RuntimeError):
+        net.eval()(x)
+    with torch.no_grad(), pytest.raises(RuntimeError):
+        net.train()(x)
+    net2 = _dropin(meta, "cpu")                       # default op set: HIP kernels only
+    with pytest.raises(RuntimeError):
+        net2.train()(x)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -169,6 +244,36 @@ def test_hip_train_ops_match_autograd(dtype):
     (rx,) = torch.autograd.grad(y2, [x2], gy.float())
     torch.testing.assert_close(y.float(), y2, **tol)
     torch.testing.assert_close(gx.float(), rx, **tol)
+    # 1x1 convolution (shared and per-image weights) and the per-head Gram, forward and backward,
+    # on channels-last views with a row stride (a slice of a wider tensor, as q / k / v of qkv)
+    gtol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=8e-2)
+    for per_image in (False, True):
+        base = torch.randn(3, 96, 13, 9, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+        x = base[:, 16:80].detach().requires_grad_()                   # K = 64, row stride 96
+        w = (0.1 * torch.randn(*((3, 40, 64) if per_image else (40, 64, 1, 1)), device=dev)).requires_grad_()
+        b = (0.1 * torch.randn(40, device=dev)).requires_grad_()
+        gy = torch.randn(3, 40, 13, 9, device=dev).to(dtype)
+        y = HipOps.conv1x1(x, w, b)
+        gx, gw, gb = torch.autograd.grad(y, [x, w, b], gy)
+        x2, w2, b2 = (t.detach().float().requires_grad_() for t in (x, w, b))
+        y2 = AtenOps.conv1x1(x2, w2, b2)
+        rx, rw, rb = torch.autograd.grad(y2, [x2, w2, b2], gy.float())
+        torch.testing.assert_close(y.float(), y2, **gtol)
+        torch.testing.assert_close(gx.float(), rx, **gtol)
+        torch.testing.assert_close(gw.float(), rw, rtol=gtol["rtol"], atol=gtol["atol"] * 20)
+        torch.testing.assert_close(gb, rb, rtol=gtol["rtol"], atol=gtol["atol"] * 20)
+    for heads in (1, 4):
+        qk = torch.randn(2, 256, 17, 19, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+        q, k = qk[:, :128].detach().requires_grad_(), qk[:, 128:].detach().requires_grad_()
+        G = HipOps.gram(q, k, heads)
+        gG = torch.randn_like(G)
+        gq, gk = torch.autograd.grad(G, [q, k], gG)
+        q2, k2 = q.detach().float().requires_grad_(), k.detach().float().requires_grad_()
+        G2 = AtenOps.gram(q2, k2, heads)
+        rq, rk = torch.autograd.grad(G2, [q2, k2], gG)
+        torch.testing.assert_close(G, G2, rtol=gtol["rtol"], atol=gtol["atol"] * 20)
+        torch.testing.assert_close(gq.float(), rq, **gtol)
+        torch.testing.assert_close(gk.float(), rk, **gtol)
 
 
 @pytest.mark.gpu
@@ -200,3 +305,31 @@ def test_bf16_train_steps_gopro_network():
     gt = (lq + 0.05 * torch.from_numpy(synthetic_frames((2, 3, 3, 128, 128), 42, name="gt")).cuda()).clamp(0, 1)
     losses = [tr.train_step(lq, gt) for _ in range(3)]
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses
+
+
+@pytest.mark.gpu
+def test_dropin_module_reference_loop_gpu_fp32_and_fp16():
+    """make_model(opt) on the GPU under the reference's optimize_parameters: fp32 gradients equal
+    the reference's (train_tiny), then one fp16-autocast + GradScaler step (the reference's own
+    training precision, video_restoration_model.py:39, 80, 102-107) completes with a finite loss and
+    finite, moved weights."""
+    g, meta = load("train_tiny")
+    net = _dropin(meta, "cuda")
+    lq, gt = _data(meta, "cuda")
+    opt = _adamw(net)
+    l = optimize_parameters(net, opt, torch.amp.GradScaler("cuda", enabled=False), lq, gt)
+    torch.cuda.synchronize()
+    assert l == pytest.approx(float(g["loss"]), rel=1e-4)
+    assert _check_grads(net, g, rtol=1e-2, atol=1e-5) == meta["n_params"]
+    before = {k: p.detach().clone() for k, p in net.named_parameters()}
+    scaler = torch.amp.GradScaler("cuda")
+    losses = [optimize_parameters(net, opt, scaler, lq.half(), gt, amp_dtype=torch.float16) for _ in range(2)]
+    torch.cuda.synchronize()
+    assert all(np.isfinite(losses)), losses
+    assert all(torch.isfinite(p).all() for p in net.parameters())
+    moved = sum(int(not torch.equal(before[k], p.detach())) for k, p in net.named_parameters())
+    assert moved > 0.9 * meta["n_params"]
+    # back in eval mode the same module restores on the HIP inference path
+    with torch.no_grad():
+        out, _, _ = net.eval()(torch.stack([lq[:, 0], lq[:, 0]], 1).float())
+    assert torch.isfinite(out).all()

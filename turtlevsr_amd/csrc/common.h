@@ -15,11 +15,15 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 #define TURTLE_DEV __device__ __forceinline__
 
+typedef _Float16 f16;          // fp16 activations of the training kernels (the reference's autocast)
+
 TURTLE_DEV float to_f(float x) { return x; }
 TURTLE_DEV float to_f(bf16 x) { return (float)x; }
+TURTLE_DEV float to_f(f16 x) { return (float)x; }
 template <typename T> TURTLE_DEV T from_f(float x);
 template <> TURTLE_DEV float from_f<float>(float x) { return x; }
 template <> TURTLE_DEV bf16 from_f<bf16>(float x) { return (bf16)x; }
+template <> TURTLE_DEV f16 from_f<f16>(float x) { return (f16)x; }
 
 // 16-byte vector of storage elements, unpacked to fp32 registers.
 template <typename T> struct Vec;

@@ -11,14 +11,14 @@
 // HBM: each K step of 16 channels computes its A tile from the raw hidden map staged in LDS.
 //
 // Structure (MI355X, bf16, fp32 accumulation):
-//   * block = 256 threads (4 waves), output tile = 4 image rows x 32 columns (128 pixels) x 256
-//     output channels; wave tile 64 pixels x 128 channels (MFMA 16x16x32, 128 accumulators);
-//   * K step s: the weights of step s + 1 go HBM/L2 -> LDS by LDS-DMA while the waves run the
-//     MFMAs of step s, then every thread computes the depthwise of step s + 1 for one column,
-//     8 channels, 2 output rows (4 input rows x 3 columns, loaded as 16-byte vectors: the column
-//     neighbours are L1 hits of the neighbouring lanes' loads) and writes its A fragment rows to
-//     the other A buffer. One barrier per K step;
-//   * the depthwise tap weights of step s + 2 are loaded during step s and parked in LDS;
+//   * block = 512 threads (8 waves, a 4 x 2 wave grid), output tile = 8 image rows x 32 columns
+//     (256 pixels) x 256 output channels; wave tile 64 pixels x 128 channels (MFMA 16x16x32,
+//     128 accumulators per lane), one block per CU;
+//   * K step s (16 hidden channels): the haloed 10 x 34 pixel input tile of step s + 3 (x1 [, x2]
+//     16 channels, the bf16 tap table and the fp32 bias) and the weights of step s + 2 go
+//     HBM/L2 -> LDS by LDS-DMA into a 4-slot / 5-slot ring while the waves work; wave w computes
+//     the depthwise of output row w on the matrix cores (below) and writes its gated A rows to the
+//     3-slot A ring; the GEMM runs on pairs of K steps. One barrier per K step;
 //   * weight rows are read in the permuted order of the kt / pn GEMMs (MFMA row 4g+e of sub-tile
 //     t <- channel 8g+4t+e of a 32-channel group), so a lane's accumulators hold 8 consecutive
 //     output channels of one pixel: register-direct epilogue, 16-byte residual loads and stores;

@@ -556,7 +556,7 @@ static void launch_cfg(const GemmArgs& g, hipStream_t st) {
 template <typename T>
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.store_mode == STORE_CB16) {                // produced only for the pn kernel (turtle.cpp)
-    if (sizeof(T) != 2 || !gemm_pn_ok(g)) abort();
+    if (sizeof(T) != 2 || !gemm_pn_ok(g)) kernel_arg_error("channel-blocked GEMM store needs the bf16 pn kernel");
     launch_gemm_pn(g, st);
     return;
   }

@@ -723,6 +723,9 @@ __global__ __launch_bounds__(256) void ending_tile_kernel(EndArgs a) {
       const bf16x8 bv = *reinterpret_cast<const bf16x8*>(sx + (r * TW + cc) * PB + c * 2);
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[st], bv, acc, 0, 0, 0);
     }
+    // rows 4..7 (lanes 16..31) hold the split-bf16 remainder part of the weights (turtle.cpp)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += __shfl_down(acc[i], 16, 64);
     const int x = x0 + xl;
     if (g == 0 && y < a.Hout && x < a.Wout) {
 #pragma unroll
@@ -807,10 +810,11 @@ bool stem_end_mfma_ok(int cin_end, int cin_stem, int cout_stem) {
   return cin_end == 64 && cout_stem == 64 && (cin_stem == 3 || cin_stem == 6);
 }
 
-void launch_ending_mfma(const EndArgs& a, hipStream_t st) {
-  if (!a.wfrag || a.Cin != 64) abort();            // packed by turtle.cpp for the 64-channel ending
+bool launch_ending_mfma(const EndArgs& a, hipStream_t st) {
+  if (!a.wfrag || a.Cin != 64 || a.Cimg < 1 || a.Cimg > 4) return false;   // fragments packed by turtle.cpp; bias[4]
   const int64_t tiles = (int64_t)a.B * ((a.Hp + ET_R - 1) / ET_R) * ((a.Wp + ET_C - 1) / ET_C);
   hipLaunchKernelGGL(ending_tile_kernel<64>, dim3((unsigned)tiles), dim3(256), 0, st, a);
+  return true;
 }
 
 void launch_stem_mfma(const StemArgs& a, hipStream_t st) {

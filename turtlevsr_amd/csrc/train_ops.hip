@@ -1,107 +1,207 @@
-// Training-path kernels with hand-written backward (include/turtle_train.h), NCHW tensors as the
-// torch autograd graph holds them, fp32 or bf16 storage, fp32 arithmetic:
+// Training-path kernels with hand-written backward (include/turtle_train.h). The training graph
+// (turtlevsr_amd/train.py) holds its activations channels-last (NHWC: a pixel's channels
+// contiguous, the inference path's layout), so every kernel here reads and writes pixel rows with a
+// row stride `ld` (elements) and fp32 / bf16 / fp16 storage, fp32 arithmetic:
 //
-//   channel LayerNorm   y = (x - mu) * rstd * w + b  (BiasFree: x * rstd * w), per pixel over C
-//                       (turtle_t1_arch.py:67-112); backward gives dx, dw, db
-//   depthwise 3x3       y = dw3x3(x) + b, pad 1 (qkv_dwconv / conv2 / dwconv / kv_dwconv);
-//                       backward dx (the same stencil with the taps flipped) and dw, db
-//   GELU gate           y = gelu(x1) * x2 over the two channel halves (GatedFeedForward 176)
+//   channel LayerNorm   y = (x - mu) rstd w + b (BiasFree: x rstd w) per pixel over C
+//                       (turtle_t1_arch.py:67-112); backward dx, dw, db
+//   depthwise 3x3       y = dw3x3(x) + b, pad 1 (qkv_dwconv / conv2 / dwconv / kv_dwconv); dgrad =
+//                       the same stencil with the taps rotated 180 degrees; wgrad dw, db
+//   GELU gate           y = gelu(x1) x2 over the two channel halves (GatedFeedForward 176)
+//   column sums         db[n] = sum_p dy[p][n] (1x1 conv bias gradients)
+//   reduction GEMM      C[img][n][k] = sum_p A[p][n] B[p][k] over the pixels of each image (or of
+//                       all images): 1x1 conv weight gradients (dW = dY^T X), the channel
+//                       attention Gram (q^T k over HW) and its backward. bf16 on the matrix cores:
+//                       pixel-major tiles staged in LDS, both operands read with the gfx950
+//                       transposing LDS read (ds_read_b64_tr_b16) so the contraction runs over
+//                       pixels; fp32 partials per pixel split, reduced by a second pass in a fixed
+//                       order (deterministic)
+//   forward / data GEMM Y[p][n] = sum_k X[p][k] W[n][k] (+ b): the inference GEMM family
+//                       (gemm*.hip), per-image weight sets optional (attention W_eff)
 //
-// Weight gradients are per-channel reductions over all pixels: each block reduces its pixels in
-// registers / LDS and adds one fp32 partial per channel (and tap) with a device atomic; the
-// caller zeroes the gradient buffers first (torch.zeros).
+// Per-channel weight gradients (LN, depthwise, bias) reduce each block's pixels in registers /
+// LDS and add one fp32 partial per channel per block with a device atomic into buffers the caller
+// zeroed.
 #include "common.h"
+#include "kernels.h"
 #include "../../include/turtle_train.h"
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <vector>
 
 namespace turtle {
 
-template <typename T> TURTLE_DEV float ldf(const T* p, int64_t i) { return to_f(p[i]); }
-template <typename T> TURTLE_DEV void stf(T* p, int64_t i, float v) { p[i] = from_f<T>(v); }
-
 TURTLE_DEV float gelu_exact(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
-TURTLE_DEV float gelu_exact_grad(float x) {   // d/dx x * Phi(x) = Phi(x) + x * phi(x)
+TURTLE_DEV float gelu_exact_grad(float x) {   // d/dx x Phi(x) = Phi(x) + x phi(x)
   const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
   const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
   return cdf + x * pdf;
 }
 
-// ---------------------------------------------------------------------------------------------
-// channel LayerNorm: one thread per pixel, channel loop strided by HW (coalesced across threads)
-// ---------------------------------------------------------------------------------------------
-template <typename T>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                     const float* __restrict__ b, T* __restrict__ y,
-                                                     float* __restrict__ mu, float* __restrict__ rstd,
-                                                     int64_t N, int C, int64_t HW, int biasfree) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= N * HW) return;
-  const int64_t n = i / HW, p = i - n * HW;
-  const T* xp = x + n * C * HW + p;
-  const float sh = ldf(xp, 0);
-  float s = 0.f, q = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float d = ldf(xp, (int64_t)c * HW) - sh;
-    s += d;
-    q = fmaf(d, d, q);
-  }
-  const float md = s / C, m = sh + md;
-  const float r = rsqrtf(fmaxf(q / C - md * md, 0.f) + 1e-5f);
-  mu[i] = m;
-  rstd[i] = r;
-  T* yp = y + n * C * HW + p;
-  for (int c = 0; c < C; ++c) {
-    const float v = ldf(xp, (int64_t)c * HW);
-    stf(yp, (int64_t)c * HW, biasfree ? v * r * w[c] : fmaf((v - m) * r, w[c], b[c]));
+// 8 consecutive elements <-> fp32 (16 B for 2-byte types, 32 B for fp32)
+template <typename T> TURTLE_DEV void ld8f(const T* p, float (&v)[8]);
+template <> TURTLE_DEV void ld8f<float>(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <> TURTLE_DEV void ld8f<bf16>(const bf16* p, float (&v)[8]) {
+  const uint4 q = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(w[i] << 16); v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u); }
+}
+template <> TURTLE_DEV void ld8f<f16>(const f16* p, float (&v)[8]) {
+  typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+  const h8 q = *reinterpret_cast<const h8*>(p);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (float)q[i];
+}
+template <typename T> TURTLE_DEV void st8f(T* p, const float (&v)[8]) {
+  if constexpr (sizeof(T) == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    typedef T t8 __attribute__((ext_vector_type(8)));
+    t8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (T)v[i];
+    *reinterpret_cast<t8*>(p) = o;
   }
 }
 
-// backward: per pixel, g = w * dy;
-//   WithBias: xh = (x - mu) r,  dx = r (g - mean(g) - xh mean(g xh))
-//   BiasFree: y = w x r (r of the centred variance), dx = r g - (x - mu) r^3 mean(g x)
-// dw[c] = sum_p dy xhat_c (xhat = (x - mu) r, BiasFree: x r), db[c] = sum_p dy: block partials in
-// LDS, one atomic per channel per block
-template <typename T>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
+// lanes per pixel for a C-channel row: a power of two covering C / 8 chunks (<= 64)
+static int ln_group(int C) {
+  int g = 1;
+  while (g < C / 8 && g < 64) g <<= 1;
+  return g;
+}
+template <int G>
+TURTLE_DEV float group_sum(float v) {
+#pragma unroll
+  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// channel LayerNorm, NHWC: G lanes per pixel, each lane NCH chunks of 8 channels
+// ---------------------------------------------------------------------------------------------
+template <typename T, int G, int NCH>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ w,
+                                                     const float* __restrict__ b, T* __restrict__ y, int64_t ldy,
+                                                     float* __restrict__ mu, float* __restrict__ rstd, int64_t P, int C,
+                                                     int biasfree) {
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t p = gid / G;
+  const int l = (int)(gid % G);
+  const bool live = p < P;
+  const int64_t pp = live ? p : 0;
+  float v[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = 8 * (l + G * j);
+    if (c < C) {
+      ld8f(x + pp * ldx + c, v[j]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[j][e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += v[j][e];
+  }
+  const float m = group_sum<G>(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+    if (8 * (l + G * j) < C)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[j][e] - m; q = fmaf(d, d, q); }
+  const float r = rsqrtf(group_sum<G>(q) / C + 1e-5f);
+  if (live && l == 0) { mu[p] = m; rstd[p] = r; }
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = 8 * (l + G * j);
+    if (!live || c >= C) continue;
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = biasfree ? v[j][e] * r * w[c + e] : fmaf((v[j][e] - m) * r, w[c + e], b[c + e]);
+    st8f(y + p * ldy + c, o);
+  }
+}
+
+// backward: g = w dy;  WithBias: xh = (x - mu) r, dx = r (g - mean(g) - xh mean(g xh));
+// BiasFree (y = w x r, r of the centred variance): dx = r g - (x - mu) r^3 mean(g x).
+// dw[c] = sum_p dy xhat (BiasFree xhat = x r), db[c] = sum_p dy: per-lane accumulators over the
+// block's pixels -> LDS -> one atomic per channel per block
+template <typename T, int G, int NCH>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ w,
                                                      const float* __restrict__ mu, const float* __restrict__ rstd,
-                                                     const T* __restrict__ dy, T* __restrict__ dx,
-                                                     float* __restrict__ dw, float* __restrict__ db,
-                                                     int64_t N, int C, int64_t HW, int biasfree) {
-  extern __shared__ float sred[];                  // [2][C] block partials of dw, db
+                                                     const T* __restrict__ dy, int64_t lddy, T* __restrict__ dx, int64_t lddx,
+                                                     float* __restrict__ dw, float* __restrict__ db, int64_t P, int C,
+                                                     int biasfree, int ppb) {
+  extern __shared__ float sred[];                  // [2][C]
   for (int c = threadIdx.x; c < 2 * C; c += 256) sred[c] = 0.f;
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const bool live = i < N * HW;
-  const int64_t ii = live ? i : 0;
-  const int64_t n = ii / HW, p = ii - n * HW;
-  const T* xp = x + n * C * HW + p;
-  const T* gp = dy + n * C * HW + p;
-  const float m = mu[ii], r = rstd[ii];
-  float sg = 0.f, sgx = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float g = w[c] * ldf(gp, (int64_t)c * HW);
-    const float v = ldf(xp, (int64_t)c * HW);
-    sg += g;
-    sgx = fmaf(g, biasfree ? v : (v - m) * r, sgx);
+  const int l = threadIdx.x % G, slot = threadIdx.x / G, nslot = 256 / G;
+  float aw[NCH][8], ab[NCH][8];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) aw[j][e] = ab[j][e] = 0.f;
+  const int64_t p0 = (int64_t)blockIdx.x * ppb;
+  const int64_t p1 = min(P, p0 + ppb);
+  for (int64_t pb = p0; pb < p1; pb += nslot) {     // uniform trip count across the block
+    const int64_t p = pb + slot;
+    const bool live = p < p1;
+    const int64_t pp = live ? p : p0;
+    const float m = mu[pp], r = rstd[pp];
+    float xv[NCH][8], gy[NCH][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = 8 * (l + G * j);
+      if (c < C) {
+        ld8f(x + pp * ldx + c, xv[j]);
+        ld8f(dy + pp * lddy + c, gy[j]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[j][e] = gy[j][e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = (c < C ? w[c + e] : 0.f) * gy[j][e];
+        sg += g;
+        sgx = fmaf(g, biasfree ? xv[j][e] : (xv[j][e] - m) * r, sgx);
+      }
+    }
+    const float mg = group_sum<G>(sg) / C, mgx = group_sum<G>(sgx) / C;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = 8 * (l + G * j);
+      if (c >= C) continue;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float g = w[c + e] * gy[j][e];
+        o[e] = biasfree ? r * g - (xv[j][e] - m) * r * r * r * mgx : r * (g - mg - (xv[j][e] - m) * r * mgx);
+        if (live) {
+          aw[j][e] = fmaf(gy[j][e], biasfree ? xv[j][e] * r : (xv[j][e] - m) * r, aw[j][e]);
+          ab[j][e] += gy[j][e];
+        }
+      }
+      if (live) st8f(dx + p * lddx + c, o);
+    }
   }
-  const float mg = sg / C, mgx = sgx / C;
-  T* dp = dx + n * C * HW + p;
-  const int lane = threadIdx.x & 63;
-  for (int c = 0; c < C; ++c) {
-    const float gy = ldf(gp, (int64_t)c * HW);
-    const float v = ldf(xp, (int64_t)c * HW);
-    const float g = w[c] * gy;
-    float d;
-    if (biasfree) d = r * g - (v - m) * r * r * r * mgx;
-    else d = r * (g - mg - (v - m) * r * mgx);
-    if (live) stf(dp, (int64_t)c * HW, d);
-    // channel partials: wave sums, then one LDS atomic per wave
-    float pw = live ? gy * (biasfree ? v * r : (v - m) * r) : 0.f;
-    float pb = live ? gy : 0.f;
-    pw = wave_sum(pw);
-    pb = wave_sum(pb);
-    if (lane == 0) {
-      atomicAdd(&sred[c], pw);
-      atomicAdd(&sred[C + c], pb);
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) {
+    const int c = 8 * (l + G * j);
+    if (c >= C) continue;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      atomicAdd(&sred[c + e], aw[j][e]);
+      atomicAdd(&sred[C + c + e], ab[j][e]);
     }
   }
   __syncthreads();
@@ -112,184 +212,524 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ x, co
 }
 
 // ---------------------------------------------------------------------------------------------
-// depthwise 3x3, pad 1: one block per (image, channel) row band; 256 threads = 256 pixels of a
-// 16 x 16 output tile, haloed 18 x 18 input tile in LDS
+// depthwise 3x3, pad 1, NHWC: one thread per (pixel, 8-channel chunk); w9 tap-major [9][C] fp32
 // ---------------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                     const float* __restrict__ b, T* __restrict__ y, int C, int H, int W,
-                                                     int flip) {
-  __shared__ float tile[18][19];
-  const int tx_n = (W + 15) / 16;
-  const int tile_id = blockIdx.x, plane = blockIdx.y;   // plane = n * C + c
-  const int c = plane % C;
-  const int ty0 = (tile_id / tx_n) * 16, tx0 = (tile_id % tx_n) * 16;
-  const T* xp = x + (int64_t)plane * H * W;
-  for (int e = threadIdx.x; e < 18 * 18; e += 256) {
-    const int r = e / 18, q = e - r * 18;
-    const int yy = ty0 - 1 + r, xx = tx0 - 1 + q;
-    tile[r][q] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? ldf(xp, (int64_t)yy * W + xx) : 0.f;
-  }
-  __syncthreads();
-  const int oy = threadIdx.x >> 4, ox = threadIdx.x & 15;
-  const int yy = ty0 + oy, xx = tx0 + ox;
-  if (yy >= H || xx >= W) return;
-  float acc = b ? b[c] : 0.f;
+__global__ __launch_bounds__(256) void dw_fwd_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ w9,
+                                                     const float* __restrict__ b, T* __restrict__ y, int64_t ldy, int64_t N,
+                                                     int C, int H, int W, int flip) {
+  const int nch = C / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t tot = N * H * W * nch;
+  if (gid >= tot) return;
+  const int ch = (int)(gid % nch);
+  const int64_t pix = gid / nch;
+  const int xx = (int)(pix % W);
+  const int64_t t = pix / W;
+  const int yy = (int)(t % H);
+  const int64_t n = t / H;
+  const int c = 8 * ch;
+  float acc[8];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) {
-    const float wt = w[c * 9 + (flip ? 8 - t : t)];
-    acc = fmaf(wt, tile[oy + t / 3][ox + t % 3], acc);
+  for (int e = 0; e < 8; ++e) acc[e] = b ? b[c + e] : 0.f;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int sy = yy + tap / 3 - 1, sx = xx + tap % 3 - 1;
+    if (sy < 0 || sy >= H || sx < 0 || sx >= W) continue;
+    float v[8];
+    ld8f(x + ((n * H + sy) * W + sx) * ldx + c, v);
+    const float* wt = w9 + (flip ? 8 - tap : tap) * C + c;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = fmaf(wt[e], v[e], acc[e]);
   }
-  stf(y + (int64_t)plane * H * W, (int64_t)yy * W + xx, acc);
+  st8f(y + pix * ldy + c, acc);
 }
 
-// dw[c][t] = sum_{n,p} dy[n,c,p] x[n,c,p + off(t)], db[c] = sum dy: tile as in the forward, each
-// thread 10 partial sums, block reduction, 10 atomics per block
+// dw9[t][c] = sum dy[n,y,x,c] x[n, y + dy_t, x + dx_t, c], db[c] = sum dy: a block takes a slice
+// of CPB 8-channel chunks (blockIdx.y) and a contiguous pixel range (blockIdx.x); thread = (chunk,
+// pixel lane), 80 accumulators, LDS block reduction, one atomic per (tap, channel) per block
+constexpr int DWG_CPB = 32;
 template <typename T>
-__global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x, const T* __restrict__ dy,
-                                                       float* __restrict__ dw, float* __restrict__ db, int C, int H, int W) {
-  __shared__ float tile[18][19];
-  __shared__ float red[4][10];
-  const int tx_n = (W + 15) / 16;
-  const int tile_id = blockIdx.x, plane = blockIdx.y;
-  const int c = plane % C;
-  const int ty0 = (tile_id / tx_n) * 16, tx0 = (tile_id % tx_n) * 16;
-  const T* xp = x + (int64_t)plane * H * W;
-  for (int e = threadIdx.x; e < 18 * 18; e += 256) {
-    const int r = e / 18, q = e - r * 18;
-    const int yy = ty0 - 1 + r, xx = tx0 - 1 + q;
-    tile[r][q] = (yy >= 0 && yy < H && xx >= 0 && xx < W) ? ldf(xp, (int64_t)yy * W + xx) : 0.f;
+__global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy,
+                                                       int64_t lddy, float* __restrict__ dw9, float* __restrict__ db,
+                                                       int64_t N, int C, int H, int W, int64_t ppb) {
+  __shared__ float sred[10 * DWG_CPB * 8];
+  for (int i = threadIdx.x; i < 10 * DWG_CPB * 8; i += 256) sred[i] = 0.f;
+  __syncthreads();
+  const int nch = min(C / 8 - (int)blockIdx.y * DWG_CPB, DWG_CPB);   // chunks in this slice
+  const int lanes = 256 / nch;                     // pixel lanes per block
+  const int ch = threadIdx.x % nch, pl = threadIdx.x / nch;
+  const int c = 8 * ((int)blockIdx.y * DWG_CPB + ch), cl = 8 * ch;   // global / slice channel
+  float a[10][8];
+#pragma unroll
+  for (int t = 0; t < 10; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[t][e] = 0.f;
+  const int64_t P = N * H * W;
+  const int64_t p0 = (int64_t)blockIdx.x * ppb, p1 = min(P, p0 + ppb);
+  if (pl < lanes) {
+    for (int64_t pix = p0 + pl; pix < p1; pix += lanes) {
+      const int xx = (int)(pix % W);
+      const int64_t t = pix / W;
+      const int yy = (int)(t % H);
+      const int64_t n = t / H;
+      float g[8];
+      ld8f(dy + pix * lddy + c, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[9][e] += g[e];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int sy = yy + tap / 3 - 1, sx = xx + tap % 3 - 1;
+        if (sy < 0 || sy >= H || sx < 0 || sx >= W) continue;
+        float v[8];
+        ld8f(x + ((n * H + sy) * W + sx) * ldx + c, v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[tap][e] = fmaf(g[e], v[e], a[tap][e]);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 10; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(&sred[(t * DWG_CPB * 8) + cl + e], a[t][e]);
   }
   __syncthreads();
-  const int oy = threadIdx.x >> 4, ox = threadIdx.x & 15;
-  const int yy = ty0 + oy, xx = tx0 + ox;
-  const bool ok = yy < H && xx < W;
-  const float g = ok ? ldf(dy + (int64_t)plane * H * W, (int64_t)(ok ? yy : 0) * W + (ok ? xx : 0)) : 0.f;
-  float part[10];
-#pragma unroll
-  for (int t = 0; t < 9; ++t) part[t] = wave_sum(g * tile[oy + t / 3][ox + t % 3]);
-  part[9] = wave_sum(g);
-  const int wid = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int t = 0; t < 10; ++t) red[wid][t] = part[t];
-  __syncthreads();
-  if (threadIdx.x < 10) {
-    const float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    if (threadIdx.x < 9) atomicAdd(&dw[c * 9 + threadIdx.x], s);
-    else if (db) atomicAdd(&db[c], s);
+  const int c0 = (int)blockIdx.y * DWG_CPB * 8, ncl = nch * 8;
+  for (int i = threadIdx.x; i < 10 * ncl; i += 256) {
+    const int t = i / ncl, j = i - t * ncl;
+    if (t < 9) atomicAdd(&dw9[t * C + c0 + j], sred[t * DWG_CPB * 8 + j]);
+    else if (db) atomicAdd(&db[c0 + j], sred[9 * DWG_CPB * 8 + j]);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// GELU gate: x [N][2h][HW] -> y [N][h][HW] = gelu(x1) * x2 (exact erf GELU, F.gelu's default)
+// GELU gate, NHWC: x [P][ldx] (x1 = channels [0, h), x2 = [h, 2h)) -> y [P][ldy] (h channels)
 // ---------------------------------------------------------------------------------------------
 template <typename T>
-__global__ __launch_bounds__(256) void gate_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t N, int h, int64_t HW) {
+__global__ __launch_bounds__(256) void gate_fwd_kernel(const T* __restrict__ x, int64_t ldx, T* __restrict__ y, int64_t ldy,
+                                                       int64_t P, int h) {
+  const int nch = h / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P * nch) return;
+  const int64_t p = gid / nch;
+  const int c = 8 * (int)(gid % nch);
+  float a[8], b[8], o[8];
+  ld8f(x + p * ldx + c, a);
+  ld8f(x + p * ldx + h + c, b);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = gelu_exact(a[e]) * b[e];
+  st8f(y + p * ldy + c, o);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void gate_bwd_kernel(const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy, int64_t lddy,
+                                                       T* __restrict__ dx, int64_t lddx, int64_t P, int h) {
+  const int nch = h / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P * nch) return;
+  const int64_t p = gid / nch;
+  const int c = 8 * (int)(gid % nch);
+  float a[8], b[8], g[8], o1[8], o2[8];
+  ld8f(x + p * ldx + c, a);
+  ld8f(x + p * ldx + h + c, b);
+  ld8f(dy + p * lddy + c, g);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { o1[e] = g[e] * b[e] * gelu_exact_grad(a[e]); o2[e] = g[e] * gelu_exact(a[e]); }
+  st8f(dx + p * lddx + c, o1);
+  st8f(dx + p * lddx + h + c, o2);
+}
+
+// column sums db[n] = sum_p dy[p][n] (8 channels per thread, pixel lanes, LDS reduction, atomics)
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, int64_t ld, float* __restrict__ db, int64_t P,
+                                                     int N, int64_t ppb) {
+  extern __shared__ float sred[];
+  for (int i = threadIdx.x; i < N; i += 256) sred[i] = 0.f;
+  __syncthreads();
+  const int nch = N / 8, lanes = 256 / nch;
+  const int ch = threadIdx.x % nch, pl = threadIdx.x / nch;
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const int64_t p0 = (int64_t)blockIdx.x * ppb, p1 = min(P, p0 + ppb);
+  if (pl < lanes) {
+    for (int64_t p = p0 + pl; p < p1; p += lanes) {
+      float v[8];
+      ld8f(dy + p * ld + 8 * ch, v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[e] += v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(&sred[8 * ch + e], a[e]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < N; i += 256) atomicAdd(&db[i], sred[i]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// reduction GEMM  C[img][n][k] = sum_{p in img} A[p][n] B[p][k]
+//   bf16: block = 64 (n) x 64 (k) output tile, 4 waves of 32 x 32 (2 x 2 MFMA 16x16x32 tiles);
+//   per stage 64 pixels of A (64 n) and B (64 k) staged in LDS (rows of 128 B + 32 B pad), both
+//   read with ds_read_b64_tr_b16. A lane group g (16 lanes) of the transposed read h covers the
+//   pixel rows 4 g + 16 h + q (q = 0..3): the 8 rows a 32-lane half reads are consecutive, which
+//   with the 160-B row pitch (40 dwords) puts them on 8 distinct 8-bank sets (conflict-free); the
+//   same pixel order is used for A and B, so the contraction is exact. Pixel splits write fp32
+//   partials [split][img][N][K]; rgemm_reduce sums them in split order.
+//   fp32 (parity builds): the same tiling on the VALU.
+// ---------------------------------------------------------------------------------------------
+constexpr int RG_BN = 64, RG_BK = 64, RG_BP = 64, RG_PITCH = 160;
+
+TURTLE_DEV uint2 ds_read_tr16(const char* lds_ptr) {
+  uint2 r;
+  const uint32_t a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const char*)lds_ptr;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return r;
+}
+
+__global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B,
+                                                         int64_t ldb, float* __restrict__ part, int64_t img_px, int nimg_out,
+                                                         int N, int K, int64_t P, int64_t ppb) {
+  typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+  __shared__ __attribute__((aligned(16))) char sA[RG_BP * RG_PITCH];
+  __shared__ __attribute__((aligned(16))) char sB[RG_BP * RG_PITCH];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int ntn = (N + RG_BN - 1) / RG_BN, ntk = (K + RG_BK - 1) / RG_BK;
+  const int tile = blockIdx.x % (ntn * ntk);
+  const int n0 = (tile / ntk) * RG_BN, k0 = (tile % ntk) * RG_BK;
+  const int split = blockIdx.x / (ntn * ntk);
+  const int img = blockIdx.y;
+  const int64_t pbase = img_px > 0 ? (int64_t)img * img_px : 0;
+  const int64_t plen = img_px > 0 ? img_px : P;
+  const int64_t p0 = (int64_t)split * ppb, p1 = min(plen, p0 + ppb);
+  const int wn = wid >> 1, wk = wid & 1;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // staging: thread -> pixel row tid >> 2, 16-B chunks 2 (tid & 3) and + 1 of each operand
+  const int srow = tid >> 2, sch = 2 * (tid & 3);
+  // transposed reads: lane group g = lane >> 4, row q = (lane >> 2) & 3, column quad pq = lane & 3
+  const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+  for (int64_t pb = p0; pb < p1; pb += RG_BP) {
+    const int64_t p = pb + srow;
+    const bool live = p < p1;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int cA = n0 + 8 * (sch + u), cB = k0 + 8 * (sch + u);
+      uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+      if (live && cA < N) va = *reinterpret_cast<const uint4*>(A + (pbase + p) * lda + cA);
+      if (live && cB < K) vb = *reinterpret_cast<const uint4*>(B + (pbase + p) * ldb + cB);
+      *reinterpret_cast<uint4*>(sA + srow * RG_PITCH + 16 * (sch + u)) = va;
+      *reinterpret_cast<uint4*>(sB + srow * RG_PITCH + 16 * (sch + u)) = vb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {               // 32 pixels per MFMA K step
+      bf16x8v af[2], bfr[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int cn = 32 * wn + 16 * t + 4 * pq, ck = 32 * wk + 16 * t + 4 * pq;
+        const int r0 = 32 * ks + 4 * g + q;
+        const uint2 a0 = ds_read_tr16(sA + r0 * RG_PITCH + 2 * cn), a1 = ds_read_tr16(sA + (r0 + 16) * RG_PITCH + 2 * cn);
+        const uint2 b0 = ds_read_tr16(sB + r0 * RG_PITCH + 2 * ck), b1 = ds_read_tr16(sB + (r0 + 16) * RG_PITCH + 2 * ck);
+        af[t] = __builtin_bit_cast(bf16x8v, make_uint4(a0.x, a0.y, a1.x, a1.y));
+        bfr[t] = __builtin_bit_cast(bf16x8v, make_uint4(b0.x, b0.y, b1.x, b1.y));
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // lane holds C[n0 + 32 wn + 16 i + 4 g + e][k0 + 32 wk + 16 j + (lane & 15)]
+  float* out = part + ((int64_t)split * nimg_out + img) * N * K;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = n0 + 32 * wn + 16 * i + 4 * g + e, k = k0 + 32 * wk + 16 * j + (lane & 15);
+        if (n < N && k < K) out[(int64_t)n * K + k] = acc[i][j][e];
+      }
+}
+
+__global__ __launch_bounds__(256) void rgemm_f32_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+                                                        int64_t ldb, float* __restrict__ part, int64_t img_px, int nimg_out,
+                                                        int N, int K, int64_t P, int64_t ppb) {
+  __shared__ float sA[32][65], sB[32][65];
+  const int tid = threadIdx.x;
+  const int ntn = (N + 63) / 64, ntk = (K + 63) / 64;
+  const int tile = blockIdx.x % (ntn * ntk);
+  const int n0 = (tile / ntk) * 64, k0 = (tile % ntk) * 64;
+  const int split = blockIdx.x / (ntn * ntk);
+  const int img = blockIdx.y;
+  const int64_t pbase = img_px > 0 ? (int64_t)img * img_px : 0;
+  const int64_t plen = img_px > 0 ? img_px : P;
+  const int64_t p0 = (int64_t)split * ppb, p1 = min(plen, p0 + ppb);
+  const int tn = tid >> 4, tk = tid & 15;          // 4 x 4 outputs per thread
+  float acc[4][4] = {};
+  for (int64_t pb = p0; pb < p1; pb += 32) {
+    for (int i = tid; i < 32 * 64; i += 256) {
+      const int r = i / 64, cc = i % 64;
+      const int64_t p = pb + r;
+      sA[r][cc] = (p < p1 && n0 + cc < N) ? A[(pbase + p) * lda + n0 + cc] : 0.f;
+      sB[r][cc] = (p < p1 && k0 + cc < K) ? B[(pbase + p) * ldb + k0 + cc] : 0.f;
+    }
+    __syncthreads();
+    for (int r = 0; r < 32; ++r)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(sA[r][4 * tn + i], sB[r][4 * tk + j], acc[i][j]);
+    __syncthreads();
+  }
+  float* out = part + ((int64_t)split * nimg_out + img) * N * K;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + 4 * tn + i, k = k0 + 4 * tk + j;
+      if (n < N && k < K) out[(int64_t)n * K + k] = acc[i][j];
+    }
+}
+
+__global__ __launch_bounds__(256) void rgemm_reduce_kernel(const float* __restrict__ part, float* __restrict__ c, int64_t n,
+                                                           int nsplit, int accumulate) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t tot = N * h * HW;
-  if (i >= tot) return;
-  const int64_t n = i / (h * HW), r = i - n * h * HW;
-  const T* xb = x + n * 2 * h * HW;
-  stf(y, i, gelu_exact(ldf(xb, r)) * ldf(xb, (int64_t)h * HW + r));
-}
-template <typename T>
-__global__ __launch_bounds__(256) void gate_bwd_kernel(const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,
-                                                       int64_t N, int h, int64_t HW) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t tot = N * h * HW;
-  if (i >= tot) return;
-  const int64_t n = i / (h * HW), r = i - n * h * HW;
-  const T* xb = x + n * 2 * h * HW;
-  T* db = dx + n * 2 * h * HW;
-  const float a = ldf(xb, r), bb = ldf(xb, (int64_t)h * HW + r), g = ldf(dy, i);
-  stf(db, r, g * bb * gelu_exact_grad(a));
-  stf(db, (int64_t)h * HW + r, g * gelu_exact(a));
+  if (i >= n) return;
+  float s = accumulate ? c[i] : 0.f;
+  for (int k = 0; k < nsplit; ++k) s += part[(int64_t)k * n + i];
+  c[i] = s;
 }
 
 // ---------------------------------------------------------------------------------------------
+// host launchers
+// ---------------------------------------------------------------------------------------------
 template <typename T>
-void ln_fwd(const void* x, const float* w, const float* b, void* y, float* mu, float* rstd, int64_t N, int C, int64_t HW,
-            int biasfree, hipStream_t st) {
-  const int64_t P = N * HW;
-  hipLaunchKernelGGL(ln_fwd_kernel<T>, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st, (const T*)x, w, b, (T*)y, mu, rstd,
-                     N, C, HW, biasfree);
+int ln_fwd(const void* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy, float* mu, float* rstd, int64_t P,
+           int C, int biasfree, hipStream_t st) {
+  const int G = ln_group(C), nch = (C / 8 + G - 1) / G;
+  const int64_t blocks = (P * G + 255) / 256;
+#define LNF(GG, NN)                                                                                                  \
+  if (G == GG && nch <= NN) {                                                                                        \
+    hipLaunchKernelGGL((ln_fwd_kernel<T, GG, NN>), dim3((unsigned)blocks), dim3(256), 0, st, (const T*)x, ldx, w, b, \
+                       (T*)y, ldy, mu, rstd, P, C, biasfree);                                                        \
+    return 0;                                                                                                        \
+  }
+  LNF(1, 1) LNF(2, 1) LNF(4, 1) LNF(8, 1) LNF(16, 1) LNF(32, 1) LNF(64, 1) LNF(64, 2) LNF(64, 4)
+#undef LNF
+  return -1;
 }
 template <typename T>
-void ln_bwd(const void* x, const float* w, const float* mu, const float* rstd, const void* dy, void* dx, float* dw, float* db,
-            int64_t N, int C, int64_t HW, int biasfree, hipStream_t st) {
-  const int64_t P = N * HW;
-  hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3((unsigned)((P + 255) / 256)), dim3(256), 2 * C * sizeof(float), st, (const T*)x, w,
-                     mu, rstd, (const T*)dy, (T*)dx, dw, db, N, C, HW, biasfree);
+int ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy, int64_t lddy, void* dx,
+           int64_t lddx, float* dw, float* db, int64_t P, int C, int biasfree, hipStream_t st) {
+  const int G = ln_group(C), nch = (C / 8 + G - 1) / G;
+  const int64_t ppb = 256;                          // pixels per block
+  const int64_t blocks = (P + ppb - 1) / ppb;
+#define LNB(GG, NN)                                                                                                       \
+  if (G == GG && nch <= NN) {                                                                                             \
+    hipLaunchKernelGGL((ln_bwd_kernel<T, GG, NN>), dim3((unsigned)blocks), dim3(256), 2 * C * sizeof(float), st, (const T*)x, \
+                       ldx, w, mu, rstd, (const T*)dy, lddy, (T*)dx, lddx, dw, db, P, C, biasfree, (int)ppb);                \
+    return 0;                                                                                                             \
+  }
+  LNB(1, 1) LNB(2, 1) LNB(4, 1) LNB(8, 1) LNB(16, 1) LNB(32, 1) LNB(64, 1) LNB(64, 2) LNB(64, 4)
+#undef LNB
+  return -1;
 }
 template <typename T>
-void dw_fwd(const void* x, const float* w, const float* b, void* y, int64_t N, int C, int H, int W, int flip, hipStream_t st) {
-  const int tiles = ((H + 15) / 16) * ((W + 15) / 16);
-  hipLaunchKernelGGL(dw_fwd_kernel<T>, dim3(tiles, (unsigned)(N * C)), dim3(256), 0, st, (const T*)x, w, b, (T*)y, C, H, W, flip);
+int dw_fwd(const void* x, int64_t ldx, const float* w9, const float* b, void* y, int64_t ldy, int64_t N, int C, int H, int W,
+           int flip, hipStream_t st) {
+  const int64_t tot = N * H * W * (C / 8);
+  hipLaunchKernelGGL(dw_fwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, ldx, w9, b, (T*)y,
+                     ldy, N, C, H, W, flip);
+  return 0;
 }
 template <typename T>
-void dw_wgrad(const void* x, const void* dy, float* dw, float* db, int64_t N, int C, int H, int W, hipStream_t st) {
-  const int tiles = ((H + 15) / 16) * ((W + 15) / 16);
-  hipLaunchKernelGGL(dw_wgrad_kernel<T>, dim3(tiles, (unsigned)(N * C)), dim3(256), 0, st, (const T*)x, (const T*)dy, dw, db, C, H, W);
+int dw_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* dw9, float* db, int64_t N, int C, int H, int W,
+             hipStream_t st) {
+  const int64_t P = N * H * W;
+  const int nsl = (C / 8 + DWG_CPB - 1) / DWG_CPB;
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 1024 / nsl), std::max<int64_t>(1, P / 64));
+  const int64_t ppb = (P + blocks - 1) / blocks;
+  hipLaunchKernelGGL(dw_wgrad_kernel<T>, dim3((unsigned)blocks, (unsigned)nsl), dim3(256), 0, st, (const T*)x, ldx,
+                     (const T*)dy, lddy, dw9, db, N, C, H, W, ppb);
+  return 0;
 }
 template <typename T>
-void gate_fwd(const void* x, void* y, int64_t N, int h, int64_t HW, hipStream_t st) {
-  const int64_t tot = N * h * HW;
-  hipLaunchKernelGGL(gate_fwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, (T*)y, N, h, HW);
+int gate_fwd(const void* x, int64_t ldx, void* y, int64_t ldy, int64_t P, int h, hipStream_t st) {
+  const int64_t tot = P * (h / 8);
+  hipLaunchKernelGGL(gate_fwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, ldx, (T*)y, ldy, P, h);
+  return 0;
 }
 template <typename T>
-void gate_bwd(const void* x, const void* dy, void* dx, int64_t N, int h, int64_t HW, hipStream_t st) {
-  const int64_t tot = N * h * HW;
-  hipLaunchKernelGGL(gate_bwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, (const T*)dy, (T*)dx,
-                     N, h, HW);
+int gate_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx, int64_t P, int h, hipStream_t st) {
+  const int64_t tot = P * (h / 8);
+  hipLaunchKernelGGL(gate_bwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, ldx, (const T*)dy,
+                     lddy, (T*)dx, lddx, P, h);
+  return 0;
+}
+template <typename T>
+int colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, hipStream_t st) {
+  const int64_t blocks = std::min<int64_t>(1024, std::max<int64_t>(1, P / 256));
+  const int64_t ppb = (P + blocks - 1) / blocks;
+  hipLaunchKernelGGL(colsum_kernel<T>, dim3((unsigned)blocks), dim3(256), N * sizeof(float), st, (const T*)dy, ld, db, P, N, ppb);
+  return 0;
+}
+
+// device constants of the GEMM family (zero / one vectors for branch-free operands), per device
+static const float* train_consts(int which) {
+  static std::mutex mu;
+  static std::map<int, float*> mem;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = mem.find(dev);
+  if (it == mem.end()) {
+    float* p = nullptr;
+    if (hipMalloc(&p, (16384 + 8192) * sizeof(float)) != hipSuccess) return nullptr;
+    std::vector<float> h(16384 + 8192, 0.f);
+    for (int i = 16384; i < 16384 + 8192; ++i) h[i] = 1.f;
+    if (hipMemcpy(p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    it = mem.emplace(dev, p).first;
+  }
+  return which ? it->second + 16384 : it->second;
+}
+
+static int64_t rgemm_splits(int64_t P, int N, int K, int64_t img_px) {
+  const int64_t plen = img_px > 0 ? img_px : P;
+  const int64_t nimg = img_px > 0 ? P / img_px : 1;
+  const int64_t tiles = ((N + RG_BN - 1) / RG_BN) * ((K + RG_BK - 1) / RG_BK) * nimg;
+  return std::max<int64_t>(1, std::min<int64_t>((1024 + tiles - 1) / tiles, (plen + 511) / 512));
 }
 
 }  // namespace turtle
 
 // ---------------------------------------------------------------------------------------------
-// C ABI (include/turtle_train.h): dtype 0 = fp32, 1 = bf16 activations; returns 0 or a HIP error
+// C ABI (include/turtle_train.h): dtype 0 = fp32, 1 = bf16, 2 = fp16 activations; returns 0, a
+// negative argument error or a positive hipError_t
 // ---------------------------------------------------------------------------------------------
 using namespace turtle;
 #define TT_DISPATCH(dt, fn, ...)                                   \
   do {                                                             \
-    if ((dt) == 1) fn<bf16>(__VA_ARGS__); else fn<float>(__VA_ARGS__); \
+    int rc_;                                                       \
+    if ((dt) == 1) rc_ = fn<bf16>(__VA_ARGS__);                    \
+    else if ((dt) == 2) rc_ = fn<f16>(__VA_ARGS__);                \
+    else if ((dt) == 0) rc_ = fn<float>(__VA_ARGS__);              \
+    else return -1;                                                \
+    if (rc_) return rc_;                                           \
     return (int)hipGetLastError();                                 \
   } while (0)
 
+static bool rows_ok(const void* p, int64_t ld, int dtype) {
+  const int es = dtype == 0 ? 4 : 2;
+  return p && ld > 0 && (reinterpret_cast<uintptr_t>(p) % 16) == 0 && (ld * es) % 16 == 0;
+}
+
 extern "C" {
 
-int turtle_train_ln_fwd(const void* x, const float* w, const float* b, void* y, float* mu, float* rstd, int64_t N, int C,
-                        int64_t HW, int biasfree, int dtype, void* stream) {
-  if (!x || !w || !y || !mu || !rstd || N <= 0 || C <= 0 || HW <= 0 || (!biasfree && !b)) return -1;
-  TT_DISPATCH(dtype, ln_fwd, x, w, b, y, mu, rstd, N, C, HW, biasfree, (hipStream_t)stream);
+int turtle_train_ln_fwd(const void* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy, float* mu, float* rstd,
+                        int64_t P, int C, int biasfree, int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !w || !mu || !rstd || P <= 0 || C <= 0 || C % 8 || C > 2048 ||
+      ldx < C || ldy < C || (!biasfree && !b))
+    return -1;
+  TT_DISPATCH(dtype, ln_fwd, x, ldx, w, b, y, ldy, mu, rstd, P, C, biasfree, (hipStream_t)stream);
 }
 
-int turtle_train_ln_bwd(const void* x, const float* w, const float* mu, const float* rstd, const void* dy, void* dx,
-                        float* dw, float* db, int64_t N, int C, int64_t HW, int biasfree, int dtype, void* stream) {
-  if (!x || !w || !mu || !rstd || !dy || !dx || !dw || N <= 0 || C <= 0 || HW <= 0) return -1;
-  TT_DISPATCH(dtype, ln_bwd, x, w, mu, rstd, dy, dx, dw, biasfree ? nullptr : db, N, C, HW, biasfree, (hipStream_t)stream);
+int turtle_train_ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy,
+                        int64_t lddy, void* dx, int64_t lddx, float* dw, float* db, int64_t P, int C, int biasfree, int dtype,
+                        void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(dy, lddy, dtype) || !rows_ok(dx, lddx, dtype) || !w || !mu || !rstd || !dw ||
+      P <= 0 || C <= 0 || C % 8 || C > 2048)
+    return -1;
+  TT_DISPATCH(dtype, ln_bwd, x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dw, biasfree ? nullptr : db, P, C, biasfree,
+              (hipStream_t)stream);
 }
 
-int turtle_train_dw3x3_fwd(const void* x, const float* w, const float* b, void* y, int64_t N, int C, int H, int W, int flip,
-                           int dtype, void* stream) {
-  if (!x || !w || !y || N <= 0 || C <= 0 || H <= 0 || W <= 0 || N * C > 65535) return -1;
-  TT_DISPATCH(dtype, dw_fwd, x, w, b, y, N, C, H, W, flip, (hipStream_t)stream);
+int turtle_train_dw3x3_fwd(const void* x, int64_t ldx, const float* w9, const float* b, void* y, int64_t ldy, int64_t N, int C,
+                           int H, int W, int flip, int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !w9 || N <= 0 || C <= 0 || C % 8 || H <= 0 || W <= 0)
+    return -1;
+  TT_DISPATCH(dtype, dw_fwd, x, ldx, w9, b, y, ldy, N, C, H, W, flip, (hipStream_t)stream);
 }
 
-int turtle_train_dw3x3_wgrad(const void* x, const void* dy, float* dw, float* db, int64_t N, int C, int H, int W, int dtype,
-                             void* stream) {
-  if (!x || !dy || !dw || N <= 0 || C <= 0 || H <= 0 || W <= 0 || N * C > 65535) return -1;
-  TT_DISPATCH(dtype, dw_wgrad, x, dy, dw, db, N, C, H, W, (hipStream_t)stream);
+int turtle_train_dw3x3_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* dw9, float* db, int64_t N, int C,
+                             int H, int W, int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(dy, lddy, dtype) || !dw9 || N <= 0 || C <= 0 || C % 8 || H <= 0 || W <= 0)
+    return -1;
+  TT_DISPATCH(dtype, dw_wgrad, x, ldx, dy, lddy, dw9, db, N, C, H, W, (hipStream_t)stream);
 }
 
-int turtle_train_gate_fwd(const void* x, void* y, int64_t N, int h, int64_t HW, int dtype, void* stream) {
-  if (!x || !y || N <= 0 || h <= 0 || HW <= 0) return -1;
-  TT_DISPATCH(dtype, gate_fwd, x, y, N, h, HW, (hipStream_t)stream);
+int turtle_train_gate_fwd(const void* x, int64_t ldx, void* y, int64_t ldy, int64_t P, int h, int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || P <= 0 || h <= 0 || h % 8) return -1;
+  TT_DISPATCH(dtype, gate_fwd, x, ldx, y, ldy, P, h, (hipStream_t)stream);
 }
 
-int turtle_train_gate_bwd(const void* x, const void* dy, void* dx, int64_t N, int h, int64_t HW, int dtype, void* stream) {
-  if (!x || !dy || !dx || N <= 0 || h <= 0 || HW <= 0) return -1;
-  TT_DISPATCH(dtype, gate_bwd, x, dy, dx, N, h, HW, (hipStream_t)stream);
+int turtle_train_gate_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx, int64_t P, int h,
+                          int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(dy, lddy, dtype) || !rows_ok(dx, lddx, dtype) || P <= 0 || h <= 0 || h % 8) return -1;
+  TT_DISPATCH(dtype, gate_bwd, x, ldx, dy, lddy, dx, lddx, P, h, (hipStream_t)stream);
+}
+
+int turtle_train_colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, int dtype, void* stream) {
+  if (!rows_ok(dy, ld, dtype) || !db || P <= 0 || N <= 0 || N % 8 || N > 2048) return -1;
+  TT_DISPATCH(dtype, colsum, dy, ld, db, P, N, (hipStream_t)stream);
+}
+
+int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride, int64_t img_px, const float* bias, void* y,
+                      int64_t ldy, int64_t P, int K, int N, int dtype, void* stream) {
+  if (dtype != 0 && dtype != 1) return -1;
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !w || P <= 0 || K <= 0 || N <= 0 || K % 8 || N % 8 || ldx < K ||
+      ldy < N || (wstride && (img_px <= 0 || P % img_px)) || (img_px > 0 && img_px >= ((int64_t)1 << 31)))
+    return -1;
+  GemmArgs g{};
+  g.a.n = 1; g.a.Ktot = K;
+  g.a.s[0] = SrcDesc{x, ldx, 0, K, 1, 0};
+  g.M = P; g.N = N;
+  g.HW = (int)(img_px > 0 ? img_px : std::min<int64_t>(P, (int64_t)1 << 30)); g.Wimg = g.HW;
+  g.w = w; g.ldw = K; g.wstride = wstride; g.wdiv = 1;
+  g.bias = bias; g.out = y; g.ldo = ldy; g.offo = 0; g.store_mode = STORE_NHWC;
+  g.zeros = train_consts(0); g.ones = train_consts(1);
+  if (!g.zeros) return (int)hipErrorOutOfMemory;
+  g.allow_panel = g.allow_lds = g.allow_pn = g.allow_ar = g.allow_kt = 1;
+  try {
+    if (dtype == 1) launch_gemm<bf16>(g, (hipStream_t)stream);
+    else launch_gemm<float>(g, (hipStream_t)stream);
+  } catch (...) {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+size_t turtle_train_rgemm_workspace(int64_t P, int N, int K, int64_t img_px) {
+  const int64_t nimg = img_px > 0 ? P / img_px : 1;
+  return (size_t)rgemm_splits(P, N, K, img_px) * nimg * N * K * sizeof(float);
+}
+
+int turtle_train_rgemm(const void* a, int64_t lda, const void* b, int64_t ldb, float* c, int64_t P, int N, int K, int64_t img_px,
+                       int accumulate, int dtype, void* ws, size_t ws_bytes, void* stream) {
+  if (dtype != 0 && dtype != 1) return -1;
+  if (!rows_ok(a, lda, dtype) || !rows_ok(b, ldb, dtype) || !c || P <= 0 || N <= 0 || K <= 0 || N % 8 || K % 8 || lda < N ||
+      ldb < K || (img_px > 0 && P % img_px))
+    return -1;
+  const int64_t plen = img_px > 0 ? img_px : P;
+  const int64_t nimg = img_px > 0 ? P / img_px : 1;
+  int64_t nsplit = rgemm_splits(P, N, K, img_px);
+  if (!ws || ws_bytes < (size_t)nsplit * nimg * N * K * sizeof(float) || nimg > 65535) return -1;
+  int64_t ppb = (plen + nsplit - 1) / nsplit;
+  ppb = (ppb + RG_BP - 1) / RG_BP * RG_BP;
+  nsplit = (plen + ppb - 1) / ppb;
+  const dim3 grid((unsigned)(((N + RG_BN - 1) / RG_BN) * ((K + RG_BK - 1) / RG_BK) * nsplit), (unsigned)nimg);
+  hipStream_t st = (hipStream_t)stream;
+  float* part = reinterpret_cast<float*>(ws);
+  if (dtype == 1)
+    hipLaunchKernelGGL(rgemm_bf16_kernel, grid, dim3(256), 0, st, (const bf16*)a, lda, (const bf16*)b, ldb, part, img_px,
+                       (int)nimg, N, K, P, ppb);
+  else
+    hipLaunchKernelGGL(rgemm_f32_kernel, grid, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, part, img_px,
+                       (int)nimg, N, K, P, ppb);
+  const int64_t n = nimg * N * K;
+  hipLaunchKernelGGL(rgemm_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, c, n, (int)nsplit, accumulate);
+  return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -28,6 +28,9 @@ struct TurtleError : std::runtime_error {
   TurtleError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 #define TFAIL(code, msg) throw TurtleError(code, msg)
+namespace turtle {
+[[noreturn]] void kernel_arg_error(const char* what) { TFAIL(TURTLE_EINVAL, what); }
+}
 #define HIPCHK(x)                                                                          \
   do {                                                                                     \
     hipError_t e_ = (x);                                                                   \
@@ -220,6 +223,7 @@ struct ModelW {
   size_t end_wf = NONE;                      // ending 3x3 as bf16 MFMA A fragments [9 Cin / 32][64 lanes][8] (spatial.hip)
   size_t zeros = NONE, ones = NONE;          // constant vectors for branch-free kernel operands
   GemmW down[3], up[3], reduce[3];
+  bool reduce_split = false;                 // reduce[2] packed as split-bf16 [W_hi | W_lo] (K doubled)
   std::vector<std::vector<BlockW>> blocks;   // [level][block]
 };
 
@@ -244,6 +248,11 @@ struct Packer {
     float f = (float)x;
     uint32_t u; std::memcpy(&u, &f, 4);
     return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  }
+  static double bf16_value(double x) {
+    const uint32_t u = (uint32_t)bf16_bits(x) << 16;
+    float f; std::memcpy(&f, &u, 4);
+    return f;
   }
   // depthwise 3x3 table [9][C] -> bf16 tap pairs [5][C]: lo = tap 2i, hi = tap 2i+1 (0 for tap 9),
   // the operand layout of v_dot2_f32_bf16 in the fused kernel's depthwise stage
@@ -322,6 +331,9 @@ struct TurtleHandle {
   int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
+  bool pdw = true;                                    // level-3 GatedFeedForward: LN -> project_in -> dw -> gate in one kernel (pdw.hip)
+  int pdw_split = 1;                                  // pdw schedule variant (pdw.hip)
+  bool split_out = true;                              // split-bf16 weights for reduce_chan_level1 (bf16 builds)
   bool dwgemm_attn = true;                            // channel attention: v's depthwise inside the W_eff GEMM (dwgemm.hip)
   int dwgemm_min_blocks = 384;                        // one 160 KB block per CU: below ~1.5 rounds (latent level) dw + GEMM is faster
   bool blaslt = getenv("TURTLE_NO_BLASLT") == nullptr; // hipBLASLt for the plain projections it wins (blas.cpp)
@@ -480,14 +492,19 @@ static void pack_all(TurtleHandle* h) {
     // A fragment s, lane l: output channel l & 15 (< Cimg, else 0), k = 32 s + 8 (l >> 4) + j -> (tap, ci)
     const auto& ew = W(h, "ending.weight");
     const int cin = d, cimg = (int)(ew.size() / ((size_t)cin * 9));
-    if (cin % 32 == 0 && cimg <= 16) {
+    // split-bf16 weights: A rows 0..3 hold bf16(w), rows 4..7 the bf16 rounding of the remainder
+    // w - bf16(w), summed in the kernel epilogue (~16-bit weight mantissa at no MFMA cost: the ending
+    // is the layer whose weight rounding moves the output PSNR most, tools/psnr_probe.py --by-module)
+    if (cin % 32 == 0 && cimg <= 4) {
       const int ks = 9 * cin / 32;
       std::vector<double> f((size_t)ks * 64 * 8, 0.0);
       for (int s = 0; s < ks; ++s)
         for (int l = 0; l < 64; ++l)
           for (int j = 0; j < 8; ++j) {
-            const int k = s * 32 + (l >> 4) * 8 + j, tap = k / cin, ci = k - tap * cin, co = l & 15;
-            if (co < cimg) f[((size_t)s * 64 + l) * 8 + j] = ew[((size_t)co * cin + ci) * 9 + tap];
+            const int k = s * 32 + (l >> 4) * 8 + j, tap = k / cin, ci = k - tap * cin, row = l & 15, co = row & 3;
+            if (co >= cimg || row >= (h->split_out ? 8 : 4)) continue;
+            const double w = ew[((size_t)co * cin + ci) * 9 + tap];
+            f[((size_t)s * 64 + l) * 8 + j] = row < 4 ? w : w - Packer::bf16_value(w);
           }
       M.end_wf = pk.bf16tab(f);
     }
@@ -502,8 +519,21 @@ static void pack_all(TurtleHandle* h) {
     const int cu = d << (3 - i);          // up i: level (3-i) channels -> 2c, shuffled to c/2
     M.up[i] = pack_conv3(h, pk, ups[i], cu, 2 * cu, true);
     const int cr = cu;                    // reduce: cat(up c/2, skip c/2) = cu -> cu/2
-    M.reduce[i] = pack_gemm(h, pk, dvec(W(h, std::string(reds[i]) + ".weight")), cr / 2, cr, "",
-                            opt_bias(h, std::string(reds[i]) + ".bias"));
+    std::vector<double> rw = dvec(W(h, std::string(reds[i]) + ".weight"));
+    if (i == 2 && pk.bf16 && h->split_out) {
+      // reduce_chan_level1 (the last 1x1 before the full-resolution decoder, second in output-PSNR
+      // sensitivity to weight rounding): split-bf16 weights [W_hi | W_lo], K doubled over the
+      // sources [up, skip, up, skip] (turtle.cpp upcat)
+      std::vector<double> w2;
+      for (int n = 0; n < cr / 2; ++n) {
+        for (int k = 0; k < cr; ++k) w2.push_back(Packer::bf16_value(rw[(size_t)n * cr + k]));
+        for (int k = 0; k < cr; ++k) w2.push_back(rw[(size_t)n * cr + k] - Packer::bf16_value(rw[(size_t)n * cr + k]));
+      }
+      M.reduce[i] = pack_gemm(h, pk, w2, cr / 2, 2 * cr, "", opt_bias(h, std::string(reds[i]) + ".bias"));
+      M.reduce_split = true;
+    } else {
+      M.reduce[i] = pack_gemm(h, pk, rw, cr / 2, cr, "", opt_bias(h, std::string(reds[i]) + ".bias"));
+    }
   }
   M.blocks.clear();
   for (auto& L : A.levels) {
@@ -873,6 +903,23 @@ struct Runner {
     a.nimg = nimg; a.H = H; a.W = Wd; a.N = c;
     return dwgemm_blocks(a) >= h->dwgemm_min_blocks;
   }
+  // shape-only (same in the sizing dry run): the level-3 GatedFeedForward as pdw + GEMM
+  bool can_pdw(int c, int hd) const {
+    return ES == 2 && h->pdw && c == 256 && hd % 16 == 0 && hd <= 2048;
+  }
+  void pdw(const GemmW& w1, const DwW& dwp, const T* x, int c, int nimg, int H, int Wd, T* out, int hd) {
+    if (dry()) return;
+    PdwArgs a{};
+    a.x = x; a.ldx = c; a.offx = 0; a.C = c; a.nimg = nimg; a.H = H; a.W = Wd;
+    a.w1 = h->ptr(w1.w); a.N1 = w1.N; a.ln = w1.ln; a.ln_s = h->fptr(w1.s); a.ln_tb = h->fptr(w1.tb);
+    a.dww16 = h->ptr(dwp.w16); a.dwb = h->fptr(dwp.bias); a.out = out; a.ldo = hd; a.offo = 0;
+    a.pad_off = (int64_t)nimg * H * Wd * hd * ES; a.split = h->pdw_split;
+    if (w1.N != 2 * hd || dwp.C != w1.N || !w1.ln || !pdw_ok(a)) TFAIL(TURTLE_EINVAL, "pdw: GatedFeedForward shape not supported");
+    const double px = (double)nimg * H * Wd;
+    tag("pdw nimg=%d H=%d W=%d C=%d N1=%d", nimg, H, Wd, c, w1.N);
+    launch(TURTLE_K_FUSED, ES * px * (c + hd) + ES * (double)w1.N * c, 2.0 * px * c * w1.N + 18.0 * px * w1.N,
+           [&] { launch_pdw(a, st); });
+  }
   // shape-only: the GatedFeedForward hidden map channel-blocked between the pn GEMM and dwgemm
   bool can_dwgemm_cb(int c, int hd, int nimg, int H, int Wd) const {
     if (ES != 2 || !h->dwgemm || !h->dwgemm_cb || !h->gemm_pn || hd % 32 || hd > 2048) return false;
@@ -1028,6 +1075,12 @@ struct Runner {
       } else if (can_pwdw(c, 2 * hd, true)) {
         T* t2 = buf(P * hd);
         pwdw(bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, 1, t2, hd, 0);
+        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
+      } else if (can_pdw(c, hd)) {
+        // project_in -> depthwise -> gate in one kernel (the 2 hd-channel hidden map stays on chip),
+        // then project_out + residual as a GEMM over the gated map
+        T* t2 = buf(P * hd + 256);                 // + the kernel's 512-byte store pad
+        pdw(bw.f_in, bw.f_dw, x, c, B, H, Wd, t2, hd);
         gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
       } else if (can_dwgemm_cb(c, hd, B, H, Wd)) {
         // project_in stores the hidden map channel-blocked ([2 hd / 16][P][16]): each dwgemm K step
@@ -1381,6 +1434,9 @@ struct Runner {
       SrcList s{}; s.n = 2; s.Ktot = c;
       s.s[0] = SrcDesc{up, c / 2, 0, c / 2, 1, 0};
       s.s[1] = SrcDesc{skip, c / 2, 0, c / 2, 1, 0};
+      if (i == 2 && h->mw.reduce_split) {          // split-bf16 weights: the same two sources twice
+        s.n = 4; s.Ktot = 2 * c; s.s[2] = s.s[0]; s.s[3] = s.s[1];
+      }
       const int H1 = 2 * H0, W1 = 2 * W0;
       gemm(h->mw.reduce[i], s, (int64_t)B * H1 * W1, H1 * W1, W1, y, c / 2, 0);
     };
@@ -1403,8 +1459,8 @@ struct Runner {
       tag("ending %dx%d", Hout, Wout);
       launch(TURTLE_K_OTHER, ES * (double)P1 * d + 8.0 * B * A.out_ch * Hout * Wout, 18.0 * P1 * d * A.out_ch,
              [&] {
-               if (h->stem_mfma && ES == 2 && stem_end_mfma_ok(d, A.in_ch, d)) launch_ending_mfma(e, st);
-               else launch_ending<T>(e, st);
+               if (!(h->stem_mfma && ES == 2 && stem_end_mfma_ok(d, A.in_ch, d) && e.wfrag && launch_ending_mfma(e, st)))
+                 launch_ending<T>(e, st);
              });
     }
   }
@@ -1502,6 +1558,12 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "dwgemm") h->dwgemm = value != 0;
     else if (n == "dwgemm_attn") h->dwgemm_attn = value != 0;
     else if (n == "dwgemm_cb") h->dwgemm_cb = value != 0;
+    else if (n == "pdw") h->pdw = value != 0;
+    else if (n == "pdw_split") h->pdw_split = value;
+    else if (n == "split_out") {                 // changes the packed weights: re-pack when loaded
+      h->split_out = value != 0;
+      if (h->loaded) pack_all(h);
+    }
     else if (n == "ffn") h->ffn = value != 0;
     else if (n == "sab_db") h->sab_db = value != 0;
     else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;

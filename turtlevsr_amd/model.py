@@ -10,8 +10,18 @@ Interface of the reference plug-in (basicsr/models/archs/turtle_t1_arch.py):
   The returned caches are ordinary torch tensors with the reference's shapes; entries are None
   where the reference returns None.
 
-Every forward runs on the HIP library; there is no PyTorch / CPU fallback: a module on a
-non-ROCm device or a missing library raises ``RuntimeError``.
+Two execution modes, one parameter tree:
+
+* inference (``eval()`` mode, or autograd off, or no parameter requiring grad): the forward runs
+  on the HIP library; there is no PyTorch / CPU fallback: a module on a non-ROCm device or a
+  missing library raises ``RuntimeError``;
+* training (``train()`` mode - nn.Module's default, set by VideoRestorationModel.__init__ :42 -
+  with autograd recording and a parameter requiring grad): the forward is the differentiable graph
+  of ``train.TrainGraph`` over the same parameters (HIP kernels forward and backward, caches not
+  detached), so the reference's ``optimize_parameters`` loop (video_restoration_model.py:78-107:
+  fp16 autocast, BPTT over the clip, ``0 * sum(p)``, GradScaler, AdamW) trains this module.
+  Validation (``eval()`` + ``no_grad``, :110-113) and inference.py (``eval()``, :253) take the HIP
+  inference path.
 
 Compute dtype: ``fp32`` (default, reference parity) or ``bf16`` (MFMA bf16, fp32 accumulation),
 chosen by ``opt['hip_dtype']`` or ``set_compute_dtype``. Cache tensors are returned in the
@@ -29,6 +39,7 @@ import torch.nn as nn
 from . import _lib
 from .arch import resolve
 from .params import TurtleParams
+from .train import TrainGraph
 
 _DT = {"fp32": (_lib.DTYPE_F32, torch.float32), "bf16": (_lib.DTYPE_BF16, torch.bfloat16)}
 
@@ -48,7 +59,7 @@ class _Handle:
             pass
 
 
-class TurtleHIP(TurtleParams):
+class TurtleHIP(TrainGraph, TurtleParams):
     """Turtle_t1 (``sr=False``) / TurtleSuper_t1 (``sr=True``) / t0 Turtle (``t0=True``) on MI355X."""
 
     def __init__(self, opt: dict, sr: bool = False, dtype: str = "fp32", t0: Optional[bool] = None):
@@ -132,9 +143,17 @@ class TurtleHIP(TurtleParams):
             self._ws = (key, torch.empty(int(n.value), dtype=torch.uint8, device=dev))
         return self._ws[1]
 
+    def _differentiable(self) -> bool:
+        """Training mode with autograd recording and some parameter requiring grad."""
+        return self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+
     def forward(self, inp_img_: torch.Tensor, k_cached: Optional[list] = None, v_cached: Optional[list] = None):
         if inp_img_.dim() != 5 or inp_img_.shape[1] != 2:
             raise ValueError("expected inp_img_ of shape [B, 2, C, H, W]")
+        if self._differentiable():
+            if inp_img_.device.type != "cuda" and self.graph_ops is None:
+                raise RuntimeError("TurtleHIP trains on a ROCm device only (the HIP training kernels have no CPU path)")
+            return self.graph_forward(inp_img_, k_cached, v_cached)
         if inp_img_.device.type != "cuda":
             raise RuntimeError("TurtleHIP.forward needs ROCm device tensors (no CPU path)")
         if self._sig is None or self._sig != self._signature():

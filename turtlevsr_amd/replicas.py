@@ -61,15 +61,20 @@ def check_world(n_gpus: int) -> int | None:
     return int(w)
 
 
-def launch_workers(n: int, argv: list[str], extra_env: dict | None = None, timeout: float | None = None) -> int:
+def launch_workers(n: int, argv: list[str], extra_env: dict | None = None, timeout: float | None = None,
+                   poll_s: float = 0.2) -> int:
     """Run `argv` as `n` worker processes, one per GPU (RANK / LOCAL_RANK / WORLD_SIZE /
-    MASTER_ADDR=127.0.0.1 / MASTER_PORT set as torch.distributed.run does), and return the worst
-    exit code. Called BEFORE the parent touches the GPU: the workers are children, never an exec
-    of an initialised process. A worker that fails makes the others exit through the process
-    group's own error path; the parent kills whatever is left at `timeout`."""
+    MASTER_ADDR=127.0.0.1 / MASTER_PORT set as torch.distributed.run does), and return an exit
+    code: 0 when every worker succeeded, otherwise the code of the first worker seen failing.
+    Called BEFORE the parent touches the GPU: the workers are children, never an exec of an
+    initialised process. All workers are polled against ONE deadline (`timeout` seconds for the
+    whole group); as soon as one exits non-zero - e.g. before the rendezvous, where its siblings
+    would otherwise block until the process group's own timeout - the others are terminated.
+    At the deadline every survivor is killed and the result is 124 (as `timeout(1)`)."""
     import os
     import socket
     import subprocess
+    import time
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -79,12 +84,31 @@ def launch_workers(n: int, argv: list[str], extra_env: dict | None = None, timeo
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         env.update(extra_env or {})
         procs.append(subprocess.Popen(argv, env=env))
+    deadline = None if timeout is None else time.monotonic() + timeout
     rc = 0
-    for p in procs:
-        try:
-            code = p.wait(timeout=timeout)
-        except subprocess.TimeoutExpired:
-            p.kill()
-            code = p.wait()
-        rc = code if rc == 0 else rc
-    return rc
+
+    def stop_all():
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_kill = time.monotonic() + 10.0
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.0, t_kill - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            stop_all()
+            return rc
+        if all(c == 0 for c in codes):
+            return 0
+        if deadline is not None and time.monotonic() >= deadline:
+            stop_all()
+            return 124
+        time.sleep(poll_s)

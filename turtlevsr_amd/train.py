@@ -21,6 +21,7 @@ base_model.py:340-365, dist_util.py:15-30) on the GPU:
 """
 from __future__ import annotations
 
+import math
 from typing import List, Optional
 
 import torch
@@ -43,35 +44,65 @@ def _conv1(m, x):
     return F.conv2d(x, m.weight, m.bias)
 
 
-class TurtleTrain(TurtleParams):
-    """Differentiable Turtle_t1 (turtle_t1_arch.py:932-1139); ``ops`` supplies layer_norm,
-    dwconv3x3 and gelu_gate (``train_ops.HipOps`` on the GPU)."""
+def positional_encoding_2d(c: int, h: int, w: int) -> torch.Tensor:
+    """Sinusoidal 2-D encoding of the t0 StateAlignBlock (turtle_arch.py:412-439): channels
+    [0, c/2) encode the column, [c/2, c) the row, sin on even and cos on odd channels, frequencies
+    10000^(-2i / (c/2))."""
+    if c % 4:
+        raise ValueError(f"Cannot use sin/cos positional encoding with odd dimension (got dim={c})")
+    half = c // 2
+    freq = torch.exp(torch.arange(0.0, half, 2) * -(math.log(10000.0) / half))      # [half / 2]
+    aw = torch.arange(0.0, w)[:, None] * freq                                       # [w, half / 2]
+    ah = torch.arange(0.0, h)[:, None] * freq
+    pe = torch.empty(c, h, w)
+    pe[0:half:2] = torch.sin(aw).t()[:, None, :].expand(-1, h, -1)
+    pe[1:half:2] = torch.cos(aw).t()[:, None, :].expand(-1, h, -1)
+    pe[half::2] = torch.sin(ah).t()[:, :, None].expand(-1, -1, w)
+    pe[half + 1::2] = torch.cos(ah).t()[:, :, None].expand(-1, -1, w)
+    return pe
 
-    def __init__(self, opt: dict, ops=None):
-        super().__init__(opt)
-        if self.arch.t0:
-            raise ValueError("training is implemented for the Turtle_t1 network")
+
+class TrainGraph:
+    """The differentiable Turtle_t1 / TurtleSuper_t1 / t0 forward (turtle_t1_arch.py:932-1139,
+    turtlesuper_t1_arch.py:1049-1071, turtle_arch.py:459-533) over a ``TurtleParams`` tree.
+
+    Mixed into ``TurtleTrain`` and into the drop-in inference module (``model.TurtleHIP``), which
+    routes its forward here whenever autograd is recording and a parameter requires grad, so the
+    module ``make_model(opt)`` returns trains under the reference's own loop
+    (video_restoration_model.py:78-107). The op set (``graph_ops``) is ``train_ops.HipOps``: the HIP
+    kernels, forward and backward; tests inject ATen ops to run the graph on CPU."""
+
+    graph_ops = None            # op-set class; None -> train_ops.HipOps
+    sr = False
+
+    def _ops(self):
+        ops = self.graph_ops
         if ops is None:
             from .train_ops import HipOps
             ops = HipOps
-        self.ops = ops
-        self._ball = {}
+        return ops
 
     # ---- blocks (turtle_t1_arch.py:159-811) ------------------------------------------------------
     def _ln(self, m, x):
-        return self.ops.layer_norm(x, m.body.weight, getattr(m.body, "bias", None), self.arch.ln_type == "BiasFree")
+        return self._ops().layer_norm(x, m.body.weight, getattr(m.body, "bias", None), self.arch.ln_type == "BiasFree")
 
     def _dw(self, m, x):
-        return self.ops.dwconv3x3(x, m.weight, m.bias)
+        return self._ops().dwconv3x3(x, m.weight, m.bias)
+
+    def _c1(self, m, x):                            # nn.Conv2d(K, N, 1): the op set's GEMM when it has one
+        ops = self._ops()
+        if hasattr(ops, "conv1x1"):
+            return ops.conv1x1(x, m.weight, m.bias)
+        return _conv1(m, x)
 
     def _gffw(self, m, x):                          # GatedFeedForward 159-178
-        return _conv1(m.project_out, self.ops.gelu_gate(self._dw(m.dwconv, _conv1(m.project_in, x))))
+        return self._c1(m.project_out, self._ops().gelu_gate(self._dw(m.dwconv, self._c1(m.project_in, x))))
 
     def _ffw(self, m, x):                           # FeedForward 181-210
-        return _conv1(m.conv5, F.gelu(_conv1(m.conv4, x))) * m.gamma
+        return self._c1(m.conv5, F.gelu(self._c1(m.conv4, x))) * m.gamma
 
     def _reduced(self, m, x):                       # ReducedAttn 704-742
-        return _conv1(m.conv3, F.gelu(self._dw(m.conv2, _conv1(m.conv1, x)))) * m.beta
+        return self._c1(m.conv3, F.gelu(self._dw(m.conv2, self._c1(m.conv1, x)))) * m.beta
 
     @staticmethod
     def _heads(t, heads):
@@ -81,35 +112,63 @@ class TurtleTrain(TurtleParams):
     def _chan(self, m, x, heads, kc=None, vc=None, ntc=None):
         """ChannelAttention 666-702; with caches / ntc: FrameHistoryRouter 218-286."""
         b, c, h, w = x.shape
-        q, k, v = self._dw(m.qkv_dwconv, _conv1(m.qkv, x)).chunk(3, dim=1)
+        qkv = self._dw(m.qkv_dwconv, self._c1(m.qkv, x))
+        ops = self._ops()
+        if ntc is None and kc is None and vc is None and hasattr(ops, "gram"):
+            # on the op set's kernels: Gram of the raw q, k over HW (per head) divided by the L2
+            # norms (== normalising first, 690-693), softmax, then project_out . blockdiag(A) as
+            # one per-image weight set applied to v (A v followed by project_out, 697-702)
+            q, k, v = qkv[:, :c], qkv[:, c:2 * c], qkv[:, 2 * c:]
+            ch = c // heads
+            G = ops.gram(q, k, heads)                                          # [b, heads, ch, ch]
+            nq = q.float().square().sum((2, 3)).sqrt().clamp_min(L2_EPS).view(b, heads, ch, 1)
+            nk = k.float().square().sum((2, 3)).sqrt().clamp_min(L2_EPS).view(b, heads, 1, ch)
+            a = torch.softmax(G / (nq * nk) * m.temperature, dim=-1)
+            wp = m.project_out.weight.reshape(c, heads, ch)
+            weff = torch.einsum("ohi,bhij->bohj", wp, a).reshape(b, c, c)
+            return ops.conv1x1(v, weff, m.project_out.bias), None, None
+        q, k, v = qkv.chunk(3, dim=1)
         q, k, v = _l2n(self._heads(q, heads), -1), _l2n(self._heads(k, heads), -1), self._heads(v, heads)
         if kc is not None and vc is not None:
             k = torch.cat([kc.to(k.dtype), k], dim=2)
             v = torch.cat([vc.to(v.dtype), v], dim=2)
         a = torch.softmax(q @ k.transpose(-2, -1) * m.temperature, dim=-1)
-        out = _conv1(m.project_out, (a @ v).reshape(b, c, h, w))
+        out = self._c1(m.project_out, (a @ v).reshape(b, c, h, w))
         if ntc is None:
             return out, None, None
         keep = int(ntc * c / heads)
         return out, k[:, :, -keep:, :], v[:, :, -keep:, :]
 
     def _ball_mask(self, th, tw, dev, dtype):
+        cache = self.__dict__.setdefault("_ball", {})
         key = (th, tw, dev, dtype)
-        if key not in self._ball:
+        if key not in cache:
             i = torch.arange(th, device=dev).repeat_interleave(tw)
             j = torch.arange(tw, device=dev).repeat(th)
-            self._ball[key] = (((i[:, None] - i[None, :]).abs() + (j[:, None] - j[None, :]).abs()) <= SAB_RADIUS).to(dtype)
-        return self._ball[key]
+            cache[key] = (((i[:, None] - i[None, :]).abs() + (j[:, None] - j[None, :]).abs()) <= SAB_RADIUS).to(dtype)
+        return cache[key]
+
+    @staticmethod
+    def _dilated(t, ws):
+        """'b d (p1 h) (p2 w) -> b 1 1 (h w) (p1 p2 d)' (turtle_t1_arch.py:573-574)."""
+        b, c, hl, wl = t.shape
+        hh, ww = hl // ws, wl // ws
+        return t.reshape(b, c, ws, hh, ws, ww).permute(0, 3, 5, 2, 4, 1).reshape(b, 1, 1, hh * ww, ws * ws * c)
+
+    @staticmethod
+    def _undilated(o, bt, c, hl, wl, ws):
+        hh, ww = hl // ws, wl // ws
+        return o.reshape(bt, hh, ww, ws, ws, c).permute(0, 5, 3, 1, 4, 2).reshape(bt, c, hl, wl)
 
     def _sab(self, m, x, ws, ntc, kc, vc):
         """StateAlignBlock live forward 548-610 (top-5 394-416, L1 ball 448-464, clipped_softmax 115-132)."""
         b, c, hl, wl = x.shape
-        qk = self._dw(m.qk_dwconv, _conv1(m.qk, x))
+        qk = self._dw(m.qk_dwconv, self._c1(m.qk, x))
         q, k = qk[:, :c], qk[:, c:]
-        v = self._dw(m.v_dwconv, _conv1(m.v, x))
+        v = self._dw(m.v_dwconv, self._c1(m.v, x))
         g = 2 * c
-        k = F.conv2d(_conv1(m.k2, k), m.k2_dwconv.weight, m.k2_dwconv.bias, ws, 1, 1, g)
-        q = F.conv2d(_conv1(m.q2, q), m.q2_dwconv.weight, m.q2_dwconv.bias, ws, 1, 1, g)
+        k = F.conv2d(self._c1(m.k2, k), m.k2_dwconv.weight, m.k2_dwconv.bias, ws, 1, 1, g)
+        q = F.conv2d(self._c1(m.q2, q), m.q2_dwconv.weight, m.q2_dwconv.bias, ws, 1, 1, g)
         th, tw = q.shape[2], q.shape[3]
         hh, ww = hl // ws, wl // ws
         if th * tw != hh * ww:
@@ -117,7 +176,7 @@ class TurtleTrain(TurtleParams):
         n = th * tw
         q = _l2n(q.reshape(b, g, n).transpose(1, 2).reshape(b, 1, 1, n, g), -1)
         k = _l2n(k.reshape(b, g, n).transpose(1, 2).reshape(b, 1, 1, n, g), -1)
-        vt = v.reshape(b, c, ws, hh, ws, ww).permute(0, 3, 5, 2, 4, 1).reshape(b, 1, 1, n, ws * ws * c)
+        vt = self._dilated(v, ws)
         if kc is not None and vc is not None:
             k = torch.cat([kc.to(k.dtype), k], dim=1)
             vt = torch.cat([vc.to(vt.dtype), vt], dim=1)
@@ -128,16 +187,38 @@ class TurtleTrain(TurtleParams):
         zero = s == 0
         p = torch.softmax(s.masked_fill(zero, float("-inf")), dim=-1).masked_fill(zero, 0.0)
         a = p / p.sum(dim=-1, keepdim=True)
-        o = (a @ vt).reshape(b * t, hh, ww, ws, ws, c).permute(0, 5, 3, 1, 4, 2).reshape(b * t, c, hl, wl)
-        o = _conv1(m.project_out, o).reshape(b, t, c, hl, wl)
+        o = self._undilated(a @ vt, b * t, c, hl, wl, ws)
+        o = self._c1(m.project_out, o).reshape(b, t, c, hl, wl)
         return o, k[:, -ntc:], vt[:, -ntc:]
+
+    def _sab_t0(self, m, x, ws, ntc, kc, vc):
+        """StateAlignBlock of the t0 network (turtle_arch.py:459-533): the attention it computes is
+        discarded (`out = v`, 521-523), so the output is project_out of every frame's v; the caches
+        are the last ntc frames of the dilated, L2-normalised k (positional encoding on the qk input,
+        412-439) and of v."""
+        b, c, hl, wl = x.shape
+        pos = positional_encoding_2d(c, hl, wl).to(device=x.device, dtype=x.dtype)
+        qk = self._dw(m.qk_dwconv, self._c1(m.qk, x + pos))
+        k = qk[:, c:]
+        v = self._dw(m.v_dwconv, self._c1(m.v, x))
+        if (hl // ws) * (wl // ws) < SAB_TOPK:
+            raise RuntimeError("selected index k out of range")
+        kt = _l2n(self._dilated(k, ws), -1)
+        vt = self._dilated(v, ws)
+        if kc is not None and vc is not None:
+            kt = torch.cat([kc.to(kt.dtype), kt], dim=1)
+            vt = torch.cat([vc.to(vt.dtype), vt], dim=1)
+        t = vt.shape[1]
+        o = self._c1(m.project_out, self._undilated(vt, b * t, c, hl, wl, ws)).reshape(b, t, c, hl, wl)
+        return o, kt[:, -ntc:], vt[:, -ntc:]
 
     def _chm(self, m, x, heads, ws, ntc, kc, vc):
         """CausalHistoryModel 612-662."""
         b, c, h, w = x.shape
-        xs, k_keep, v_keep = self._sab(m.spatial_aligner, x, ws, ntc, kc, vc)
+        sab = self._sab_t0 if self.arch.t0 else self._sab
+        xs, k_keep, v_keep = sab(m.spatial_aligner, x, ws, ntc, kc, vc)
         t = xs.shape[1]
-        kv = self._dw(m.kv_dwconv, _conv1(m.kv, xs.reshape(b * t, c, h, w)))
+        kv = self._dw(m.kv_dwconv, self._c1(m.kv, xs.reshape(b * t, c, h, w)))
         kh, vh = kv[:, :c], kv[:, c:]
         ch = c // heads
         kh = kh.reshape(b, t, heads, ch, h * w).transpose(1, 2).reshape(b, heads, t * ch, h * w)
@@ -177,15 +258,27 @@ class TurtleTrain(TurtleParams):
         x, k2o, v2o = self._block(specs[-1], mods[-1], x, k2, v2)
         return x, k1o, v1o, k2o, v2o
 
-    def forward(self, inp_img_: torch.Tensor, k_cached: Optional[List] = None, v_cached: Optional[List] = None):
-        """Turtle_t1.forward 1045-1132: [B, 2, C, H, W] -> (out [B, C, H, W], k_list[8], v_list[8])."""
+    def graph_forward(self, inp_img_: torch.Tensor, k_cached: Optional[List] = None, v_cached: Optional[List] = None):
+        """Turtle_t1.forward 1045-1132 (TurtleSuper_t1: bilinear x4 first, turtlesuper_t1_arch.py:
+        1049-1071): [B, 2, C, H, W] -> (out [B, C, H, W] (x4 for SR), k_list[8], v_list[8])."""
         b, _, c, h, w = inp_img_.shape
         if k_cached is None:
             k_cached, v_cached = [None] * 8, [None] * 8
-        ph, pw = (32 - h % 32) % 32, (32 - w % 32) % 32
-        x5 = F.pad(inp_img_, (0, pw, 0, ph)) if ph or pw else inp_img_
-        current = x5[:, 1]
-        img = torch.cat([x5[:, 0], x5[:, 1]], dim=1) if self.arch.use_both else current
+        if self.sr:
+            if self.arch.use_both:      # turtlesuper_t1_arch.py:1059-1065 never defines `current` there
+                raise ValueError("TurtleSuper_t1 with use_both_input=True is not runnable in the reference")
+            h, w = 4 * h, 4 * w
+            src = F.interpolate(inp_img_[:, 1], scale_factor=4, mode="bilinear", align_corners=False)
+            ph, pw = (32 - h % 32) % 32, (32 - w % 32) % 32
+            img = F.pad(src, (0, pw, 0, ph)) if ph or pw else src
+            current = img[:, -c:]
+        else:
+            ph, pw = (32 - h % 32) % 32, (32 - w % 32) % 32
+            x5 = F.pad(inp_img_, (0, pw, 0, ph)) if ph or pw else inp_img_
+            current = x5[:, 1]
+            img = torch.cat([x5[:, 0], x5[:, 1]], dim=1) if self.arch.use_both else current
+        if getattr(self._ops(), "channels_last", False):
+            img = img.contiguous(memory_format=torch.channels_last)
         ip = self.input_projection
         e1 = F.conv2d(img.float(), ip.weight, ip.bias, 1, 1)
         ks, vs = [], []
@@ -196,15 +289,29 @@ class TurtleTrain(TurtleParams):
         e3, k, v = self._level("encoder_level3", down(self.down2_3, e2), k_cached[2], v_cached[2]); ks.append(k); vs.append(v)
         lat, k1, v1, k2, v2 = self._latent(down(self.down3_4, e3), k_cached[3], v_cached[3], k_cached[4], v_cached[4])
         ks += [k1, k2]; vs += [v1, v2]
-        d3 = _conv1(self.reduce_chan_level3, torch.cat([up(self.up4_3, lat), e3], 1))
+        d3 = self._c1(self.reduce_chan_level3, torch.cat([up(self.up4_3, lat), e3], 1))
         d3, k, v = self._level("decoder_level3", d3, k_cached[5], v_cached[5]); ks.append(k); vs.append(v)
-        d2 = _conv1(self.reduce_chan_level2, torch.cat([up(self.up3_2, d3), e2], 1))
+        d2 = self._c1(self.reduce_chan_level2, torch.cat([up(self.up3_2, d3), e2], 1))
         d2, k, v = self._level("decoder_level2", d2, k_cached[6], v_cached[6]); ks.append(k); vs.append(v)
-        d1 = _conv1(self.reduce_chan_level1, torch.cat([up(self.up2_1, d2), e1], 1))
+        d1 = self._c1(self.reduce_chan_level1, torch.cat([up(self.up2_1, d2), e1], 1))
         d1, k, v = self._level("decoder_level1", d1, k_cached[7], v_cached[7]); ks.append(k); vs.append(v)
         r, _, _ = self._level("refinement", d1)
         out = F.conv2d(r, self.ending.weight, self.ending.bias, 1, 1) + current
         return out[:, :, :h, :w], ks, vs
+
+
+class TurtleTrain(TrainGraph, TurtleParams):
+    """Differentiable Turtle_t1 (turtle_t1_arch.py:932-1139) for the training step; ``ops`` supplies
+    layer_norm, dwconv3x3 and gelu_gate (``train_ops.HipOps`` on the GPU)."""
+
+    def __init__(self, opt: dict, ops=None, sr: bool = False):
+        TurtleParams.__init__(self, opt)
+        self.sr = sr
+        if ops is not None:
+            self.graph_ops = ops
+
+    def forward(self, inp_img_: torch.Tensor, k_cached: Optional[List] = None, v_cached: Optional[List] = None):
+        return self.graph_forward(inp_img_, k_cached, v_cached)
 
 
 class Trainer:

@@ -1,15 +1,23 @@
 """Autograd Functions over the hand-written HIP training kernels (include/turtle_train.h).
 
-The training graph (turtlevsr_amd/train.py) runs these three op families through libturtle_hip.so,
-forward and backward:
+The training graph (turtlevsr_amd/train.py) keeps its activations channels-last (torch
+``channels_last``: NHWC storage, the inference path's layout) and runs these op families through
+libturtle_hip.so, forward and backward:
 
-* ``layer_norm``  per-pixel LayerNorm over channels (turtle_t1_arch.py:67-112), 98 per frame;
-* ``dwconv3x3``   depthwise 3x3 / pad 1 convolutions (99 per frame: qkv_dwconv, conv2, dwconv,
-                  qk/v/kv_dwconv);
-* ``gelu_gate``   gelu(x1) * x2 of the GatedFeedForward (turtle_t1_arch.py:176).
+* ``conv1x1``      pointwise convolutions (217 per frame, 87 % of the MACs): the inference GEMM
+                   family forward and for the input gradient (W transposed); the weight gradient
+                   dW = dY^T X as a reduction GEMM over pixels on the matrix cores; bias gradients as
+                   column sums. Per-image weight sets (channel attention W_eff = project_out .
+                   blockdiag(A), turtle_t1_arch.py:694-702) use the same kernels;
+* ``gram``         the channel-attention Gram q^T k over HW per head (turtle_t1_arch.py:694-697) as a
+                   reduction GEMM; its backward as GEMMs with block-diagonal per-image weights;
+* ``layer_norm``   per-pixel LayerNorm over channels (turtle_t1_arch.py:67-112), 98 per frame;
+* ``dwconv3x3``    depthwise 3x3 / pad 1 convolutions (99 per frame);
+* ``gelu_gate``    gelu(x1) * x2 of the GatedFeedForward (turtle_t1_arch.py:176).
 
 They run on the caller's current HIP stream; weights and their gradients are fp32, activations
-fp32 or bf16 (autocast). There is no CPU path: a CPU tensor or a missing library raises.
+fp32 or bf16 (autocast), fp16 for the elementwise kernels; the GEMMs take fp16 autocast operands
+as bf16 (cast in, cast back). There is no CPU path: a CPU tensor or a missing library raises.
 """
 from __future__ import annotations
 
@@ -20,6 +28,7 @@ import torch
 from . import _lib
 
 _train = None
+CL = torch.channels_last
 
 
 def lib():
@@ -27,13 +36,18 @@ def lib():
     if _train is not None:
         return _train
     L = _lib.lib()
-    vp, i64, ci = C.c_void_p, C.c_int64, C.c_int
-    L.turtle_train_ln_fwd.argtypes = [vp, vp, vp, vp, vp, vp, i64, ci, i64, ci, ci, vp]
-    L.turtle_train_ln_bwd.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, ci, i64, ci, ci, vp]
-    L.turtle_train_dw3x3_fwd.argtypes = [vp, vp, vp, vp, i64, ci, ci, ci, ci, ci, vp]
-    L.turtle_train_dw3x3_wgrad.argtypes = [vp, vp, vp, vp, i64, ci, ci, ci, ci, vp]
-    L.turtle_train_gate_fwd.argtypes = [vp, vp, i64, ci, i64, ci, vp]
-    L.turtle_train_gate_bwd.argtypes = [vp, vp, vp, i64, ci, i64, ci, vp]
+    vp, i64, ci, sz = C.c_void_p, C.c_int64, C.c_int, C.c_size_t
+    L.turtle_train_ln_fwd.argtypes = [vp, i64, vp, vp, vp, i64, vp, vp, i64, ci, ci, ci, vp]
+    L.turtle_train_ln_bwd.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, vp, i64, ci, ci, ci, vp]
+    L.turtle_train_dw3x3_fwd.argtypes = [vp, i64, vp, vp, vp, i64, i64, ci, ci, ci, ci, ci, vp]
+    L.turtle_train_dw3x3_wgrad.argtypes = [vp, i64, vp, i64, vp, vp, i64, ci, ci, ci, ci, vp]
+    L.turtle_train_gate_fwd.argtypes = [vp, i64, vp, i64, i64, ci, ci, vp]
+    L.turtle_train_gate_bwd.argtypes = [vp, i64, vp, i64, vp, i64, i64, ci, ci, vp]
+    L.turtle_train_colsum.argtypes = [vp, i64, vp, i64, ci, ci, vp]
+    L.turtle_train_gemm.argtypes = [vp, i64, vp, i64, i64, vp, vp, i64, i64, ci, ci, ci, vp]
+    L.turtle_train_rgemm_workspace.argtypes = [i64, ci, ci, i64]
+    L.turtle_train_rgemm_workspace.restype = sz
+    L.turtle_train_rgemm.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, i64, ci, ci, vp, sz, vp]
     _train = L
     return L
 
@@ -47,7 +61,9 @@ def _dt(t: torch.Tensor) -> int:
         return 0
     if t.dtype == torch.bfloat16:
         return 1
-    raise TypeError(f"training kernels take fp32 / bf16 activations, got {t.dtype}")
+    if t.dtype == torch.float16:
+        return 2
+    raise TypeError(f"training kernels take fp32 / bf16 / fp16 activations, got {t.dtype}")
 
 
 def _stream(t):
@@ -61,33 +77,57 @@ def _check(rc, what):
         raise RuntimeError(f"{what} failed ({rc})")
 
 
+def rows(t: torch.Tensor):
+    """(tensor, ld): a [B, C, H, W] tensor as NHWC pixel rows - channel stride 1, images and rows
+    contiguous with pixel stride ld, 16-byte aligned - copied to channels_last when it is not."""
+    if t.dim() != 4:
+        raise ValueError("expected a [B, C, H, W] tensor")
+    B, Cc, H, W = t.shape
+    s = t.stride()
+    es = t.element_size()
+    ld = s[3] if W > 1 else (s[2] if H > 1 else (s[0] if B > 1 else Cc))
+    ok = (Cc == 1 or s[1] == 1) and ld >= Cc and (W == 1 or s[3] == ld) and (H == 1 or s[2] == W * ld) and \
+         (B == 1 or s[0] == H * W * ld) and t.data_ptr() % 16 == 0 and (ld * es) % 16 == 0
+    if ok:
+        return t, ld
+    return t.contiguous(memory_format=CL), Cc
+
+
+def _empty(B, Cc, H, W, like):
+    return torch.empty((B, Cc, H, W), dtype=like.dtype, device=like.device, memory_format=CL)
+
+
+def _gemm_dt(x: torch.Tensor) -> torch.dtype:
+    return torch.float32 if x.dtype == torch.float32 else torch.bfloat16
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, biasfree: bool):
-        x = x.contiguous()
-        N, Cc = x.shape[0], x.shape[1]
-        HW = x[0, 0].numel()
-        y = torch.empty_like(x)
-        mu = torch.empty(N * HW, dtype=torch.float32, device=x.device)
+        x, ldx = rows(x)
+        B, Cc, H, W = x.shape
+        P = B * H * W
+        y = _empty(B, Cc, H, W, x)
+        mu = torch.empty(P, dtype=torch.float32, device=x.device)
         rs = torch.empty_like(mu)
         w32 = w.float().contiguous()
         b32 = None if b is None else b.float().contiguous()
-        _check(lib().turtle_train_ln_fwd(_p(x), _p(w32), _p(b32), _p(y), _p(mu), _p(rs), N, Cc, HW, int(biasfree), _dt(x),
+        _check(lib().turtle_train_ln_fwd(_p(x), ldx, _p(w32), _p(b32), _p(y), Cc, _p(mu), _p(rs), P, Cc, int(biasfree), _dt(x),
                                          _stream(x)), "ln_fwd")
         ctx.save_for_backward(x, w32, mu, rs)
-        ctx.biasfree, ctx.has_b = biasfree, b is not None
+        ctx.biasfree, ctx.has_b, ctx.ldx = biasfree, b is not None, ldx
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w32, mu, rs = ctx.saved_tensors
-        dy = dy.contiguous().to(x.dtype)
-        N, Cc = x.shape[0], x.shape[1]
-        HW = x[0, 0].numel()
-        dx = torch.empty_like(x)
+        dy, lddy = rows(dy.to(x.dtype))
+        B, Cc, H, W = x.shape
+        P = B * H * W
+        dx = _empty(B, Cc, H, W, x)
         dw = torch.zeros(Cc, dtype=torch.float32, device=x.device)
         db = torch.zeros(Cc, dtype=torch.float32, device=x.device) if ctx.has_b else None
-        _check(lib().turtle_train_ln_bwd(_p(x), _p(w32), _p(mu), _p(rs), _p(dy), _p(dx), _p(dw), _p(db), N, Cc, HW,
+        _check(lib().turtle_train_ln_bwd(_p(x), ctx.ldx, _p(w32), _p(mu), _p(rs), _p(dy), lddy, _p(dx), Cc, _p(dw), _p(db), P, Cc,
                                          int(ctx.biasfree), _dt(x), _stream(x)), "ln_bwd")
         return dx, dw, db, None
 
@@ -95,60 +135,162 @@ class _LayerNorm(torch.autograd.Function):
 class _DWConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
-        x = x.contiguous()
-        N, Cc, H, W = x.shape
-        w32 = w.float().reshape(Cc, 9).contiguous()
+        x, ldx = rows(x)
+        B, Cc, H, W = x.shape
+        w9 = w.float().reshape(Cc, 9).t().contiguous()
         b32 = None if b is None else b.float().contiguous()
-        y = torch.empty_like(x)
-        _check(lib().turtle_train_dw3x3_fwd(_p(x), _p(w32), _p(b32), _p(y), N, Cc, H, W, 0, _dt(x), _stream(x)), "dw_fwd")
-        ctx.save_for_backward(x, w32)
-        ctx.has_b = b is not None
+        y = _empty(B, Cc, H, W, x)
+        _check(lib().turtle_train_dw3x3_fwd(_p(x), ldx, _p(w9), _p(b32), _p(y), Cc, B, Cc, H, W, 0, _dt(x), _stream(x)), "dw_fwd")
+        ctx.save_for_backward(x, w9)
+        ctx.has_b, ctx.ldx = b is not None, ldx
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w32 = ctx.saved_tensors
-        dy = dy.contiguous().to(x.dtype)
-        N, Cc, H, W = x.shape
-        dx = torch.empty_like(x)
+        x, w9 = ctx.saved_tensors
+        dy, lddy = rows(dy.to(x.dtype))
+        B, Cc, H, W = x.shape
+        dx = _empty(B, Cc, H, W, x)
         st = _stream(x)
-        _check(lib().turtle_train_dw3x3_fwd(_p(dy), _p(w32), None, _p(dx), N, Cc, H, W, 1, _dt(x), st), "dw_dgrad")
-        dw = torch.zeros(Cc, 9, dtype=torch.float32, device=x.device)
+        _check(lib().turtle_train_dw3x3_fwd(_p(dy), lddy, _p(w9), None, _p(dx), Cc, B, Cc, H, W, 1, _dt(x), st), "dw_dgrad")
+        dw9 = torch.zeros(9, Cc, dtype=torch.float32, device=x.device)
         db = torch.zeros(Cc, dtype=torch.float32, device=x.device) if ctx.has_b else None
-        _check(lib().turtle_train_dw3x3_wgrad(_p(x), _p(dy), _p(dw), _p(db), N, Cc, H, W, _dt(x), st), "dw_wgrad")
-        return dx, dw.reshape(Cc, 1, 3, 3), db
+        _check(lib().turtle_train_dw3x3_wgrad(_p(x), ctx.ldx, _p(dy), lddy, _p(dw9), _p(db), B, Cc, H, W, _dt(x), st), "dw_wgrad")
+        return dx, dw9.t().reshape(Cc, 1, 3, 3), db
 
 
 class _Gate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
-        x = x.contiguous()
-        N, C2 = x.shape[0], x.shape[1]
-        h, HW = C2 // 2, x[0, 0].numel()
-        y = torch.empty((N, h) + tuple(x.shape[2:]), dtype=x.dtype, device=x.device)
-        _check(lib().turtle_train_gate_fwd(_p(x), _p(y), N, h, HW, _dt(x), _stream(x)), "gate_fwd")
+        x, ldx = rows(x)
+        B, C2, H, W = x.shape
+        h = C2 // 2
+        y = _empty(B, h, H, W, x)
+        _check(lib().turtle_train_gate_fwd(_p(x), ldx, _p(y), h, B * H * W, h, _dt(x), _stream(x)), "gate_fwd")
         ctx.save_for_backward(x)
+        ctx.ldx = ldx
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
-        dy = dy.contiguous().to(x.dtype)
-        N, C2 = x.shape[0], x.shape[1]
-        dx = torch.empty_like(x)
-        _check(lib().turtle_train_gate_bwd(_p(x), _p(dy), _p(dx), N, C2 // 2, x[0, 0].numel(), _dt(x), _stream(x)), "gate_bwd")
+        dy, lddy = rows(dy.to(x.dtype))
+        B, C2, H, W = x.shape
+        dx = _empty(B, C2, H, W, x)
+        _check(lib().turtle_train_gate_bwd(_p(x), ctx.ldx, _p(dy), lddy, _p(dx), C2, B * H * W, C2 // 2, _dt(x), _stream(x)),
+               "gate_bwd")
         return dx
 
 
+def _rgemm(a, lda, b, ldb, P, N, K, img_px):
+    """c [nimg, N, K] fp32 = sum over each image's pixels (all pixels when img_px = 0) of
+    a[p][n] b[p][k]; a, b are pixel-row tensors (or head slices of one)."""
+    L = lib()
+    nimg = P // img_px if img_px else 1
+    c = torch.empty(nimg, N, K, dtype=torch.float32, device=a.device)
+    nws = L.turtle_train_rgemm_workspace(P, N, K, img_px)
+    ws = torch.empty(max(int(nws), 16), dtype=torch.uint8, device=a.device)
+    _check(L.turtle_train_rgemm(_p(a), lda, _p(b), ldb, _p(c), P, N, K, img_px, 0, _dt(a), _p(ws), ws.numel(), _stream(a)),
+           "rgemm")
+    return c
+
+
+def _gemm_into(x, ldx, w, img_px, bias, P, K, N):
+    """y = x w^T (+ bias): x rows [P][ldx] of a [B, K, H, W] tensor; w [N, K] or [nimg, N, K] in x's
+    dtype; returns a channels_last [B, N, H, W] tensor."""
+    B, _, H, W = x.shape
+    y = _empty(B, N, H, W, x)
+    wstride = (N * K) if w.dim() == 3 else 0
+    _check(lib().turtle_train_gemm(_p(x), ldx, _p(w), wstride, img_px if wstride else 0, _p(bias), _p(y), N, P, K, N, _dt(x),
+                                   _stream(x)), "gemm")
+    return y
+
+
+class _Conv1x1(torch.autograd.Function):
+    """y = x W^T + b on NHWC rows; W [N, K] (shared) or [B, N, K] (one set per image)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        gdt = _gemm_dt(x)
+        out_dt = x.dtype
+        xg, ldx = rows(x.to(gdt))
+        B, K, H, W = xg.shape
+        N = w.shape[-2]
+        wg = w.to(gdt).contiguous()
+        b32 = None if b is None else b.float().contiguous()
+        y = _gemm_into(xg, ldx, wg, H * W, b32, B * H * W, K, N)
+        ctx.save_for_backward(xg, wg)
+        ctx.ldx, ctx.has_b, ctx.in_dt, ctx.w_dt = ldx, b is not None, x.dtype, w.dtype
+        return y.to(out_dt)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xg, wg = ctx.saved_tensors
+        B, K, H, W = xg.shape
+        N = wg.shape[-2]
+        P, HW = B * H * W, H * W
+        dy, lddy = rows(dy.to(xg.dtype))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wt = wg.transpose(-1, -2).contiguous()               # [.., K, N]
+            dx = _gemm_into(dy, lddy, wt, HW, None, P, N, K).to(ctx.in_dt)
+        if ctx.needs_input_grad[1]:
+            if wg.dim() == 3:
+                dw = _rgemm(dy, lddy, xg, ctx.ldx, P, N, K, HW)  # [B, N, K]
+            else:
+                dw = _rgemm(dy, lddy, xg, ctx.ldx, P, N, K, 0)[0]
+            dw = dw.to(ctx.w_dt)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.zeros(N, dtype=torch.float32, device=dy.device)
+            _check(lib().turtle_train_colsum(_p(dy), lddy, _p(db), P, N, _dt(dy), _stream(dy)), "colsum")
+        return dx, dw, db
+
+
+class _Gram(torch.autograd.Function):
+    """G[b, h] = sum over HW of q[b, head h channels] k[b, head h channels]^T (fp32)."""
+
+    @staticmethod
+    def forward(ctx, q, k, heads: int):
+        gdt = _gemm_dt(q)
+        q, ldq = rows(q.to(gdt))
+        k, ldk = rows(k.to(gdt))
+        B, Cc, H, W = q.shape
+        ch = Cc // heads
+        P, HW = B * H * W, H * W
+        G = torch.empty(B, heads, ch, ch, dtype=torch.float32, device=q.device)
+        for h in range(heads):
+            G[:, h] = _rgemm(q[:, h * ch:(h + 1) * ch], ldq, k[:, h * ch:(h + 1) * ch], ldk, P, ch, ch, HW)
+        ctx.save_for_backward(q, k)
+        ctx.heads, ctx.ldq, ctx.ldk = heads, ldq, ldk
+        return G
+
+    @staticmethod
+    def backward(ctx, dG):
+        q, k = ctx.saved_tensors
+        B, Cc, H, W = q.shape
+        heads, ch = ctx.heads, Cc // ctx.heads
+        HW, P = H * W, B * H * W
+        # block-diagonal per-image weights D[b][i][j] = dG[b, h, i', j'] inside head h:
+        # dq = k D^T, dk = q D (GEMMs over the pixels with one weight set per image)
+        D = torch.zeros(B, Cc, Cc, dtype=torch.float32, device=q.device)
+        for h in range(heads):
+            D[:, h * ch:(h + 1) * ch, h * ch:(h + 1) * ch] = dG[:, h]
+        dq = _gemm_into(k, ctx.ldk, D.to(k.dtype).contiguous(), HW, None, P, Cc, Cc)
+        dk = _gemm_into(q, ctx.ldq, D.transpose(1, 2).to(q.dtype).contiguous(), HW, None, P, Cc, Cc)
+        return dq, dk, None
+
+
 def _act(x: torch.Tensor) -> torch.Tensor:
-    """Activations enter the kernels in the autocast dtype (bf16 under bf16 autocast)."""
+    """Activations enter the kernels in the autocast dtype (bf16 / fp16 under autocast)."""
     if torch.is_autocast_enabled("cuda") and x.dtype == torch.float32:
         return x.to(torch.get_autocast_dtype("cuda"))
     return x
 
 
 class HipOps:
-    """The op set of the training graph, on the HIP kernels."""
+    """The op set of the training graph, on the HIP kernels (channels-last activations)."""
+
+    channels_last = True
 
     @staticmethod
     def layer_norm(x, w, b, biasfree: bool):
@@ -161,3 +303,12 @@ class HipOps:
     @staticmethod
     def gelu_gate(x):
         return _Gate.apply(_act(x))
+
+    @staticmethod
+    def conv1x1(x, w, b):
+        """nn.Conv2d(K, N, 1)(x): w [N, K, 1, 1] (or [B, N, K]: one weight set per image)."""
+        return _Conv1x1.apply(_act(x), w.reshape(w.shape[0], w.shape[1]) if w.dim() == 4 else w, b)
+
+    @staticmethod
+    def gram(q, k, heads: int):
+        return _Gram.apply(_act(q), _act(k), heads)
