@@ -58,6 +58,12 @@ for s in $STEPS; do
       timeout -s KILL 120 rocprofv3 --kernel-include-regex $K --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_MISC -f csv -d $OUT/pmc/p2 -o run -- $B > $OUT/pmc_p2.log 2>&1 &&
       timeout -s KILL 120 rocprofv3 --kernel-include-regex $K --pmc SQ_ACTIVE_INST_MFMA SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM SQ_WAIT_INST_VMEM SQ_INSTS_VMEM -f csv -d $OUT/pmc/p3 -o run -- $B > $OUT/pmc_p3.log 2>&1
       rc=$?; echo "pmc rc=$rc"; python3 tools/kpmc_report.py $OUT/pmc > $OUT/pmc_report.txt 2>&1; head -20 $OUT/pmc_report.txt; [ $rc -ne 0 ] && exit $rc ;;
+    pdb)
+      timeout -k 10 120 ./tools/pdbench 20 > $OUT/pdbench.log 2>&1 && timeout -k 10 120 ./tools/pdbench 5 16 56 >> $OUT/pdbench.log 2>&1
+      rc=$?; echo "pdb rc=$rc"; cat $OUT/pdbench.log | head -30; [ $rc -ne 0 ] && exit $rc ;;
+    iso)
+      timeout -k 10 300 python -u tools/bf16_isolate.py > $OUT/iso.log 2>&1
+      rc=$?; echo "iso rc=$rc"; cat $OUT/iso.log | grep PSNR; [ $rc -ne 0 ] && exit $rc ;;
     tdebug)
       HIP_LAUNCH_BLOCKING=1 timeout -k 10 300 python -u tools/train_debug.py ${TD_CLIP:-train_tiny} > $OUT/train_debug.log 2>&1
       rc=$?; echo "tdebug rc=$rc"; tail -5 $OUT/train_debug.log; [ $rc -ne 0 ] && exit $rc ;;

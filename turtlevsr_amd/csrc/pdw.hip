@@ -309,7 +309,9 @@ __global__ __launch_bounds__(PD_NT, 1) void pdw_kernel(PdwArgs g) {
   // other; the W_in DMA of step s + 1 is issued after the barrier. Per wave and iteration the vector
   // memory queue gets 2 DMA then 2 stores, so at the top of iteration s, vmcnt(2) means "the W_in of
   // step s has landed" (the 2 younger ops are the previous iteration's stores) ----
+  const bool drain = (g.split & 2) != 0;          // debug: drain every vector-memory op at the barrier
   auto sync = [&] {
+    if (drain) pd_wait_vm<0>();
     pd_wait_vm<2>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -363,7 +365,7 @@ void launch_pdw(const PdwArgs& g, hipStream_t st) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(pdw_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  if (g.split) hipLaunchKernelGGL(pdw_kernel<1>, dim3((unsigned)pdw_blocks(g)), dim3(PD_NT), pdw_lds_bytes(g.N1), st, g);
+  if (g.split & 1) hipLaunchKernelGGL(pdw_kernel<1>, dim3((unsigned)pdw_blocks(g)), dim3(PD_NT), pdw_lds_bytes(g.N1), st, g);
   else hipLaunchKernelGGL(pdw_kernel<0>, dim3((unsigned)pdw_blocks(g)), dim3(PD_NT), pdw_lds_bytes(g.N1), st, g);
 }
 

@@ -331,7 +331,7 @@ struct TurtleHandle {
   int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
-  bool pdw = true;                                    // level-3 GatedFeedForward: LN -> project_in -> dw -> gate in one kernel (pdw.hip)
+  bool pdw = false;                                   // level-3 GatedFeedForward: LN -> project_in -> dw -> gate in one kernel (pdw.hip); off until it beats pn + dwgemm
   int pdw_split = 1;                                  // pdw schedule variant (pdw.hip)
   bool split_out = true;                              // split-bf16 weights for reduce_chan_level1 (bf16 builds)
   bool dwgemm_attn = true;                            // channel attention: v's depthwise inside the W_eff GEMM (dwgemm.hip)
@@ -484,6 +484,7 @@ static void pack_all(TurtleHandle* h) {
   Arch& A = h->arch;
   Packer pk; pk.bf16 = h->bf16();
   ModelW& M = h->mw;
+  M.reduce_split = false;
   const int d = A.dim;
   M.stem_w = pk.f32(dvec(W(h, "input_projection.weight")));
   if (has(h, "input_projection.bias")) M.stem_b = pk.f32(dvec(W(h, "input_projection.bias")));

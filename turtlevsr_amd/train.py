@@ -89,6 +89,13 @@ class TrainGraph:
     def _dw(self, m, x):
         return self._ops().dwconv3x3(x, m.weight, m.bias)
 
+    def _dense(self, x, w, b=None, stride=1, padding=1, groups=1):
+        """Dense / window convolutions (stem, ending, Down/Upsample, SAB window convs) through
+        F.conv2d on a standard-layout copy: MIOpen's channels-last backward faults on some of
+        these shapes (MI355X, ROCm 7.2), its NCHW path does not. Channels-last again afterwards."""
+        y = F.conv2d(x.contiguous(), w, b, stride, padding, 1, groups)
+        return y.contiguous(memory_format=torch.channels_last) if getattr(self._ops(), "channels_last", False) else y
+
     def _c1(self, m, x):                            # nn.Conv2d(K, N, 1): the op set's GEMM when it has one
         ops = self._ops()
         if hasattr(ops, "conv1x1"):
@@ -167,8 +174,8 @@ class TrainGraph:
         q, k = qk[:, :c], qk[:, c:]
         v = self._dw(m.v_dwconv, self._c1(m.v, x))
         g = 2 * c
-        k = F.conv2d(self._c1(m.k2, k), m.k2_dwconv.weight, m.k2_dwconv.bias, ws, 1, 1, g)
-        q = F.conv2d(self._c1(m.q2, q), m.q2_dwconv.weight, m.q2_dwconv.bias, ws, 1, 1, g)
+        k = self._dense(self._c1(m.k2, k), m.k2_dwconv.weight, m.k2_dwconv.bias, ws, 1, g)
+        q = self._dense(self._c1(m.q2, q), m.q2_dwconv.weight, m.q2_dwconv.bias, ws, 1, g)
         th, tw = q.shape[2], q.shape[3]
         hh, ww = hl // ws, wl // ws
         if th * tw != hh * ww:
@@ -277,14 +284,12 @@ class TrainGraph:
             x5 = F.pad(inp_img_, (0, pw, 0, ph)) if ph or pw else inp_img_
             current = x5[:, 1]
             img = torch.cat([x5[:, 0], x5[:, 1]], dim=1) if self.arch.use_both else current
-        if getattr(self._ops(), "channels_last", False):
-            img = img.contiguous(memory_format=torch.channels_last)
         ip = self.input_projection
-        e1 = F.conv2d(img.float(), ip.weight, ip.bias, 1, 1)
+        e1 = self._dense(img.float(), ip.weight, ip.bias)
         ks, vs = [], []
         e1, k, v = self._level("encoder_level1", e1, k_cached[0], v_cached[0]); ks.append(k); vs.append(v)
-        down = lambda m, t: F.pixel_unshuffle(F.conv2d(t, m.body[0].weight, None, 1, 1), 2)     # Downsample 136-144
-        up = lambda m, t: F.pixel_shuffle(F.conv2d(t, m.body[0].weight, None, 1, 1), 2)         # Upsample 146-154
+        down = lambda m, t: F.pixel_unshuffle(self._dense(t, m.body[0].weight), 2)     # Downsample 136-144
+        up = lambda m, t: F.pixel_shuffle(self._dense(t, m.body[0].weight), 2)         # Upsample 146-154
         e2, k, v = self._level("encoder_level2", down(self.down1_2, e1), k_cached[1], v_cached[1]); ks.append(k); vs.append(v)
         e3, k, v = self._level("encoder_level3", down(self.down2_3, e2), k_cached[2], v_cached[2]); ks.append(k); vs.append(v)
         lat, k1, v1, k2, v2 = self._latent(down(self.down3_4, e3), k_cached[3], v_cached[3], k_cached[4], v_cached[4])
@@ -296,7 +301,7 @@ class TrainGraph:
         d1 = self._c1(self.reduce_chan_level1, torch.cat([up(self.up2_1, d2), e1], 1))
         d1, k, v = self._level("decoder_level1", d1, k_cached[7], v_cached[7]); ks.append(k); vs.append(v)
         r, _, _ = self._level("refinement", d1)
-        out = F.conv2d(r, self.ending.weight, self.ending.bias, 1, 1) + current
+        out = self._dense(r, self.ending.weight, self.ending.bias) + current
         return out[:, :, :h, :w], ks, vs
 
 
