@@ -12,6 +12,13 @@ for s in $STEPS; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
       rc=$?; echo "tests rc=$rc"; tail -3 $OUT/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc ;;
+    testsall)
+      # every GPU test, no -x (one pass shows every failure); $DESELECT: extra --deselect ids
+      timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread $DESELECT > $OUT/pytest_gpu.log 2>&1
+      rc=$?; echo "testsall rc=$rc"; tail -3 $OUT/pytest_gpu.log; [ $rc -gt 1 ] && exit $rc ;;
+    vprobe)
+      timeout -k 10 300 python -u tools/variant_probe.py > $OUT/vprobe.log 2>&1
+      rc=$?; echo "vprobe rc=$rc"; cat $OUT/vprobe.log | grep dB; [ $rc -ne 0 ] && exit $rc ;;
     quick)
       timeout -k 10 600 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread -k "dropin or train" > $OUT/pytest_quick.log 2>&1
       rc=$?; echo "quick rc=$rc"; tail -3 $OUT/pytest_quick.log; [ $rc -ne 0 ] && exit $rc ;;
@@ -59,7 +66,10 @@ for s in $STEPS; do
       timeout -s KILL 120 rocprofv3 --kernel-include-regex $K --pmc SQ_ACTIVE_INST_MFMA SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM SQ_WAIT_INST_VMEM SQ_INSTS_VMEM -f csv -d $OUT/pmc/p3 -o run -- $B > $OUT/pmc_p3.log 2>&1
       rc=$?; echo "pmc rc=$rc"; python3 tools/kpmc_report.py $OUT/pmc > $OUT/pmc_report.txt 2>&1; head -20 $OUT/pmc_report.txt; [ $rc -ne 0 ] && exit $rc ;;
     pdb)
-      timeout -k 10 120 ./tools/pdbench 20 > $OUT/pdbench.log 2>&1 && timeout -k 10 120 ./tools/pdbench 5 16 56 >> $OUT/pdbench.log 2>&1
+      : > $OUT/pdbench.log
+      for hw in ${PDB_SIZES:-272x480 32x32 16x16 36x70}; do
+        timeout -k 10 120 ./tools/pdbench 20 ${hw%x*} ${hw#*x} >> $OUT/pdbench.log 2>&1 || { echo "pdbench $hw failed"; cat $OUT/pdbench.log; exit 1; }
+      done
       rc=$?; echo "pdb rc=$rc"; cat $OUT/pdbench.log | head -30; [ $rc -ne 0 ] && exit $rc ;;
     iso)
       timeout -k 10 300 python -u tools/bf16_isolate.py > $OUT/iso.log 2>&1
