@@ -1,5 +1,5 @@
 """bf16 PSNR of a golden clip under kernel-switch variants (which switch breaks bf16 parity?).
-    python tools/bf16_isolate.py [clip_gopro_64] ["pdw=0" "split_out=0" ...]"""
+    python tools/bf16_isolate.py [clip_gopro_64] ["split_out=0" "ffn=0" ...]"""
 import os
 import sys
 
@@ -13,7 +13,7 @@ from golden_io import clip_input, load, synth_sd  # noqa: E402
 from turtlevsr_amd.model import TurtleHIP  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "clip_gopro_64"
-variants = sys.argv[2:] or ["", "pdw=0", "split_out=0", "pdw=0 split_out=0"]
+variants = sys.argv[2:] or ["", "split_out=0"]
 g, meta = load(name)
 clip = torch.from_numpy(clip_input(g, meta)).cuda()
 for v in variants:

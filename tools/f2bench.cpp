@@ -7,6 +7,7 @@
 // the average launch time (HIP events) and the relative RMS / max error against that reference.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -42,7 +43,10 @@ static T* dev_copy(const std::vector<T>& h) {
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
   const char* only = argc > 2 ? argv[2] : nullptr;      // substring of the shape tag
-  const int only_v = argc > 3 ? atoi(argv[3]) : -1;     // fused2 variant (-1: all, and the old kernel)
+  // fused2 variants: a comma-separated list, or -1 (all, and the tile-fused kernel)
+  std::vector<int> vlist;
+  if (argc > 3) for (const char* p = argv[3]; *p;) { vlist.push_back(atoi(p)); while (*p && *p != ',') ++p; if (*p) ++p; }
+  const int only_v = vlist.empty() ? -1 : vlist[0];
   const Shape shapes[] = {
       {1088, 1920, 64, 320, 64, F_GATE, 1, "L1 GFFW gate"},
       {1088, 1920, 64, 128, 64, F_GELU, 1, "L1 ReducedAttn"},
@@ -149,10 +153,10 @@ int main(int argc, char** argv) {
     };
     if (only_v < 0 && has_ref) run("fused", [&] { launch_fused<bf16>(ab, 0); });
     if (fused2_ok(ab)) {
-      for (int v = 0; v < 7; ++v) {
-        if (only_v >= 0 && v != only_v) continue;
+      for (int v = 0; v < 9; ++v) {
+        if (only_v >= 0 && std::find(vlist.begin(), vlist.end(), v) == vlist.end()) continue;
         if (ab.C == 256 && v >= 3) continue;
-        if (v == 6 && !(ab.mode == F_GATE && ab.C == 64)) continue;
+        if (v >= 6 && !(ab.mode == F_GATE && ab.C == 64)) continue;
         FusedArgs c = ab; c.dbg = v;
         char nm[16]; snprintf(nm, sizeof nm, "fused2.%d", v);
         run(nm, [&] { launch_fused2(c, 0); });

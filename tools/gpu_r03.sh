@@ -48,7 +48,7 @@ for s in $STEPS; do
       rc=$?; echo "modprobe rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     ab)
       # launch-shape reports of the default build and kernel-switch variants (AB_OPTS, ';'-separated)
-      IFS=';' read -ra VARS <<< "${AB_OPTS:-;pdw_split=0;blaslt=0;pdw=0}"
+      IFS=';' read -ra VARS <<< "${AB_OPTS:-;blaslt=0}"
       i=0
       for v in "${VARS[@]}"; do
         extra=""; for o in $v; do extra="$extra --opt $o"; done
@@ -59,18 +59,18 @@ for s in $STEPS; do
         i=$((i+1))
       done ;;
     pmcpdw)
-      K=${PMC_KERNEL:-pdw_kernel}
+      K=${PMC_KERNEL:-fused2_kernel}
       B="python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-psnr --no-scaling-point --no-roofline"
       timeout -s KILL 120 rocprofv3 --kernel-include-regex $K --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES -f csv -d $OUT/pmc/p1 -o run -- $B > $OUT/pmc_p1.log 2>&1 &&
       timeout -s KILL 120 rocprofv3 --kernel-include-regex $K --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_MISC -f csv -d $OUT/pmc/p2 -o run -- $B > $OUT/pmc_p2.log 2>&1 &&
       timeout -s KILL 120 rocprofv3 --kernel-include-regex $K --pmc SQ_ACTIVE_INST_MFMA SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM SQ_WAIT_INST_VMEM SQ_INSTS_VMEM -f csv -d $OUT/pmc/p3 -o run -- $B > $OUT/pmc_p3.log 2>&1
       rc=$?; echo "pmc rc=$rc"; python3 tools/kpmc_report.py $OUT/pmc > $OUT/pmc_report.txt 2>&1; head -20 $OUT/pmc_report.txt; [ $rc -ne 0 ] && exit $rc ;;
-    pdb)
-      : > $OUT/pdbench.log
-      for hw in ${PDB_SIZES:-272x480 32x32 16x16 36x70}; do
-        timeout -k 10 120 ./tools/pdbench 20 ${hw%x*} ${hw#*x} >> $OUT/pdbench.log 2>&1 || { echo "pdbench $hw failed"; cat $OUT/pdbench.log; exit 1; }
-      done
-      rc=$?; echo "pdb rc=$rc"; cat $OUT/pdbench.log | head -30; [ $rc -ne 0 ] && exit $rc ;;
+    f2b)
+      timeout -k 10 300 ./tools/f2bench ${F2B_REPS:-20} "${F2B_ONLY:-}" ${F2B_V:-0} > $OUT/f2bench.log 2>&1
+      rc=$?; echo "f2b rc=$rc"; cat $OUT/f2bench.log; [ $rc -ne 0 ] && exit $rc ;;
+    f2old)
+      timeout -k 10 300 ./tools/f2bench_old ${F2B_REPS:-20} "${F2B_ONLY:-}" ${F2B_V:-0} > $OUT/f2bench_old.log 2>&1
+      rc=$?; echo "f2old rc=$rc"; cat $OUT/f2bench_old.log; [ $rc -ne 0 ] && exit $rc ;;
     iso)
       timeout -k 10 300 python -u tools/bf16_isolate.py > $OUT/iso.log 2>&1
       rc=$?; echo "iso rc=$rc"; cat $OUT/iso.log | grep PSNR; [ $rc -ne 0 ] && exit $rc ;;

@@ -34,6 +34,10 @@
 
 namespace turtle {
 
+#ifndef F2_WALK_UNROLL
+#define F2_WALK_UNROLL 0   // 1: the walk's 3-row trips fully unrolled (A/B builds of tools/f2bench)
+#endif
+
 constexpr int F2_TX = 14;   // output columns per tile (16 haloed lanes)
 
 template <int N, int I = 0, typename F>
@@ -89,6 +93,7 @@ template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE, int TPB = 
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void fused2_kernel(FusedArgs a) {
   using L = F2L<CM, R, HPM, TG ? 0 : N1M, MODE == F_GATEOUT ? NW * R * 512 : 0>;
   constexpr int KS = CM / 32;                       // GEMM1 K steps
+  static_assert((R + 4) * 16 * L::XP <= L::BYTES, "the walk's last trip reads two rows past the X tile");
   constexpr int NT = NW * 64;
   __shared__ __attribute__((aligned(16))) char smem[L::BYTES];
   char* sX = smem;
@@ -159,27 +164,42 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   }
   if (tile + 1 < t_end) fetch_x(tile + 1);           // in flight during this tile's walks
   __syncthreads();
-  // ---- LayerNorm statistics per haloed pixel (2 threads per pixel, shifted sums) ----
-  for (int e = tid; e < 2 * L::NXP; e += NT) {
-    const int p = e >> 1, h = e & 1;
-    float2 st{0.f, 1.f};
-    if (a.ln) {                                    // uniform: the shuffles run in whole waves
-      const bf16* row = reinterpret_cast<const bf16*>(sX + p * L::XP);
+  // ---- LayerNorm of every haloed pixel in place (2 threads per pixel, shifted sums): the tile
+  // becomes (x - mu) rs (BiasFree: x rs, uncentred), rounded to bf16 once - the resident-panel
+  // GEMM does the same - so GEMM1's epilogue is only + (W1 b_ln + b1), carried in as the MFMA's
+  // initial accumulator. The residual of GEMM2 is re-read from HBM/L2 (the raw tile is gone). ----
+  if (a.ln) {                                      // uniform: the shuffles run in whole waves
+    for (int e = tid; e < 2 * L::NXP; e += NT) {
+      const int p = e >> 1, h = e & 1;
+      bf16* row = reinterpret_cast<bf16*>(sX + p * L::XP);
       const float sh = (float)row[0];
+      constexpr int NC = CM / 16;                  // 16-byte chunks of this thread: h, h + 2, ..
+      uint4 raw[NC];
       float ls = 0.f, lq = 0.f;
 #pragma unroll
-      for (int k = h * 8; k < CM; k += 16) {
-        Vec<bf16> v; v.load(row + k);
+      for (int j = 0; j < NC; ++j) {
+        raw[j] = *reinterpret_cast<const uint4*>(row + h * 8 + 16 * j);
+        Vec<bf16> v; v.from_raw(raw[j]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) { const float d = v.v[i] - sh; ls += d; lq = fmaf(d, d, lq); }
       }
       ls += __shfl_xor(ls, 1, 64);
       lq += __shfl_xor(lq, 1, 64);
       const float md = ls / CM;
-      st = float2{sh + md, rsqrtf(fmaxf(lq / CM - md * md, 0.f) + 1e-5f)};
-      if (!a.ln_s) st.x = 0.f;                     // BiasFree LayerNorm: x * rs, uncentred
+      const float rs = rsqrtf(fmaxf(lq / CM - md * md, 0.f) + 1e-5f);
+      const float c0 = a.ln_s ? -(sh + md) * rs : 0.f;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        Vec<bf16> v; v.from_raw(raw[j]);
+        uint32_t o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const f32x2 r = __builtin_elementwise_fma(f32x2{v.v[2 * i], v.v[2 * i + 1]}, f32x2{rs, rs}, f32x2{c0, c0});
+          o[i] = (uint32_t)__builtin_bit_cast(unsigned short, (bf16)r.x) | ((uint32_t)__builtin_bit_cast(unsigned short, (bf16)r.y) << 16);
+        }
+        *reinterpret_cast<uint4*>(row + h * 8 + 16 * j) = make_uint4(o[0], o[1], o[2], o[3]);
+      }
     }
-    if (h == 0) sSt[p] = st;
   }
   __syncthreads();
 
@@ -227,23 +247,24 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
       for (int k = 0; k < KS; ++k) xf[k] = *reinterpret_cast<const bf16x8*>(xbase + hr * 16 * L::XP + k * 64);
     };
+    // GEMM1 of one haloed row from the bias (0 in the columns outside the image: the depthwise
+    // zero-pads, and the normalised tile is 0 there)
+    const f32x4 tbm = tb * colok;
+    (void)s4;
     auto gemm1 = [&](const bf16x8 (&xf)[KS]) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      f32x4 acc = tbm;
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc = mfma(wf[k], xf[k], acc);
       return acc;
     };
-    // LN / bias epilogue of haloed row hr (stats st); zero outside the image (dw zero padding)
-    auto epi = [&](const f32x4& acc, int hr, float2 st, f32x4& w) {
+    // rows outside the image are 0 (depthwise zero padding): one packed multiply by a wave-uniform
+    // 0 / 1 (the statistics of the pre-normalised tile are already applied)
+    auto epi = [&](const f32x4& acc, int hr, float2, f32x4& w) {
       const int yg = y0 - 1 + hr;
-      const float m = (yg >= 0 && yg < a.H) ? colok : 0.f;
-      const float rs = m * st.y, c0 = -st.x * st.y * m;
-      // packed f32 pairs (v_pk_mul / v_pk_fma: two lanes' values per VALU issue, same roundings)
+      const float m = (yg >= 0 && yg < a.H) ? 1.f : 0.f;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const f32x2 r = __builtin_elementwise_fma(f32x2{rs, rs}, f32x2{acc[2 * h], acc[2 * h + 1]},
-                                                  __builtin_elementwise_fma(f32x2{c0, c0}, f32x2{s4[2 * h], s4[2 * h + 1]},
-                                                                            f32x2{m, m} * f32x2{tb[2 * h], tb[2 * h + 1]}));
+        const f32x2 r = f32x2{m, m} * f32x2{acc[2 * h], acc[2 * h + 1]};
         w[2 * h] = r.x; w[2 * h + 1] = r.y;
       }
       // pin the row here in the asm order: its first DPP read (as row y+1 of the next depthwise
@@ -258,42 +279,53 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     f32x4 wc[3];
     bf16x8 xf[KS];
     load_x(xf, 0);
-    float2 st_c = sSt[px];
+    float2 st_c = float2{0.f, 1.f};
     f32x4 acc_c = gemm1(xf);
     load_x(xf, 1);
-    float2 st_n = sSt[16 + px];
+    float2 st_n = float2{0.f, 1.f};
     f32x4 acc_n = gemm1(xf);
     load_x(xf, 2);
     epi(acc_c, 0, st_c, wc[0]);
     acc_c = acc_n; st_c = st_n;
     acc_n = gemm1(xf);
-    st_n = sSt[32 + px];
+    st_n = float2{0.f, 1.f};
     load_x(xf, 3);
     epi(acc_c, 1, st_c, wc[1]);
     acc_c = acc_n; st_c = st_n;
+    // 3-row trips. The last trip's GEMM1 of row R + 2 and its reads of rows R + 2, R + 3 (past the
+    // X tile, inside the block's LDS tables) are computed and dropped: no branches in the body
+#if F2_WALK_UNROLL
+#pragma unroll
+#else
 #pragma nounroll
+#endif
     for (int hb = 2; hb < R + 2; hb += 3) {
       static_for<3>([&](auto J) {
         constexpr int j = decltype(J)::value;
         constexpr int s2 = (2 + j) % 3, s0 = (s2 + 1) % 3, s1 = (s2 + 2) % 3;   // rows y+1, y-1, y
         const int hr = hb + j;
-        if (hr + 1 < R + 2) {
-          acc_n = gemm1(xf);                           // row hr+1
-          st_n = sSt[(hr + 1) * 16 + px];
-        }
-        if (hr + 2 < R + 2) load_x(xf, hr + 2);
+        acc_n = gemm1(xf);                             // row hr+1
+        st_n = float2{0.f, 1.f};
+        load_x(xf, hr + 2);
         epi(acc_c, hr, st_c, wc[s2]);
         acc_c = acc_n; st_c = st_n;
-        float d[4] = {db[0], db[1], db[2], db[3]};
-        // tap-major, channel-minor: 4 independent accumulation chains in flight
+        float d[4];
+        // tap-major, channel-minor: 4 independent accumulation chains in flight; the first row's
+        // centre tap starts the chains from the bias (no copies of it)
         auto row = [&](const f32x4& w, int t0) {
+          if (t0 != 0) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) fmac_shr1(d[q], w[q], wt[t0][q]);
+            for (int q = 0; q < 4; ++q) fmac_shr1(d[q], w[q], wt[t0][q]);
+          }
 #pragma unroll
           for (int h = 0; h < 2; ++h) {   // centre tap: packed pairs
             const f32x2 r = __builtin_elementwise_fma(f32x2{wt[t0 + 1][2 * h], wt[t0 + 1][2 * h + 1]}, f32x2{w[2 * h], w[2 * h + 1]},
-                                                      f32x2{d[2 * h], d[2 * h + 1]});
+                                                      t0 == 0 ? f32x2{db[2 * h], db[2 * h + 1]} : f32x2{d[2 * h], d[2 * h + 1]});
             d[2 * h] = r.x; d[2 * h + 1] = r.y;
+          }
+          if (t0 == 0) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) fmac_shr1(d[q], w[q], wt[t0][q]);
           }
 #pragma unroll
           for (int q = 0; q < 4; ++q) fmac_shl1(d[q], w[q], wt[t0 + 2][q]);
@@ -471,7 +503,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         }
       }
     }
-    // ---- epilogue: (acc + b2) * scale2 + x (raw input tile), 4 consecutive channels per lane ----
+    // ---- epilogue: (acc + b2) * scale2 + x (re-read from L2), 4 consecutive channels per lane ----
     bf16* out = reinterpret_cast<bf16*>(a.out);
 #pragma unroll
     for (int o = 0; o < NOT; ++o) {
@@ -480,10 +512,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       const int ch = ot * 16 + grp * 4;
       const f32x4 b = ld_f4(a.b2 ? a.b2 + ch : zf);
       const f32x4 sc = a.scale2 ? ld_f4(a.scale2 + ch) : f32x4{1.f, 1.f, 1.f, 1.f};
+      const bf16* xres = reinterpret_cast<const bf16*>(a.x);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const bf16x4 xr = *reinterpret_cast<const bf16x4*>(sX + ((r + 1) * 16 + px) * L::XP + ch * 2);
         const int y = y0 + r;
+        // residual = the block input (res == x, ldx == C: fused2_ok), clamped address off-image
+        const bool rin = out_lane && y < a.H;
+        const bf16x4 xr = *reinterpret_cast<const bf16x4*>(
+            xres + (rin ? (((int64_t)img * a.H + y) * a.W + xg) * a.ldx + ch : (int64_t)0));
         bf16x4 ov;
 #pragma unroll
         for (int q = 0; q < 4; ++q) ov[q] = (bf16)fmaf(acc2[o][r][q] + b[q], sc[q], (float)xr[q]);
@@ -564,6 +600,8 @@ void launch_fused2(const FusedArgs& a, hipStream_t st) {
         case 2: f2_launch<F_GATE, 64, 12, 4, 64, 2>(a, st); break;
         case 3: f2_launch<F_GATE, 64, 9, 4, 64, 3, 4>(a, st); break;   // 4 tiles per block, next tile prefetched
         case 6: f2_launch<F_GATE, 64, 6, 4, 64, 3, 1, true>(a, st); break;   // tables from L2 (spills: 924 us)
+        case 7: f2_launch<F_GATE, 64, 6, 5, 160, 2>(a, st); break;   // 5 waves, one pass (10 units: 2 per wave)
+        case 8: f2_launch<F_GATE, 64, 6, 5, 160, 3>(a, st); break;
         case 4: f2_launch<F_GATE, 64, 6, 4, 64, 4>(a, st); break;
         case 5: f2_launch<F_GATE, 64, 3, 4, 64, 4>(a, st); break;
         default: f2_launch<F_GATE, 64, 6, 4, 64, 3>(a, st);           // 46 KB: 3 blocks per CU

@@ -249,20 +249,6 @@ bool dwgemm_ok(const DwGemmArgs& g);
 int64_t dwgemm_blocks(const DwGemmArgs& g);
 void launch_dwgemm(const DwGemmArgs& g, hipStream_t st);
 
-struct PdwArgs {                   // pdw.hip: G = gelu(dw(H1)) * dw(H2), H = LN(x) W_in^T, bf16, C = 256
-  const void* x; int64_t ldx; int offx;   // [nimg][H][W][ldx], channels [offx, offx + C)
-  int C, nimg, H, W;
-  const void* w1; int N1;          // [N1][C] LN-folded W_in' rows (H1 = [0, N1/2), H2 = [N1/2, N1))
-  int ln;                          // LayerNorm prologue
-  const float* ln_s; const float* ln_tb;  // [N1] rowsum(W_in') (null: BiasFree), W_in b_ln + b_in (null: 0)
-  const void* dww16; const float* dwb;    // [9][N1] bf16 taps, [N1] fp32 bias or null
-  void* out; int64_t ldo; int offo;       // G [nimg][H][W][ldo], N1 / 2 channels at offo
-  int64_t pad_off;                        // byte offset (from out) of 512 writable pad bytes after G
-  int split;                              // schedule variant (turtle_set_option "pdw_split")
-};
-bool pdw_ok(const PdwArgs& g);
-int64_t pdw_blocks(const PdwArgs& g);
-void launch_pdw(const PdwArgs& g, hipStream_t st);
 
 struct FfnArgs {                   // ffn.hip: out = x + g2 * (W2 gelu(LN-folded W1 x) + b2), bf16, C in {64, 128}
   const void* x; void* out;        // [M][C] pixel-major; out may alias x

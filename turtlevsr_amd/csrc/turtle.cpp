@@ -331,8 +331,6 @@ struct TurtleHandle {
   int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
-  bool pdw = false;                                   // level-3 GatedFeedForward: LN -> project_in -> dw -> gate in one kernel (pdw.hip); off until it beats pn + dwgemm
-  int pdw_split = 1;                                  // pdw schedule variant (pdw.hip)
   bool split_out = true;                              // split-bf16 weights for reduce_chan_level1 (bf16 builds)
   bool dwgemm_attn = true;                            // channel attention: v's depthwise inside the W_eff GEMM (dwgemm.hip)
   int dwgemm_min_blocks = 384;                        // one 160 KB block per CU: below ~1.5 rounds (latent level) dw + GEMM is faster
@@ -904,23 +902,6 @@ struct Runner {
     a.nimg = nimg; a.H = H; a.W = Wd; a.N = c;
     return dwgemm_blocks(a) >= h->dwgemm_min_blocks;
   }
-  // shape-only (same in the sizing dry run): the level-3 GatedFeedForward as pdw + GEMM
-  bool can_pdw(int c, int hd) const {
-    return ES == 2 && h->pdw && c == 256 && hd % 16 == 0 && hd <= 2048;
-  }
-  void pdw(const GemmW& w1, const DwW& dwp, const T* x, int c, int nimg, int H, int Wd, T* out, int hd) {
-    if (dry()) return;
-    PdwArgs a{};
-    a.x = x; a.ldx = c; a.offx = 0; a.C = c; a.nimg = nimg; a.H = H; a.W = Wd;
-    a.w1 = h->ptr(w1.w); a.N1 = w1.N; a.ln = w1.ln; a.ln_s = h->fptr(w1.s); a.ln_tb = h->fptr(w1.tb);
-    a.dww16 = h->ptr(dwp.w16); a.dwb = h->fptr(dwp.bias); a.out = out; a.ldo = hd; a.offo = 0;
-    a.pad_off = (int64_t)nimg * H * Wd * hd * ES; a.split = h->pdw_split;
-    if (w1.N != 2 * hd || dwp.C != w1.N || !w1.ln || !pdw_ok(a)) TFAIL(TURTLE_EINVAL, "pdw: GatedFeedForward shape not supported");
-    const double px = (double)nimg * H * Wd;
-    tag("pdw nimg=%d H=%d W=%d C=%d N1=%d", nimg, H, Wd, c, w1.N);
-    launch(TURTLE_K_FUSED, ES * px * (c + hd) + ES * (double)w1.N * c, 2.0 * px * c * w1.N + 18.0 * px * w1.N,
-           [&] { launch_pdw(a, st); });
-  }
   // shape-only: the GatedFeedForward hidden map channel-blocked between the pn GEMM and dwgemm
   bool can_dwgemm_cb(int c, int hd, int nimg, int H, int Wd) const {
     if (ES != 2 || !h->dwgemm || !h->dwgemm_cb || !h->gemm_pn || hd % 32 || hd > 2048) return false;
@@ -1076,12 +1057,6 @@ struct Runner {
       } else if (can_pwdw(c, 2 * hd, true)) {
         T* t2 = buf(P * hd);
         pwdw(bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, 1, t2, hd, 0);
-        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
-      } else if (can_pdw(c, hd)) {
-        // project_in -> depthwise -> gate in one kernel (the 2 hd-channel hidden map stays on chip),
-        // then project_out + residual as a GEMM over the gated map
-        T* t2 = buf(P * hd + 256);                 // + the kernel's 512-byte store pad
-        pdw(bw.f_in, bw.f_dw, x, c, B, H, Wd, t2, hd);
         gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
       } else if (can_dwgemm_cb(c, hd, B, H, Wd)) {
         // project_in stores the hidden map channel-blocked ([2 hd / 16][P][16]): each dwgemm K step
@@ -1559,8 +1534,6 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "dwgemm") h->dwgemm = value != 0;
     else if (n == "dwgemm_attn") h->dwgemm_attn = value != 0;
     else if (n == "dwgemm_cb") h->dwgemm_cb = value != 0;
-    else if (n == "pdw") h->pdw = value != 0;
-    else if (n == "pdw_split") h->pdw_split = value;
     else if (n == "split_out") {                 // changes the packed weights: re-pack when loaded
       h->split_out = value != 0;
       if (h->loaded) pack_all(h);
