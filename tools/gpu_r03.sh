@@ -71,6 +71,9 @@ for s in $STEPS; do
     f2old)
       timeout -k 10 300 ./tools/f2bench_old ${F2B_REPS:-20} "${F2B_ONLY:-}" ${F2B_V:-0} > $OUT/f2bench_old.log 2>&1
       rc=$?; echo "f2old rc=$rc"; cat $OUT/f2bench_old.log; [ $rc -ne 0 ] && exit $rc ;;
+    tprof)
+      timeout -k 10 400 python -u tools/train_prof.py > $OUT/train_prof.txt 2>&1
+      rc=$?; echo "tprof rc=$rc"; tail -40 $OUT/train_prof.txt | head -5; [ $rc -ne 0 ] && exit $rc ;;
     iso)
       timeout -k 10 300 python -u tools/bf16_isolate.py > $OUT/iso.log 2>&1
       rc=$?; echo "iso rc=$rc"; cat $OUT/iso.log | grep PSNR; [ $rc -ne 0 ] && exit $rc ;;
