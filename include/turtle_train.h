@@ -19,10 +19,12 @@ extern "C" {
 #endif
 
 /* LayerNorm over channels per pixel (turtle_t1_arch.py:67-112, WithBias_LayerNorm / BiasFree_LayerNorm):
- * x [P][ldx] -> y [P][ldy] (C channels, C % 8 == 0, C <= 2048); w, b [C]; saves mu, rstd [P]. */
+ * x [P][ldx] -> y [P][ldy] (C channels, C % 8 == 0, C <= 2048); w, b [C]; saves mu, rstd [P].
+ * dtype: bits 0-3 = x's type (0 fp32, 1 bf16, 2 fp16); bits 4-7 = 1 + y's type when y differs (only fp32 x
+ * with bf16 / fp16 y: autocast's cast of the fp32 residual stream folded into the LayerNorm). */
 int turtle_train_ln_fwd(const void* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy, float* mu, float* rstd,
                         int64_t P, int C, int biasfree, int dtype, void* stream);
-/* dx [P][lddx]; dw, db [C] accumulated (db unused for BiasFree) */
+/* dx [P][lddx] in x's type, dy in y's type (dtype as ln_fwd); dw, db [C] accumulated (db unused for BiasFree) */
 int turtle_train_ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy,
                         int64_t lddy, void* dx, int64_t lddx, float* dw, float* db, int64_t P, int C, int biasfree, int dtype,
                         void* stream);

@@ -222,6 +222,25 @@ def test_hip_train_ops_match_autograd(dtype):
         torch.testing.assert_close(gw, rw, rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
         if gb:
             torch.testing.assert_close(gb[0], rb[0], rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
+    if dtype == torch.bfloat16:
+        # the fp32 residual stream under bf16 autocast: LayerNorm reads fp32, writes bf16 and returns
+        # an fp32 input gradient (the cast is folded into the kernels)
+        x = (torch.randn(2, 64, 9, 13, device=dev) * 2 + 0.5).contiguous(memory_format=torch.channels_last).requires_grad_()
+        w = (1 + 0.1 * torch.randn(64, device=dev)).requires_grad_()
+        b = (0.1 * torch.randn(64, device=dev)).requires_grad_()
+        gy = torch.randn(2, 64, 9, 13, device=dev).to(dtype)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = HipOps.layer_norm(x, w, b, False)
+        assert y.dtype == torch.bfloat16
+        gx, gw, gb = torch.autograd.grad(y, [x, w, b], gy)
+        assert gx.dtype == torch.float32
+        x2, w2, b2 = (t.detach().requires_grad_() for t in (x, w, b))
+        y2 = AtenOps.layer_norm(x2, w2, b2, False)
+        rx, rw, rb = torch.autograd.grad(y2, [x2, w2, b2], gy.float())
+        torch.testing.assert_close(y.float(), y2, **tol)
+        torch.testing.assert_close(gx, rx, rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(gw, rw, rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
+        torch.testing.assert_close(gb, rb, rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
     x = torch.randn(3, 40, 37, 21, device=dev).to(dtype).requires_grad_()
     w = (0.3 * torch.randn(40, 1, 3, 3, device=dev)).requires_grad_()
     b = (0.1 * torch.randn(40, device=dev)).requires_grad_()
@@ -289,6 +308,37 @@ def test_hip_training_graph_matches_reference_gradients(name):
     torch.cuda.synchronize()
     assert float(loss.detach()) == pytest.approx(float(g["loss"]), rel=1e-4)
     assert _check_grads(net, g, rtol=1e-2, atol=1e-5) == meta["n_params"]
+
+
+@pytest.mark.gpu
+def test_gopro_width_gradients_match_aten_autograd():
+    """GoPro widths (59 M parameters, 64-512 channels), fp32 on the GPU: the loss and every parameter
+    gradient of the graph on the HIP training kernels equal ATen autograd of the same graph (torch
+    ops on the same device) - 2 clips x 2 frames of 128x128 with BPTT through the caches."""
+    import yaml
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "options",
+                           "Turtle_Deblur_Gopro.yml")) as f:
+        opt = yaml.safe_load(f)
+    lq = torch.from_numpy(synthetic_frames((2, 2, 3, 128, 128), 43, name="lq")).cuda()
+    gt = (lq + 0.05 * torch.from_numpy(synthetic_frames((2, 2, 3, 128, 128), 44, name="gt")).cuda()).clamp(0, 1)
+    res = []
+    for ops in (None, AtenOps):
+        net = _net(dict(opt=opt, seed=3), ops, "cuda")
+        tr = Trainer(net, amp=None)
+        loss = tr.loss(lq, gt)
+        (loss + 0 * sum(p.sum() for p in net.parameters())).backward()
+        torch.cuda.synchronize()
+        res.append((float(loss.detach()), {k: p.grad.detach().float().cpu() for k, p in net.named_parameters()}))
+        del net, tr
+    (lh, gh), (la, ga) = res
+    assert lh == pytest.approx(la, rel=1e-4)
+    bad = []
+    for k, r in ga.items():
+        tol = 1e-3 * float(r.abs().max()) + 1e-7
+        err = float((gh[k] - r).abs().max())
+        if err > tol:
+            bad.append((k, err, tol))
+    assert not bad, bad[:10]
 
 
 @pytest.mark.gpu

@@ -74,6 +74,9 @@ for s in $STEPS; do
     tprof)
       timeout -k 10 400 python -u tools/train_prof.py > $OUT/train_prof.txt 2>&1
       rc=$?; echo "tprof rc=$rc"; tail -40 $OUT/train_prof.txt | head -5; [ $rc -ne 0 ] && exit $rc ;;
+    tcopy)
+      timeout -k 10 300 python -u tools/train_copies.py --gpu --res 128 --batch 2 --frames 2 > $OUT/train_copies.txt 2>&1
+      rc=$?; echo "tcopy rc=$rc"; head -30 $OUT/train_copies.txt; [ $rc -ne 0 ] && exit $rc ;;
     iso)
       timeout -k 10 300 python -u tools/bf16_isolate.py > $OUT/iso.log 2>&1
       rc=$?; echo "iso rc=$rc"; cat $OUT/iso.log | grep PSNR; [ $rc -ne 0 ] && exit $rc ;;

@@ -127,6 +127,19 @@ struct GramArgs {
 };
 template <typename T> void launch_gram(const GramArgs& a, hipStream_t st);
 
+// attn.hip gram_dw: the channel-attention Gram with the q / k depthwise 3x3 computed on the fly
+// from the raw qkv map (bf16, one key segment, 64 channels per head): the dw'd q / k never reach HBM
+struct GramDwArgs {
+  const void* in; int64_t ld; int qoff, koff;   // raw q channel h*ch+i at qoff, k at koff
+  const float* w; const float* bias; int Cw;    // taps [9][Cw] fp32 (q channels then k), bias [Cw]; Cw = 2 C
+  int B, heads, ch, H, W;
+  int RB, nstrip, nband;                        // chunk = (strip of 32 columns, band of RB rows): nchunk = nstrip * nband
+  float* part;                                  // [B*heads][nchunk][ch*ch + 2 ch] as gram_kernel
+};
+bool gram_dw_ok(const GramDwArgs& a);
+void gram_dw_geometry(GramDwArgs& a);           // sets RB / nstrip / nband from B, heads, H, W
+void launch_gram_dw(const GramDwArgs& a, hipStream_t st);
+
 struct AttnFinArgs {               // per-row Gram reduction + softmax
   const float* part; int nchunk;
   int B, heads, ch, nseg;

@@ -24,6 +24,8 @@
 // zeroed.
 #include "common.h"
 #include "kernels.h"
+
+#include <type_traits>
 #include "../../include/turtle_train.h"
 
 #include <algorithm>
@@ -32,6 +34,8 @@
 #include <vector>
 
 namespace turtle {
+
+__device__ __attribute__((aligned(64))) uint4 g_zero_tw[2];   // zero line for branch-free operand loads
 
 TURTLE_DEV float gelu_exact(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 TURTLE_DEV float gelu_exact_grad(float x) {   // d/dx x Phi(x) = Phi(x) + x phi(x)
@@ -87,9 +91,9 @@ TURTLE_DEV float group_sum(float v) {
 // ---------------------------------------------------------------------------------------------
 // channel LayerNorm, NHWC: G lanes per pixel, each lane NCH chunks of 8 channels
 // ---------------------------------------------------------------------------------------------
-template <typename T, int G, int NCH>
+template <typename T, typename TY, int G, int NCH>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ w,
-                                                     const float* __restrict__ b, T* __restrict__ y, int64_t ldy,
+                                                     const float* __restrict__ b, TY* __restrict__ y, int64_t ldy,
                                                      float* __restrict__ mu, float* __restrict__ rstd, int64_t P, int C,
                                                      int biasfree) {
   const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -135,10 +139,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, in
 // BiasFree (y = w x r, r of the centred variance): dx = r g - (x - mu) r^3 mean(g x).
 // dw[c] = sum_p dy xhat (BiasFree xhat = x r), db[c] = sum_p dy: per-lane accumulators over the
 // block's pixels -> LDS -> one atomic per channel per block
-template <typename T, int G, int NCH>
+template <typename T, typename TY, int G, int NCH>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ w,
                                                      const float* __restrict__ mu, const float* __restrict__ rstd,
-                                                     const T* __restrict__ dy, int64_t lddy, T* __restrict__ dx, int64_t lddx,
+                                                     const TY* __restrict__ dy, int64_t lddy, T* __restrict__ dx, int64_t lddx,
                                                      float* __restrict__ dw, float* __restrict__ db, int64_t P, int C,
                                                      int biasfree, int ppb) {
   extern __shared__ float sred[];                  // [2][C]
@@ -301,6 +305,106 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x, 
   }
 }
 
+// Row-sweeping depthwise weight gradient (the forward's dw_rows geometry, spatial.hip): a block
+// owns a (32-column strip) x (64 channels) x (band of RB rows) box of one image, thread =
+// (column, 8-channel vector); walking down the band it keeps the 3 x 3 x-neighbourhood of its
+// column as a rolling window of three rows (raw, one new row loaded ahead of the math) and
+// accumulates dw9[t] += dy * x[p + off_t], db += dy. Column sums by cross-lane shuffles, the 4
+// waves meet in LDS, one global atomic per (tap, channel) per block.
+template <typename T>
+struct Raw8 {                                   // 8 consecutive elements, raw
+  uint4 q[sizeof(T) / 2];
+  TURTLE_DEV void load(const void* p) {
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 2); ++i) q[i] = reinterpret_cast<const uint4*>(p)[i];
+  }
+  TURTLE_DEV void unpack(float (&v)[8]) const { ld8f(reinterpret_cast<const T*>(q), v); }
+};
+constexpr int TW_SX = 32, TW_CV = 8;
+template <typename T>
+__global__ __launch_bounds__(256) void dw_wgrad_rows_kernel(const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy,
+                                                            int64_t lddy, float* __restrict__ dw9, float* __restrict__ db,
+                                                            int C, int H, int W, int RB, int nstrip, int nchunk, int nband) {
+  __shared__ float sred[10][TW_CV * 8];
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int i = tid; i < 10 * TW_CV * 8; i += 256) (&sred[0][0])[i] = 0.f;
+  int t = blockIdx.x;
+  const int band = t % nband;
+  t /= nband;
+  const int strip = t % nstrip;
+  t /= nstrip;
+  const int chunk = t % nchunk;
+  const int64_t img = t / nchunk;
+  const int cvl = tid % TW_CV, xs = tid / TW_CV;
+  const int CV = C / 8;
+  const int xcol = strip * TW_SX + xs, cv = chunk * TW_CV + cvl;
+  const bool live = xcol < W && cv < CV;
+  const int xc = min(xcol, W - 1), c0 = min(cv, CV - 1) * 8;
+  const int y0 = band * RB, y1 = min(H, y0 + RB);
+  const T* xin = x + img * H * W * ldx + c0;
+  const T* gin = dy + img * H * W * lddy + c0;
+  const bool okl = xc > 0, okr = xc + 1 < W;
+  auto load_row = [&](int y, Raw8<T> (&r)[3]) {
+    const bool oky = y >= 0 && y < H;
+    const T* p = xin + ((int64_t)(oky ? y : 0) * W + xc) * ldx;
+    r[0].load(oky && okl ? reinterpret_cast<const void*>(p - ldx) : g_zero_tw);
+    r[1].load(oky ? reinterpret_cast<const void*>(p) : g_zero_tw);
+    r[2].load(oky && okr ? reinterpret_cast<const void*>(p + ldx) : g_zero_tw);
+  };
+  float a[10][8];
+#pragma unroll
+  for (int k = 0; k < 10; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[k][e] = 0.f;
+  Raw8<T> w0[3], w1[3], w2[3], nx[3], gr;
+  load_row(y0 - 1, w0);
+  load_row(y0, w1);
+  load_row(y0 + 1, w2);
+  for (int y = y0; y < y1; ++y) {
+    if (y + 1 < y1) load_row(y + 2, nx);
+    gr.load(live ? reinterpret_cast<const void*>(gin + ((int64_t)y * W + xc) * lddy) : g_zero_tw);
+    float g[8];
+    gr.unpack(g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[9][e] += g[e];
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const Raw8<T>& q = tap < 3 ? w0[tap] : tap < 6 ? w1[tap - 3] : w2[tap - 6];
+      float v[8];
+      q.unpack(v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a[tap][e] = fmaf(g[e], v[e], a[tap][e]);
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { w0[k] = w1[k]; w1[k] = w2[k]; w2[k] = nx[k]; }
+  }
+  // sum over the 8 columns of a wave (lane bits 3..5), then over the 4 waves in LDS
+#pragma unroll
+  for (int k = 0; k < 10; ++k)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = a[k][e];
+      v += __shfl_xor(v, 8, 64);
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      a[k][e] = v;
+    }
+  __syncthreads();
+  if (lane < TW_CV) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(&sred[k][lane * 8 + e], a[k][e]);
+  }
+  __syncthreads();
+  for (int i = tid; i < 10 * TW_CV * 8; i += 256) {
+    const int k = i / (TW_CV * 8), j = i - k * TW_CV * 8, c = chunk * TW_CV * 8 + j;
+    if (c >= C) continue;
+    if (k < 9) atomicAdd(&dw9[k * C + c], sred[k][j]);
+    else if (db) atomicAdd(&db[c], sred[9][j]);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // GELU gate, NHWC: x [P][ldx] (x1 = channels [0, h), x2 = [h, 2h)) -> y [P][ldy] (h channels)
 // ---------------------------------------------------------------------------------------------
@@ -407,19 +511,28 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
   const int srow = tid >> 2, sch = 2 * (tid & 3);
   // transposed reads: lane group g = lane >> 4, row q = (lane >> 2) & 3, column quad pq = lane & 3
   const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
-  for (int64_t pb = p0; pb < p1; pb += RG_BP) {
+  // the next stage's operands are loaded into registers while this stage's MFMAs run; loads are
+  // unconditional (a zero line past the map / the tile), so they issue back to back
+  uint4 va[2], vb[2];
+  auto fetch = [&](int64_t pb) {
     const int64_t p = pb + srow;
     const bool live = p < p1;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int cA = n0 + 8 * (sch + u), cB = k0 + 8 * (sch + u);
-      uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
-      if (live && cA < N) va = *reinterpret_cast<const uint4*>(A + (pbase + p) * lda + cA);
-      if (live && cB < K) vb = *reinterpret_cast<const uint4*>(B + (pbase + p) * ldb + cB);
-      *reinterpret_cast<uint4*>(sA + srow * RG_PITCH + 16 * (sch + u)) = va;
-      *reinterpret_cast<uint4*>(sB + srow * RG_PITCH + 16 * (sch + u)) = vb;
+      va[u] = *reinterpret_cast<const uint4*>(live && cA < N ? reinterpret_cast<const void*>(A + (pbase + p) * lda + cA) : g_zero_tw);
+      vb[u] = *reinterpret_cast<const uint4*>(live && cB < K ? reinterpret_cast<const void*>(B + (pbase + p) * ldb + cB) : g_zero_tw);
+    }
+  };
+  if (p0 < p1) fetch(p0);
+  for (int64_t pb = p0; pb < p1; pb += RG_BP) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      *reinterpret_cast<uint4*>(sA + srow * RG_PITCH + 16 * (sch + u)) = va[u];
+      *reinterpret_cast<uint4*>(sB + srow * RG_PITCH + 16 * (sch + u)) = vb[u];
     }
     __syncthreads();
+    if (pb + RG_BP < p1) fetch(pb + RG_BP);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {               // 32 pixels per MFMA K step
       bf16x8v af[2], bfr[2];
@@ -505,31 +618,35 @@ __global__ __launch_bounds__(256) void rgemm_reduce_kernel(const float* __restri
 // ---------------------------------------------------------------------------------------------
 // host launchers
 // ---------------------------------------------------------------------------------------------
-template <typename T>
+template <typename T, typename TY = T>
 int ln_fwd(const void* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy, float* mu, float* rstd, int64_t P,
            int C, int biasfree, hipStream_t st) {
   const int G = ln_group(C), nch = (C / 8 + G - 1) / G;
   const int64_t blocks = (P * G + 255) / 256;
 #define LNF(GG, NN)                                                                                                  \
   if (G == GG && nch <= NN) {                                                                                        \
-    hipLaunchKernelGGL((ln_fwd_kernel<T, GG, NN>), dim3((unsigned)blocks), dim3(256), 0, st, (const T*)x, ldx, w, b, \
-                       (T*)y, ldy, mu, rstd, P, C, biasfree);                                                        \
+    hipLaunchKernelGGL((ln_fwd_kernel<T, TY, GG, NN>), dim3((unsigned)blocks), dim3(256), 0, st, (const T*)x, ldx, w, b, \
+                       (TY*)y, ldy, mu, rstd, P, C, biasfree);                                                        \
     return 0;                                                                                                        \
   }
   LNF(1, 1) LNF(2, 1) LNF(4, 1) LNF(8, 1) LNF(16, 1) LNF(32, 1) LNF(64, 1) LNF(64, 2) LNF(64, 4)
 #undef LNF
   return -1;
 }
-template <typename T>
+template <typename T, typename TY = T>
 int ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy, int64_t lddy, void* dx,
            int64_t lddx, float* dw, float* db, int64_t P, int C, int biasfree, hipStream_t st) {
   const int G = ln_group(C), nch = (C / 8 + G - 1) / G;
-  const int64_t ppb = 256;                          // pixels per block
+  // ~512 blocks whatever P is (a fixed 256 pixels per block left a 32 x 32 x 8 latent map on 32
+  // blocks); pixels per block a multiple of the block's pixel slots
+  const int64_t nslot = 256 / G;
+  int64_t ppb = std::max<int64_t>(nslot, (P + 511) / 512);
+  ppb = (ppb + nslot - 1) / nslot * nslot;
   const int64_t blocks = (P + ppb - 1) / ppb;
 #define LNB(GG, NN)                                                                                                       \
   if (G == GG && nch <= NN) {                                                                                             \
-    hipLaunchKernelGGL((ln_bwd_kernel<T, GG, NN>), dim3((unsigned)blocks), dim3(256), 2 * C * sizeof(float), st, (const T*)x, \
-                       ldx, w, mu, rstd, (const T*)dy, lddy, (T*)dx, lddx, dw, db, P, C, biasfree, (int)ppb);                \
+    hipLaunchKernelGGL((ln_bwd_kernel<T, TY, GG, NN>), dim3((unsigned)blocks), dim3(256), 2 * C * sizeof(float), st, (const T*)x, \
+                       ldx, w, mu, rstd, (const TY*)dy, lddy, (T*)dx, lddx, dw, db, P, C, biasfree, (int)ppb);                \
     return 0;                                                                                                             \
   }
   LNB(1, 1) LNB(2, 1) LNB(4, 1) LNB(8, 1) LNB(16, 1) LNB(32, 1) LNB(64, 1) LNB(64, 2) LNB(64, 4)
@@ -539,6 +656,17 @@ int ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const fl
 template <typename T>
 int dw_fwd(const void* x, int64_t ldx, const float* w9, const float* b, void* y, int64_t ldy, int64_t N, int C, int H, int W,
            int flip, hipStream_t st) {
+  if constexpr (!std::is_same<T, f16>::value) {
+    if (!flip && N <= INT32_MAX) {
+      // the inference path's row-sweeping kernel (spatial.hip: each input byte leaves HBM about
+      // once, rolling 3-row register window) instead of the per-pixel 9-load gather
+      DwArgs a{};
+      a.in = x; a.ldi = ldx; a.offi = 0; a.out = y; a.ldo = ldy; a.offo = 0; a.w = w9; a.bias = b;
+      a.nimg = (int)N; a.H = H; a.W = W; a.C = C; a.mode = DW_PLAIN; a.tok_ws = 0; a.rows = 1;
+      launch_dw<T>(a, st);
+      return 0;
+    }
+  }
   const int64_t tot = N * H * W * (C / 8);
   hipLaunchKernelGGL(dw_fwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, ldx, w9, b, (T*)y,
                      ldy, N, C, H, W, flip);
@@ -547,6 +675,16 @@ int dw_fwd(const void* x, int64_t ldx, const float* w9, const float* b, void* y,
 template <typename T>
 int dw_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* dw9, float* db, int64_t N, int C, int H, int W,
              hipStream_t st) {
+  if (N <= INT32_MAX) {
+    const int nstrip = (W + TW_SX - 1) / TW_SX, nchunk = (C / 8 + TW_CV - 1) / TW_CV;
+    int RB = 32;
+    auto nblk = [&](int rb) { return N * nchunk * nstrip * ((H + rb - 1) / rb); };
+    while (RB > 4 && nblk(RB) < 2048) RB /= 2;
+    const int nband = (H + RB - 1) / RB;
+    hipLaunchKernelGGL(dw_wgrad_rows_kernel<T>, dim3((unsigned)nblk(RB)), dim3(256), 0, st, (const T*)x, ldx, (const T*)dy, lddy,
+                       dw9, db, C, H, W, RB, nstrip, nchunk, nband);
+    return 0;
+  }
   const int64_t P = N * H * W;
   const int nsl = (C / 8 + DWG_CPB - 1) / DWG_CPB;
   const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 1024 / nsl), std::max<int64_t>(1, P / 64));
@@ -599,7 +737,8 @@ static int64_t rgemm_splits(int64_t P, int N, int K, int64_t img_px) {
   const int64_t plen = img_px > 0 ? img_px : P;
   const int64_t nimg = img_px > 0 ? P / img_px : 1;
   const int64_t tiles = ((N + RG_BN - 1) / RG_BN) * ((K + RG_BK - 1) / RG_BK) * nimg;
-  return std::max<int64_t>(1, std::min<int64_t>((1024 + tiles - 1) / tiles, (plen + 511) / 512));
+  // ~512 blocks and >= 1024 pixels (16 stages) per block: fewer fp32 partials for the reduce
+  return std::max<int64_t>(1, std::min<int64_t>((512 + tiles - 1) / tiles, (plen + 1023) / 1024));
 }
 
 }  // namespace turtle
@@ -629,20 +768,41 @@ extern "C" {
 
 int turtle_train_ln_fwd(const void* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy, float* mu, float* rstd,
                         int64_t P, int C, int biasfree, int dtype, void* stream) {
-  if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !w || !mu || !rstd || P <= 0 || C <= 0 || C % 8 || C > 2048 ||
+  // dtype: x's type in bits 0-3; bits 4-7 = 1 + y's type when it differs (fp32 residual stream in,
+  // autocast bf16 / fp16 out: the cast folded into the LayerNorm)
+  const int xdt = dtype & 15, ydt = (dtype >> 4) ? (dtype >> 4) - 1 : xdt;
+  if (!rows_ok(x, ldx, xdt) || !rows_ok(y, ldy, ydt) || !w || !mu || !rstd || P <= 0 || C <= 0 || C % 8 || C > 2048 ||
       ldx < C || ldy < C || (!biasfree && !b))
     return -1;
-  TT_DISPATCH(dtype, ln_fwd, x, ldx, w, b, y, ldy, mu, rstd, P, C, biasfree, (hipStream_t)stream);
+  if (xdt != ydt) {
+    int rc;
+    if (xdt == 0 && ydt == 1) rc = ln_fwd<float, bf16>(x, ldx, w, b, y, ldy, mu, rstd, P, C, biasfree, (hipStream_t)stream);
+    else if (xdt == 0 && ydt == 2) rc = ln_fwd<float, f16>(x, ldx, w, b, y, ldy, mu, rstd, P, C, biasfree, (hipStream_t)stream);
+    else return -1;
+    return rc ? rc : (int)hipGetLastError();
+  }
+  TT_DISPATCH(xdt, ln_fwd, x, ldx, w, b, y, ldy, mu, rstd, P, C, biasfree, (hipStream_t)stream);
 }
 
 int turtle_train_ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy,
                         int64_t lddy, void* dx, int64_t lddx, float* dw, float* db, int64_t P, int C, int biasfree, int dtype,
                         void* stream) {
-  if (!rows_ok(x, ldx, dtype) || !rows_ok(dy, lddy, dtype) || !rows_ok(dx, lddx, dtype) || !w || !mu || !rstd || !dw ||
+  // dtype as turtle_train_ln_fwd: x and dx in x's type, dy in y's type
+  const int xdt = dtype & 15, ydt = (dtype >> 4) ? (dtype >> 4) - 1 : xdt;
+  if (!rows_ok(x, ldx, xdt) || !rows_ok(dy, lddy, ydt) || !rows_ok(dx, lddx, xdt) || !w || !mu || !rstd || !dw ||
       P <= 0 || C <= 0 || C % 8 || C > 2048)
     return -1;
-  TT_DISPATCH(dtype, ln_bwd, x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dw, biasfree ? nullptr : db, P, C, biasfree,
-              (hipStream_t)stream);
+  float* dbb = biasfree ? nullptr : db;
+  if (xdt != ydt) {
+    int rc;
+    if (xdt == 0 && ydt == 1)
+      rc = ln_bwd<float, bf16>(x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dw, dbb, P, C, biasfree, (hipStream_t)stream);
+    else if (xdt == 0 && ydt == 2)
+      rc = ln_bwd<float, f16>(x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dw, dbb, P, C, biasfree, (hipStream_t)stream);
+    else return -1;
+    return rc ? rc : (int)hipGetLastError();
+  }
+  TT_DISPATCH(xdt, ln_bwd, x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dw, dbb, P, C, biasfree, (hipStream_t)stream);
 }
 
 int turtle_train_dw3x3_fwd(const void* x, int64_t ldx, const float* w9, const float* b, void* y, int64_t ldy, int64_t N, int C,

@@ -328,6 +328,7 @@ struct TurtleHandle {
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
+  bool gram_dw = true;                                // level-3 channel attention: q / k depthwise inside the Gram kernel (attn.hip)
   int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
@@ -946,17 +947,32 @@ struct Runner {
   struct Seg { const void* base; int64_t ld; int off; int hstride; int mul, add; int norm; int64_t col; int colh; };
 
   // channel attention core: Gram over (q, key segments), softmax, W_eff, then out = x + W_eff [v srcs]
+  // the q / k depthwise inside the Gram kernel (attn.hip gram_dw): bf16, one key segment, 64
+  // channels per head (shape-only, same in the sizing dry run)
+  bool can_gram_dw(int c, int heads) const { return ES == 2 && h->gram_dw && heads > 0 && c == 64 * heads; }
+
+  // qkdw: q, k are the RAW projections (q at qoff, k at segs[0].off of the same map) and their
+  // depthwise runs inside the Gram (gram_dw); otherwise q / segs are already depthwise'd
   void chan_attn(const BlockW& bw, const Blk& b, const T* q, int64_t ldq, int qoff, const std::vector<Seg>& segs,
                  const SrcList& vsrc, int HW, int Wimg, T* x, float* kinv, int cur_seg,
-                 const DwW* vdw = nullptr, const T* vraw = nullptr, int64_t ldv = 0, int offv = 0) {
+                 const DwW* vdw = nullptr, const T* vraw = nullptr, int64_t ldv = 0, int offv = 0, const DwW* qkdw = nullptr) {
     const int c = b.dim, ch = c / b.heads, nseg = (int)segs.size(), ncol = nseg * ch;
     if (ncol > 512 || nseg > TURTLE_MAX_SEG) TFAIL(TURTLE_EINVAL, "channel attention: more than 512 key columns");
-    // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each, whole
-    // 128-pixel steps of the bf16 Gram
-    int nchunk = std::max(1, std::min((HW + 255) / 256, std::max(1, h->gram_blocks / (B * b.heads))));
-    int chunk = (HW + nchunk - 1) / nchunk;
-    chunk = (chunk + 127) / 128 * 128;
-    nchunk = (HW + chunk - 1) / chunk;
+    GramDwArgs gd{};
+    int nchunk, chunk = 0;
+    if (qkdw) {
+      if (nseg != 1 || ch != 64) TFAIL(TURTLE_EINVAL, "channel attention: gram_dw needs one 64-channel key segment");
+      gd.B = B; gd.heads = b.heads; gd.ch = ch; gd.H = HW / Wimg; gd.W = Wimg;
+      gram_dw_geometry(gd);
+      nchunk = gd.nstrip * gd.nband;
+    } else {
+      // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each, whole
+      // 128-pixel steps of the bf16 Gram
+      nchunk = std::max(1, std::min((HW + 255) / 256, std::max(1, h->gram_blocks / (B * b.heads))));
+      chunk = (HW + nchunk - 1) / nchunk;
+      chunk = (chunk + 127) / 128 * 128;
+      nchunk = (HW + chunk - 1) / chunk;
+    }
     const int stride = ch * ncol + ch + ncol;
     float* part = fbuf((int64_t)B * b.heads * nchunk * stride);
     float* red = fbuf((int64_t)B * b.heads * stride);
@@ -964,6 +980,14 @@ struct Runner {
     T* weff = buf((int64_t)B * c * vsrc.Ktot);
     if (dry()) return;
     if (ch > 128) TFAIL(TURTLE_EINVAL, "channel attention: more than 128 channels per head");
+    if (qkdw) {
+      gd.in = q; gd.ld = ldq; gd.qoff = qoff; gd.koff = segs[0].off;
+      gd.w = h->fptr(qkdw->w); gd.bias = h->fptr(qkdw->bias); gd.Cw = qkdw->C; gd.part = part;
+      if (!gram_dw_ok(gd) || segs[0].base != q || segs[0].ld != ldq) TFAIL(TURTLE_EINVAL, "channel attention: gram_dw not eligible");
+      tag("gram_dw B=%d HW=%d c=%d heads=%d nchunk=%d", B, HW, c, b.heads, nchunk);
+      launch(TURTLE_K_ATTN, ES * (double)B * HW * 2 * c, 2.0 * B * b.heads * ch * ch * (double)HW + 36.0 * B * HW * c,
+             [&] { launch_gram_dw(gd, st); });
+    }
     GramArgs g{};
     g.q = q; g.ldq = ldq; g.qoff = qoff; g.nseg = nseg;
     unsigned mask = 0;
@@ -972,9 +996,11 @@ struct Runner {
       if (segs[s].norm) mask |= 1u << s;
     }
     g.B = B; g.heads = b.heads; g.ch = ch; g.HW = HW; g.nchunk = nchunk; g.chunk = chunk; g.part = part;
-    tag("gram B=%d HW=%d c=%d heads=%d nseg=%d nchunk=%d", B, HW, c, b.heads, nseg, nchunk);
-    launch(TURTLE_K_ATTN, ES * (double)B * HW * c * (1 + nseg), 2.0 * B * b.heads * ch * ncol * (double)HW,
-           [&] { launch_gram<T>(g, st); });
+    if (!qkdw) {
+      tag("gram B=%d HW=%d c=%d heads=%d nseg=%d nchunk=%d", B, HW, c, b.heads, nseg, nchunk);
+      launch(TURTLE_K_ATTN, ES * (double)B * HW * c * (1 + nseg), 2.0 * B * b.heads * ch * ncol * (double)HW,
+             [&] { launch_gram<T>(g, st); });
+    }
     AttnFinArgs f{};
     f.part = part; f.nchunk = nchunk; f.B = B; f.heads = b.heads; f.ch = ch; f.nseg = nseg;
     f.norm_mask = mask; f.tau = h->fptr(bw.tau); f.kinv = kinv; f.cur_seg = cur_seg; f.red = red; f.attn = attn;
@@ -1031,9 +1057,25 @@ struct Runner {
         // qkv GEMM, depthwise of q,k only; v's depthwise runs inside the W_eff GEMM (dwgemm.hip)
         T* t1 = buf(P * 3 * c);
         gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
-        dw(bw.a_dw_qk, t1, 3 * c, 0, t2, 3 * c, 0, B, H, Wd, DW_PLAIN);
-        chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t1, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1, &bw.a_dw_v, t1, 3 * c,
-                  2 * c);
+        if (can_gram_dw(c, b.heads)) {
+          // q, k's depthwise inside the Gram kernel: the dw'd q / k map is never stored
+          std::vector<Seg> rsegs{{t1, 3 * c, c, ch, 1, 0, 1, 0, ch}};
+          chan_attn(bw, b, t1, 3 * c, 0, rsegs, src1(t1, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1, &bw.a_dw_v, t1, 3 * c,
+                    2 * c, &bw.a_dw_qk);
+        } else {
+          dw(bw.a_dw_qk, t1, 3 * c, 0, t2, 3 * c, 0, B, H, Wd, DW_PLAIN);
+          chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t1, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1, &bw.a_dw_v, t1, 3 * c,
+                    2 * c);
+        }
+      } else if (!can_fuse(c, F_DWONLY, 3 * c, 0) && !can_fused2_wide(c, F_DWONLY, 3 * c, 0) && !can_pwdw(c, 3 * c, false) &&
+                 can_gram_dw(c, b.heads)) {
+        // (latent level) qkv GEMM, v's depthwise alone, q / k's inside the Gram kernel
+        T* t1 = buf(P * 3 * c);
+        gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
+        dw(bw.a_dw_v, t1, 3 * c, 2 * c, t2, 3 * c, 2 * c, B, H, Wd, DW_PLAIN);
+        std::vector<Seg> rsegs{{t1, 3 * c, c, ch, 1, 0, 1, 0, ch}};
+        chan_attn(bw, b, t1, 3 * c, 0, rsegs, src1(t2, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1, nullptr, nullptr, 0, 0,
+                  &bw.a_dw_qk);
       } else {
         qkv_dw(bw, x, c, t2, B, H, Wd);
         chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t2, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1);

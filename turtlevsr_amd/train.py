@@ -5,10 +5,12 @@ base_model.py:340-365, dist_util.py:15-30) on the GPU:
 
 * ``TurtleTrain`` is the differentiable Turtle_t1 graph over the SAME parameter tree as the
   inference module (633 keys, turtlevsr_amd/params.py), so checkpoints move between training and
-  the HIP inference path unchanged. Its LayerNorms, depthwise 3x3 convolutions and GELU gates run
-  on hand-written HIP kernels with hand-written backward (``train_ops.HipOps``); pointwise 1x1
-  convolutions, the attention contractions and the SAB top-5 selection are torch ops (hipBLASLt /
-  MIOpen on ROCm), differentiated by autograd.
+  the HIP inference path unchanged. On the GPU its LayerNorms, depthwise 3x3 convolutions, GELU
+  gates, pointwise 1x1 convolutions (forward, input and weight gradients) and the channel-attention
+  Gram run on hand-written HIP kernels with hand-written backward (``train_ops.HipOps``,
+  include/turtle_train.h), on channels-last activations; the dense / window 3x3 convolutions
+  (stem, ending, Down/Upsample, SAB q2/k2) and the SAB dense scores / top-5 / A.v are torch ops
+  (MIOpen / hipBLASLt), differentiated by autograd.
 * caches are NOT detached between frames: the loss of frame j back-propagates into frames < j
   through the history state (video_restoration_model.py:85-95);
 * ``Trainer.train_step``: zero_grad -> autocast forward over the T frames -> L1 per frame summed,
@@ -42,6 +44,59 @@ def _l2n(x, dim):
 
 def _conv1(m, x):
     return F.conv2d(x, m.weight, m.bias)
+
+
+class _ChanSplit(torch.autograd.Function):
+    """x[:, a:b] channel slices whose backward concatenates the slice gradients in x's memory
+    format. Plain slicing's backward (slice_backward) builds each slice gradient into a zero-filled
+    NCHW tensor and sums them: three fills, three transposing copies and a re-layout back to
+    channels-last per qkv split on the HIP graph (the largest copy traffic of the training step)."""
+
+    @staticmethod
+    def forward(ctx, x, *sizes):
+        ctx.sizes = sizes
+        ctx.cl = x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
+        outs, a = [], 0
+        for n in sizes:
+            outs.append(x.narrow(1, a, n))
+            a += n
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        parts = []
+        for g, n in zip(grads, ctx.sizes):
+            if g is None:
+                ref = next(t for t in grads if t is not None)
+                shape = list(ref.shape)
+                shape[1] = n
+                g = torch.zeros(shape, dtype=ref.dtype, device=ref.device,
+                                memory_format=torch.channels_last if ctx.cl else torch.contiguous_format)
+            elif ctx.cl:
+                g = g.contiguous(memory_format=torch.channels_last)
+            parts.append(g)
+        out = torch.cat(parts, dim=1)
+        return (out,) + (None,) * len(ctx.sizes)
+
+
+def _split(x, *sizes):
+    return _ChanSplit.apply(x, *sizes)
+
+
+class _ToNCHW(torch.autograd.Function):
+    """x.contiguous() for MIOpen's NCHW convolution path whose gradient goes back in x's own
+    memory format: otherwise the NCHW input gradient of every dense conv (and the loss's NCHW
+    gradient through the ending conv) makes the whole channels-last residual-stream backward NCHW,
+    and each HIP op re-lays it out."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.cl = x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
+        return x.contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.contiguous(memory_format=torch.channels_last) if ctx.cl else g
 
 
 def positional_encoding_2d(c: int, h: int, w: int) -> torch.Tensor:
@@ -93,8 +148,9 @@ class TrainGraph:
         """Dense / window convolutions (stem, ending, Down/Upsample, SAB window convs) through
         F.conv2d on a standard-layout copy: MIOpen's channels-last backward faults on some of
         these shapes (MI355X, ROCm 7.2), its NCHW path does not. Channels-last again afterwards."""
-        y = F.conv2d(x.contiguous(), w, b, stride, padding, 1, groups)
-        return y.contiguous(memory_format=torch.channels_last) if getattr(self._ops(), "channels_last", False) else y
+        cl = getattr(self._ops(), "channels_last", False)
+        y = F.conv2d(_ToNCHW.apply(x) if cl else x.contiguous(), w, b, stride, padding, 1, groups)
+        return y.contiguous(memory_format=torch.channels_last) if cl else y
 
     def _c1(self, m, x):                            # nn.Conv2d(K, N, 1): the op set's GEMM when it has one
         ops = self._ops()
@@ -125,7 +181,7 @@ class TrainGraph:
             # on the op set's kernels: Gram of the raw q, k over HW (per head) divided by the L2
             # norms (== normalising first, 690-693), softmax, then project_out . blockdiag(A) as
             # one per-image weight set applied to v (A v followed by project_out, 697-702)
-            q, k, v = qkv[:, :c], qkv[:, c:2 * c], qkv[:, 2 * c:]
+            q, k, v = _split(qkv, c, c, c)
             ch = c // heads
             G = ops.gram(q, k, heads)                                          # [b, heads, ch, ch]
             nq = q.float().square().sum((2, 3)).sqrt().clamp_min(L2_EPS).view(b, heads, ch, 1)
@@ -134,7 +190,7 @@ class TrainGraph:
             wp = m.project_out.weight.reshape(c, heads, ch)
             weff = torch.einsum("ohi,bhij->bohj", wp, a).reshape(b, c, c)
             return ops.conv1x1(v, weff, m.project_out.bias), None, None
-        q, k, v = qkv.chunk(3, dim=1)
+        q, k, v = _split(qkv, c, c, c)
         q, k, v = _l2n(self._heads(q, heads), -1), _l2n(self._heads(k, heads), -1), self._heads(v, heads)
         if kc is not None and vc is not None:
             k = torch.cat([kc.to(k.dtype), k], dim=2)
@@ -171,7 +227,7 @@ class TrainGraph:
         """StateAlignBlock live forward 548-610 (top-5 394-416, L1 ball 448-464, clipped_softmax 115-132)."""
         b, c, hl, wl = x.shape
         qk = self._dw(m.qk_dwconv, self._c1(m.qk, x))
-        q, k = qk[:, :c], qk[:, c:]
+        q, k = _split(qk, c, c)
         v = self._dw(m.v_dwconv, self._c1(m.v, x))
         g = 2 * c
         k = self._dense(self._c1(m.k2, k), m.k2_dwconv.weight, m.k2_dwconv.bias, ws, 1, g)
@@ -226,7 +282,7 @@ class TrainGraph:
         xs, k_keep, v_keep = sab(m.spatial_aligner, x, ws, ntc, kc, vc)
         t = xs.shape[1]
         kv = self._dw(m.kv_dwconv, self._c1(m.kv, xs.reshape(b * t, c, h, w)))
-        kh, vh = kv[:, :c], kv[:, c:]
+        kh, vh = _split(kv, c, c)
         ch = c // heads
         kh = kh.reshape(b, t, heads, ch, h * w).transpose(1, 2).reshape(b, heads, t * ch, h * w)
         vh = vh.reshape(b, t, heads, ch, h * w).transpose(1, 2).reshape(b, heads, t * ch, h * w)

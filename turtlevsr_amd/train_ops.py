@@ -102,34 +102,40 @@ def _gemm_dt(x: torch.Tensor) -> torch.dtype:
 
 
 class _LayerNorm(torch.autograd.Function):
+    """y = LayerNorm(x) in ``out_dtype``: an fp32 x (the residual stream under autocast, promoted by
+    the fp32 gamma / beta scales as in the reference) is read as fp32 and y written in the autocast
+    dtype by the kernel itself, and the backward writes dx in fp32 - no cast passes either way."""
+
     @staticmethod
-    def forward(ctx, x, w, b, biasfree: bool):
+    def forward(ctx, x, w, b, biasfree: bool, out_dtype):
         x, ldx = rows(x)
         B, Cc, H, W = x.shape
         P = B * H * W
-        y = _empty(B, Cc, H, W, x)
+        y = torch.empty((B, Cc, H, W), dtype=out_dtype, device=x.device, memory_format=CL)
         mu = torch.empty(P, dtype=torch.float32, device=x.device)
         rs = torch.empty_like(mu)
         w32 = w.float().contiguous()
         b32 = None if b is None else b.float().contiguous()
-        _check(lib().turtle_train_ln_fwd(_p(x), ldx, _p(w32), _p(b32), _p(y), Cc, _p(mu), _p(rs), P, Cc, int(biasfree), _dt(x),
+        dt = _dt(x) | ((_dt(y) + 1) << 4 if y.dtype != x.dtype else 0)
+        _check(lib().turtle_train_ln_fwd(_p(x), ldx, _p(w32), _p(b32), _p(y), Cc, _p(mu), _p(rs), P, Cc, int(biasfree), dt,
                                          _stream(x)), "ln_fwd")
         ctx.save_for_backward(x, w32, mu, rs)
-        ctx.biasfree, ctx.has_b, ctx.ldx = biasfree, b is not None, ldx
+        ctx.biasfree, ctx.has_b, ctx.ldx, ctx.ydt = biasfree, b is not None, ldx, y.dtype
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, w32, mu, rs = ctx.saved_tensors
-        dy, lddy = rows(dy.to(x.dtype))
+        dy, lddy = rows(dy.to(ctx.ydt))
         B, Cc, H, W = x.shape
         P = B * H * W
         dx = _empty(B, Cc, H, W, x)
         dw = torch.zeros(Cc, dtype=torch.float32, device=x.device)
         db = torch.zeros(Cc, dtype=torch.float32, device=x.device) if ctx.has_b else None
+        dt = _dt(x) | ((_dt(dy) + 1) << 4 if dy.dtype != x.dtype else 0)
         _check(lib().turtle_train_ln_bwd(_p(x), ctx.ldx, _p(w32), _p(mu), _p(rs), _p(dy), lddy, _p(dx), Cc, _p(dw), _p(db), P, Cc,
-                                         int(ctx.biasfree), _dt(x), _stream(x)), "ln_bwd")
-        return dx, dw, db, None
+                                         int(ctx.biasfree), dt, _stream(x)), "ln_bwd")
+        return dx, dw, db, None, None
 
 
 class _DWConv(torch.autograd.Function):
@@ -152,7 +158,10 @@ class _DWConv(torch.autograd.Function):
         B, Cc, H, W = x.shape
         dx = _empty(B, Cc, H, W, x)
         st = _stream(x)
-        _check(lib().turtle_train_dw3x3_fwd(_p(dy), lddy, _p(w9), None, _p(dx), Cc, B, Cc, H, W, 1, _dt(x), st), "dw_dgrad")
+        # dx = depthwise of dy with the taps flipped (correlation transposed); the flipped table is
+        # passed as a plain forward so the row-sweeping kernel takes it
+        w9f = w9.flip(0).contiguous()
+        _check(lib().turtle_train_dw3x3_fwd(_p(dy), lddy, _p(w9f), None, _p(dx), Cc, B, Cc, H, W, 0, _dt(x), st), "dw_dgrad")
         dw9 = torch.zeros(9, Cc, dtype=torch.float32, device=x.device)
         db = torch.zeros(Cc, dtype=torch.float32, device=x.device) if ctx.has_b else None
         _check(lib().turtle_train_dw3x3_wgrad(_p(x), ctx.ldx, _p(dy), lddy, _p(dw9), _p(db), B, Cc, H, W, _dt(x), st), "dw_wgrad")
@@ -280,6 +289,12 @@ class _Gram(torch.autograd.Function):
         return dq, dk, None
 
 
+def _act_dtype(x: torch.Tensor) -> torch.dtype:
+    if torch.is_autocast_enabled("cuda") and x.dtype == torch.float32:
+        return torch.get_autocast_dtype("cuda")
+    return x.dtype
+
+
 def _act(x: torch.Tensor) -> torch.Tensor:
     """Activations enter the kernels in the autocast dtype (bf16 / fp16 under autocast)."""
     if torch.is_autocast_enabled("cuda") and x.dtype == torch.float32:
@@ -294,7 +309,8 @@ class HipOps:
 
     @staticmethod
     def layer_norm(x, w, b, biasfree: bool):
-        return _LayerNorm.apply(_act(x), w, b, biasfree)
+        out = _act_dtype(x)                          # an fp32 x under autocast: cast inside the kernel
+        return _LayerNorm.apply(x, w, b, biasfree, out)
 
     @staticmethod
     def dwconv3x3(x, w, b):
