@@ -1581,6 +1581,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
       if (h->loaded) pack_all(h);
     }
     else if (n == "ffn") h->ffn = value != 0;
+    else if (n == "gram_dw") h->gram_dw = value != 0;
     else if (n == "sab_db") h->sab_db = value != 0;
     else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
