@@ -47,6 +47,9 @@ int turtle_train_gate_bwd(const void* x, int64_t ldx, const void* dy, int64_t ld
 
 /* column sums db[n] += sum_p dy[p][n] (a 1x1 convolution's bias gradient), N % 8 == 0 */
 int turtle_train_colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, int dtype, void* stream);
+/* per-image column sums of squares (the channel-attention L2 norms over HW, turtle_t1_arch.py:690-691):
+ * out[img][n] += sum over the img_px pixels of image img of x[p][n]^2; out fp32 [P / img_px][N], zeroed by the caller */
+int turtle_train_colsumsq(const void* x, int64_t ld, float* out, int64_t P, int N, int64_t img_px, int dtype, void* stream);
 
 /* pointwise GEMM (a 1x1 convolution, nn.Conv2d(K, N, 1) on NHWC rows; also its input gradient with
  * W transposed, and the channel-attention A.v with per-image weights):

@@ -37,3 +37,12 @@ class AtenOps:
         b, c, h, w = q.shape
         qh, kh = q.reshape(b, heads, c // heads, h * w), k.reshape(b, heads, c // heads, h * w)
         return qh @ kh.transpose(-2, -1)
+
+    @staticmethod
+    def norm_gram(qk, heads):
+        b, c2, h, w = qk.shape
+        c = c2 // 2
+        q, k = qk[:, :c].reshape(b, heads, c // heads, h * w), qk[:, c:].reshape(b, heads, c // heads, h * w)
+        q = q / q.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+        k = k / k.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+        return q @ k.transpose(-2, -1)

@@ -37,6 +37,16 @@ def test_exports_match_header():
         assert hasattr(L, s)
 
 
+def test_training_exports_match_header():
+    """Every entry point include/turtle_train.h declares is exported by libturtle_hip.so."""
+    hdr = open(os.path.join(REPO, "include", "turtle_train.h")).read()
+    declared = set(re.findall(r"\b(turtle_train_[a-z0-9_]+)\s*\(", hdr))
+    assert len(declared) >= 10
+    L = _lib.lib()
+    for s in declared:
+        assert hasattr(L, s), s
+
+
 @pytest.mark.parametrize("model,sr", [("Turtle_t1", False), ("TurtleSuper_t1", True)])
 def test_state_dict_surface(model, sr):
     L, h = handle(gopro(), sr)

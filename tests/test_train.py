@@ -282,6 +282,18 @@ def test_hip_train_ops_match_autograd(dtype):
         torch.testing.assert_close(gw.float(), rw, rtol=gtol["rtol"], atol=gtol["atol"] * 20)
         torch.testing.assert_close(gb, rb, rtol=gtol["rtol"], atol=gtol["atol"] * 20)
     for heads in (1, 4):
+        # the normalised Gram over a channel slice [q | k] of a wider (qkv-like) map
+        qkv = torch.randn(2, 384, 17, 19, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+        qk = qkv[:, :256].detach().requires_grad_()
+        Gn = HipOps.norm_gram(qk, heads)
+        gG = torch.randn_like(Gn)
+        (gqk,) = torch.autograd.grad(Gn, [qk], gG)
+        qk2 = qk.detach().float().requires_grad_()
+        Gn2 = AtenOps.norm_gram(qk2, heads)
+        (rqk,) = torch.autograd.grad(Gn2, [qk2], gG)
+        torch.testing.assert_close(Gn, Gn2, rtol=gtol["rtol"], atol=gtol["atol"] * 0.1)
+        torch.testing.assert_close(gqk.float(), rqk, rtol=gtol["rtol"], atol=float(rqk.abs().max()) * 2e-2)
+    for heads in (1, 4):
         qk = torch.randn(2, 256, 17, 19, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
         q, k = qk[:, :128].detach().requires_grad_(), qk[:, 128:].detach().requires_grad_()
         G = HipOps.gram(q, k, heads)

@@ -444,8 +444,10 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const T* __restrict__ x, 
 // column sums db[n] = sum_p dy[p][n] (8 channels per thread, pixel lanes, LDS reduction, atomics)
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, int64_t ld, float* __restrict__ db, int64_t P,
-                                                     int N, int64_t ppb) {
+                                                     int N, int64_t ppb, int square) {
   extern __shared__ float sred[];
+  dy += (int64_t)blockIdx.y * P * ld;              // image blockIdx.y of P pixels (one image: y = 0)
+  db += (int64_t)blockIdx.y * N;
   for (int i = threadIdx.x; i < N; i += 256) sred[i] = 0.f;
   __syncthreads();
   const int nch = N / 8, lanes = 256 / nch;
@@ -456,8 +458,13 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, i
     for (int64_t p = p0 + pl; p < p1; p += lanes) {
       float v[8];
       ld8f(dy + p * ld + 8 * ch, v);
+      if (square) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) a[e] += v[e];
+        for (int e = 0; e < 8; ++e) a[e] = fmaf(v[e], v[e], a[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] += v[e];
+      }
     }
 #pragma unroll
     for (int e = 0; e < 8; ++e) atomicAdd(&sred[8 * ch + e], a[e]);
@@ -710,7 +717,17 @@ template <typename T>
 int colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, hipStream_t st) {
   const int64_t blocks = std::min<int64_t>(1024, std::max<int64_t>(1, P / 256));
   const int64_t ppb = (P + blocks - 1) / blocks;
-  hipLaunchKernelGGL(colsum_kernel<T>, dim3((unsigned)blocks), dim3(256), N * sizeof(float), st, (const T*)dy, ld, db, P, N, ppb);
+  hipLaunchKernelGGL(colsum_kernel<T>, dim3((unsigned)blocks), dim3(256), N * sizeof(float), st, (const T*)dy, ld, db, P, N, ppb, 0);
+  return 0;
+}
+// per-image column sums of squares: out[img][n] += sum over the image's img_px pixels of x^2
+template <typename T>
+int colsumsq(const void* x, int64_t ld, float* out, int64_t P, int N, int64_t img_px, hipStream_t st) {
+  const int64_t nimg = P / img_px;
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 512 / nimg), std::max<int64_t>(1, img_px / 256));
+  const int64_t ppb = (img_px + blocks - 1) / blocks;
+  hipLaunchKernelGGL(colsum_kernel<T>, dim3((unsigned)blocks, (unsigned)nimg), dim3(256), N * sizeof(float), st, (const T*)x, ld, out,
+                     img_px, N, ppb, 1);
   return 0;
 }
 
@@ -833,6 +850,12 @@ int turtle_train_gate_bwd(const void* x, int64_t ldx, const void* dy, int64_t ld
 int turtle_train_colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, int dtype, void* stream) {
   if (!rows_ok(dy, ld, dtype) || !db || P <= 0 || N <= 0 || N % 8 || N > 2048) return -1;
   TT_DISPATCH(dtype, colsum, dy, ld, db, P, N, (hipStream_t)stream);
+}
+
+int turtle_train_colsumsq(const void* x, int64_t ld, float* out, int64_t P, int N, int64_t img_px, int dtype, void* stream) {
+  if (!rows_ok(x, ld, dtype) || !out || P <= 0 || N <= 0 || N % 8 || N > 2048 || img_px <= 0 || P % img_px || P / img_px > 65535)
+    return -1;
+  TT_DISPATCH(dtype, colsumsq, x, ld, out, P, N, img_px, (hipStream_t)stream);
 }
 
 int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride, int64_t img_px, const float* bias, void* y,

@@ -177,6 +177,16 @@ class TrainGraph:
         b, c, h, w = x.shape
         qkv = self._dw(m.qkv_dwconv, self._c1(m.qkv, x))
         ops = self._ops()
+        if ntc is None and kc is None and vc is None and hasattr(ops, "norm_gram"):
+            # on the op set's kernels: the Gram of the L2-normalised q, k (690-697) in one op over
+            # the channel-adjacent [q | k] rows, softmax, then project_out . blockdiag(A) as one
+            # per-image weight set applied to v (A v followed by project_out, 697-702)
+            qk, v = _split(qkv, 2 * c, c)
+            ch = c // heads
+            a = torch.softmax(ops.norm_gram(qk, heads) * m.temperature, dim=-1)
+            wp = m.project_out.weight.reshape(c, heads, ch)
+            weff = torch.einsum("ohi,bhij->bohj", wp, a).reshape(b, c, c)
+            return ops.conv1x1(v, weff, m.project_out.bias), None, None
         if ntc is None and kc is None and vc is None and hasattr(ops, "gram"):
             # on the op set's kernels: Gram of the raw q, k over HW (per head) divided by the L2
             # norms (== normalising first, 690-693), softmax, then project_out . blockdiag(A) as

@@ -289,6 +289,61 @@ class _Gram(torch.autograd.Function):
         return dq, dk, None
 
 
+class _NormGram(torch.autograd.Function):
+    """Gn[b, h] = normalize(q_h) normalize(k_h)^T over HW (F.normalize, eps 1e-12:
+    turtle_t1_arch.py:690-697) from the channel-adjacent [q | k] rows of qkv. Forward: the Gram by
+    the reduction GEMM, the L2 norms by one column sum-of-squares pass over [q | k]. Backward: one
+    GEMM over the same [q | k] rows with per-image weights [[diag(a_q), D], [D^T, diag(a_k)]] (D =
+    dGn / (|q| |k|^T) block-diagonal per head, a = the norms' gradient / |x|), so neither the fp32
+    copies of q and k nor the norm ops' elementwise passes of the ATen formulation exist."""
+
+    @staticmethod
+    def forward(ctx, qk, heads: int):
+        gdt = _gemm_dt(qk)
+        in_dt = qk.dtype
+        qk, ld = rows(qk.to(gdt))
+        B, C2, H, W = qk.shape
+        c = C2 // 2
+        ch = c // heads
+        P, HW = B * H * W, H * W
+        G = torch.empty(B, heads, ch, ch, dtype=torch.float32, device=qk.device)
+        for h in range(heads):
+            G[:, h] = _rgemm(qk[:, h * ch:(h + 1) * ch], ld, qk[:, c + h * ch:c + (h + 1) * ch], ld, P, ch, ch, HW)
+        ss = torch.zeros(B, C2, dtype=torch.float32, device=qk.device)
+        _check(lib().turtle_train_colsumsq(_p(qk), ld, _p(ss), P, C2, HW, _dt(qk), _stream(qk)), "colsumsq")
+        n = ss.sqrt()
+        nc = n.clamp_min(1e-12)
+        nq, nk = nc[:, :c].view(B, heads, ch), nc[:, c:].view(B, heads, ch)
+        Gn = G / (nq[..., :, None] * nk[..., None, :])
+        ctx.save_for_backward(qk, Gn, nq, nk, n)
+        ctx.heads, ctx.ld, ctx.in_dt = heads, ld, in_dt
+        return Gn
+
+    @staticmethod
+    def backward(ctx, dGn):
+        qk, Gn, nq, nk, n = ctx.saved_tensors
+        B, C2, H, W = qk.shape
+        c, heads = C2 // 2, ctx.heads
+        ch = c // heads
+        P, HW = B * H * W, H * W
+        dGn = dGn.float()
+        D = dGn / (nq[..., :, None] * nk[..., None, :])                  # dL/dG
+        t = dGn * Gn
+        live = (n > 1e-12).float()
+        aq = (-t.sum(-1) / (nq * nq)).reshape(B, c) * live[:, :c]          # dL/d|q_i| / |q_i|
+        ak = (-t.sum(-2) / (nk * nk)).reshape(B, c) * live[:, c:]
+        Wd = torch.zeros(B, C2, C2, dtype=torch.float32, device=qk.device)
+        idx = torch.arange(c, device=qk.device)
+        Wd[:, idx, idx] = aq
+        Wd[:, c + idx, c + idx] = ak
+        for h in range(heads):
+            s0, s1 = h * ch, (h + 1) * ch
+            Wd[:, s0:s1, c + s0:c + s1] = D[:, h]
+            Wd[:, c + s0:c + s1, s0:s1] = D[:, h].transpose(1, 2)
+        dqk = _gemm_into(qk, ctx.ld, Wd.to(qk.dtype).contiguous(), HW, None, P, C2, C2)
+        return dqk.to(ctx.in_dt), None
+
+
 def _act_dtype(x: torch.Tensor) -> torch.dtype:
     if torch.is_autocast_enabled("cuda") and x.dtype == torch.float32:
         return torch.get_autocast_dtype("cuda")
@@ -328,3 +383,9 @@ class HipOps:
     @staticmethod
     def gram(q, k, heads: int):
         return _Gram.apply(_act(q), _act(k), heads)
+
+    @staticmethod
+    def norm_gram(qk, heads: int):
+        """[b, heads, ch, ch] Gram of the L2-normalised (over HW) q and k, the first / second half of
+        qk's channels."""
+        return _NormGram.apply(_act(qk), heads)
