@@ -29,6 +29,8 @@ class AtenOps:
     def conv1x1(x, w, b):
         if w.dim() == 4:
             return F.conv2d(x, w, b)
+        if w.dim() == 2:                                # [N, K]: one shared weight set
+            return F.conv2d(x, w[:, :, None, None], b)
         y = torch.einsum("bkhw,bnk->bnhw", x, w)        # one weight set per image
         return y if b is None else y + b.view(1, -1, 1, 1)
 

@@ -158,14 +158,27 @@ class TrainGraph:
             return ops.conv1x1(x, m.weight, m.bias)
         return _conv1(m, x)
 
+    def _c1_scaled(self, m, x, scale):
+        """nn.Conv2d(K, N, 1)(x) * scale (scale [1, N, 1, 1]: FeedForward's gamma, ReducedAttn's
+        beta) with the scale folded into the weights and bias - W' = diag(scale) W, b' = scale b, tiny
+        ops autograd differentiates - so the full-size multiply and its two backward passes (the
+        input gradient and gamma's reduction over every pixel) do not run on the op set's GEMM."""
+        ops = self._ops()
+        if not hasattr(ops, "conv1x1"):
+            return _conv1(m, x) * scale
+        sv = scale.reshape(-1)
+        w = m.weight.reshape(m.weight.shape[0], m.weight.shape[1]) * sv[:, None]
+        b = None if m.bias is None else m.bias * sv
+        return ops.conv1x1(x, w, b)
+
     def _gffw(self, m, x):                          # GatedFeedForward 159-178
         return self._c1(m.project_out, self._ops().gelu_gate(self._dw(m.dwconv, self._c1(m.project_in, x))))
 
     def _ffw(self, m, x):                           # FeedForward 181-210
-        return self._c1(m.conv5, F.gelu(self._c1(m.conv4, x))) * m.gamma
+        return self._c1_scaled(m.conv5, F.gelu(self._c1(m.conv4, x)), m.gamma)
 
     def _reduced(self, m, x):                       # ReducedAttn 704-742
-        return self._c1(m.conv3, F.gelu(self._dw(m.conv2, self._c1(m.conv1, x)))) * m.beta
+        return self._c1_scaled(m.conv3, F.gelu(self._dw(m.conv2, self._c1(m.conv1, x))), m.beta)
 
     @staticmethod
     def _heads(t, heads):
