@@ -77,6 +77,9 @@ for s in $STEPS; do
     tcopy)
       timeout -k 10 300 python -u tools/train_copies.py --gpu --res 128 --batch 2 --frames 2 > $OUT/train_copies.txt 2>&1
       rc=$?; echo "tcopy rc=$rc"; head -30 $OUT/train_copies.txt; [ $rc -ne 0 ] && exit $rc ;;
+    pmc)
+      timeout -k 10 900 bash tools/gpu_pmc.sh $TAG/pmc > $OUT/pmc.log 2>&1
+      rc=$?; echo "pmc rc=$rc"; tail -3 $OUT/pmc.log; [ $rc -ne 0 ] && exit $rc ;;
     iso)
       timeout -k 10 300 python -u tools/bf16_isolate.py > $OUT/iso.log 2>&1
       rc=$?; echo "iso rc=$rc"; cat $OUT/iso.log | grep PSNR; [ $rc -ne 0 ] && exit $rc ;;

@@ -65,6 +65,17 @@ struct DwArgs {
 };
 template <typename T> void launch_dw(const DwArgs& a, hipStream_t st);
 
+// spatial.hip: level-1 Downsample as an LDS-tiled 3x3 conv (Cin -> Cin / 2, bf16) with the
+// PixelUnshuffle(2) store; weights as pre-packed MFMA A fragments [Cout / 16][9 Cin / 32][64 lanes][8]
+struct DownTileArgs {
+  const void* x; int64_t ldx; int Cin;        // input NHWC [nimg][H][W][ldx]
+  const void* wfrag;
+  void* out; int64_t ldo;                     // output NHWC [nimg][H/2][W/2][ldo], channels 0 .. 2 Cin - 1
+  int nimg, H, W;
+};
+bool down_tile_ok(const DownTileArgs& a);
+void launch_down_tile(const DownTileArgs& a, hipStream_t st);
+
 struct WinArgs {                   // SAB q2/k2 window conv (ws x ws, stride ws, pad 1) + L2 norm
   const void* in; int64_t ldi; int offi;
   const float* w;                  // [ws*ws][C] fp32

@@ -736,6 +736,92 @@ __global__ __launch_bounds__(256) void ending_tile_kernel(EndArgs a) {
   }
 }
 
+// Down1_2 (turtle_t1_arch.py:136-144 at level 1): 3x3 conv CIN -> COUT = CIN / 2 + PixelUnshuffle(2),
+// LDS-tiled like the ending: a block owns 4 rows x 64 columns of the conv output, stages the
+// haloed 6 x 66 x CIN input once (coalesced 16-byte loads), and each wave runs its row as 4 runs of
+// 16 pixels x COUT channels on the matrix cores (A = pre-packed weight fragments in registers, B =
+// pixel rows from LDS). The unshuffled output tile (2 rows x 32 pixels x 4 COUT channels) is staged
+// in LDS and written as 16-byte rows. Against the implicit-GEMM path (9 L2 re-reads of every input
+// vector for a 32-channel output): each input byte leaves L2 about 1.5 times.
+constexpr int DT_R = 4, DT_C = 64;
+template <int CIN>
+__global__ __launch_bounds__(256) void down_tile_kernel(DownTileArgs a) {
+  constexpr int COUT = CIN / 2, NCT = COUT / 16, KS = 9 * CIN / 32, PB = CIN * 2 + 16, TW = DT_C + 2, NPX = (DT_R + 2) * TW;
+  constexpr int CV = CIN / 8, OC = 4 * COUT;               // output channels after the unshuffle
+  __shared__ __attribute__((aligned(16))) char sx[NPX * PB];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int tpr = (a.W + DT_C - 1) / DT_C, tpc = (a.H + DT_R - 1) / DT_R;
+  const int bx = blockIdx.x % tpr, rest = blockIdx.x / tpr, by = rest % tpc, b = rest / tpc;
+  const int x0 = bx * DT_C, y0 = by * DT_R;
+  const bf16* X = reinterpret_cast<const bf16*>(a.x);
+  for (int e = tid; e < NPX * CV; e += 256) {
+    const int p = e / CV, k = e - p * CV, r = p / TW, c = p - r * TW;
+    const int yy = y0 - 1 + r, xx = x0 - 1 + c;
+    const bool ok = yy >= 0 && yy < a.H && xx >= 0 && xx < a.W;
+    const uint4 v = ld16(ok ? reinterpret_cast<const void*>(X + (((int64_t)b * a.H + yy) * a.W + xx) * a.ldx + k * 8) : g_zero_end);
+    *reinterpret_cast<uint4*>(sx + p * PB + k * 16) = v;
+  }
+  bf16x8 wf[NCT][KS];
+#pragma unroll
+  for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+    for (int st = 0; st < KS; ++st)
+      wf[ct][st] = __builtin_bit_cast(bf16x8, ld16(reinterpret_cast<const bf16*>(a.wfrag) + ((ct * KS + st) * 64 + lane) * 8));
+  __syncthreads();
+  const int y = y0 + wid;
+  f32x4 acc[DT_C / 16][NCT];
+#pragma unroll
+  for (int run = 0; run < DT_C / 16; ++run) {
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct) acc[run][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int xl = run * 16 + li;
+#pragma unroll
+    for (int st = 0; st < KS; ++st) {
+      const int k0 = st * 32 + g * 8, tap = k0 / CIN, c = k0 - tap * CIN;
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(sx + ((wid + tap / 3) * TW + xl + tap % 3) * PB + c * 2);
+#pragma unroll
+      for (int ct = 0; ct < NCT; ++ct) acc[run][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ct][st], bv, acc[run][ct], 0, 0, 0);
+    }
+  }
+  __syncthreads();                                  // the input tile is dead: LDS holds the output tile
+  // lane: conv-output channels 16 ct + 4 g + i of pixel (y, x0 + 16 run + li) -> unshuffled pixel
+  // ((y - y0) / 2, (xl) / 2), channel (16 ct + 4 g + i) * 4 + (y & 1) * 2 + (xl & 1)
+  char* so = sx;                                     // [DT_R / 2][DT_C / 2][OC] bf16
+#pragma unroll
+  for (int run = 0; run < DT_C / 16; ++run) {
+    const int xl = run * 16 + li;
+#pragma unroll
+    for (int ct = 0; ct < NCT; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = 16 * ct + 4 * g + i;
+        const int off = ((wid >> 1) * (DT_C / 2) + (xl >> 1)) * OC + co * 4 + (wid & 1) * 2 + (xl & 1);
+        reinterpret_cast<bf16*>(so)[off] = (bf16)acc[run][ct][i];
+      }
+  }
+  __syncthreads();
+  const int Ho = a.H / 2, Wo = a.W / 2, Y0 = y0 / 2, X0 = x0 / 2;
+  bf16* O = reinterpret_cast<bf16*>(a.out);
+  constexpr int NV16 = (DT_R / 2) * (DT_C / 2) * OC / 8;
+  for (int e = tid; e < NV16; e += 256) {
+    const int px = e / (OC / 8), k = e - px * (OC / 8), yr = px / (DT_C / 2), xc = px - yr * (DT_C / 2);
+    const int Y = Y0 + yr, Xo = X0 + xc;
+    if (Y < Ho && Xo < Wo)
+      *reinterpret_cast<uint4*>(O + (((int64_t)b * Ho + Y) * Wo + Xo) * a.ldo + k * 8) = *reinterpret_cast<const uint4*>(so + (px * OC + k * 8) * 2);
+  }
+}
+
+bool down_tile_ok(const DownTileArgs& a) {
+  if (a.Cin != 64 || !a.wfrag || !a.x || !a.out || a.H % 2 || a.W % 2 || a.H < 2 || a.W < 2) return false;
+  if (a.ldx % 8 || a.ldo % 8 || a.ldo < 2 * a.Cin) return false;
+  return ((reinterpret_cast<uintptr_t>(a.x) | reinterpret_cast<uintptr_t>(a.out) | reinterpret_cast<uintptr_t>(a.wfrag)) & 15) == 0;
+}
+
+void launch_down_tile(const DownTileArgs& a, hipStream_t st) {
+  const int64_t blocks = (int64_t)a.nimg * ((a.H + DT_R - 1) / DT_R) * ((a.W + DT_C - 1) / DT_C);
+  hipLaunchKernelGGL(down_tile_kernel<64>, dim3((unsigned)blocks), dim3(256), 0, st, a);
+}
+
 template <int CIN>   // frame channels (Cimg, or 2 Cimg with use_both_input); K = 9 CIN padded to 32 KS
 __global__ __launch_bounds__(256) void stem_mfma_kernel(StemArgs a) {
   constexpr int KS = (9 * CIN + 31) / 32;

@@ -518,28 +518,19 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
   const int srow = tid >> 2, sch = 2 * (tid & 3);
   // transposed reads: lane group g = lane >> 4, row q = (lane >> 2) & 3, column quad pq = lane & 3
   const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
-  // the next stage's operands are loaded into registers while this stage's MFMAs run; loads are
-  // unconditional (a zero line past the map / the tile), so they issue back to back
-  uint4 va[2], vb[2];
-  auto fetch = [&](int64_t pb) {
+  for (int64_t pb = p0; pb < p1; pb += RG_BP) {
     const int64_t p = pb + srow;
     const bool live = p < p1;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int cA = n0 + 8 * (sch + u), cB = k0 + 8 * (sch + u);
-      va[u] = *reinterpret_cast<const uint4*>(live && cA < N ? reinterpret_cast<const void*>(A + (pbase + p) * lda + cA) : g_zero_tw);
-      vb[u] = *reinterpret_cast<const uint4*>(live && cB < K ? reinterpret_cast<const void*>(B + (pbase + p) * ldb + cB) : g_zero_tw);
-    }
-  };
-  if (p0 < p1) fetch(p0);
-  for (int64_t pb = p0; pb < p1; pb += RG_BP) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      *reinterpret_cast<uint4*>(sA + srow * RG_PITCH + 16 * (sch + u)) = va[u];
-      *reinterpret_cast<uint4*>(sB + srow * RG_PITCH + 16 * (sch + u)) = vb[u];
+      uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+      if (live && cA < N) va = *reinterpret_cast<const uint4*>(A + (pbase + p) * lda + cA);
+      if (live && cB < K) vb = *reinterpret_cast<const uint4*>(B + (pbase + p) * ldb + cB);
+      *reinterpret_cast<uint4*>(sA + srow * RG_PITCH + 16 * (sch + u)) = va;
+      *reinterpret_cast<uint4*>(sB + srow * RG_PITCH + 16 * (sch + u)) = vb;
     }
     __syncthreads();
-    if (pb + RG_BP < p1) fetch(pb + RG_BP);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {               // 32 pixels per MFMA K step
       bf16x8v af[2], bfr[2];
@@ -754,8 +745,7 @@ static int64_t rgemm_splits(int64_t P, int N, int K, int64_t img_px) {
   const int64_t plen = img_px > 0 ? img_px : P;
   const int64_t nimg = img_px > 0 ? P / img_px : 1;
   const int64_t tiles = ((N + RG_BN - 1) / RG_BN) * ((K + RG_BK - 1) / RG_BK) * nimg;
-  // ~512 blocks and >= 1024 pixels (16 stages) per block: fewer fp32 partials for the reduce
-  return std::max<int64_t>(1, std::min<int64_t>((512 + tiles - 1) / tiles, (plen + 1023) / 1024));
+  return std::max<int64_t>(1, std::min<int64_t>((1024 + tiles - 1) / tiles, (plen + 511) / 512));
 }
 
 }  // namespace turtle

@@ -221,6 +221,7 @@ struct BlockW {
 struct ModelW {
   size_t stem_w = NONE, stem_b = NONE, end_w = NONE, end_b = NONE;
   size_t end_wf = NONE;                      // ending 3x3 as bf16 MFMA A fragments [9 Cin / 32][64 lanes][8] (spatial.hip)
+  size_t down_wf = NONE;                     // level-1 Downsample 3x3 as bf16 A fragments [Cout / 16][9 Cin / 32][64][8] (down_tile_kernel)
   size_t zeros = NONE, ones = NONE;          // constant vectors for branch-free kernel operands
   GemmW down[3], up[3], reduce[3];
   bool reduce_split = false;                 // reduce[2] packed as split-bf16 [W_hi | W_lo] (K doubled)
@@ -328,10 +329,11 @@ struct TurtleHandle {
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
-  bool gram_dw = true;                                // level-3 channel attention: q / k depthwise inside the Gram kernel (attn.hip)
+  bool gram_dw = false;                               // ChannelAttention q / k depthwise inside the Gram kernel (attn.hip): measured slower, off
   int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
+  bool down_tile = true;                              // level-1 Downsample as the LDS-tiled conv kernel (spatial.hip down_tile_kernel)
   bool split_out = true;                              // split-bf16 weights for reduce_chan_level1 (bf16 builds)
   bool dwgemm_attn = true;                            // channel attention: v's depthwise inside the W_eff GEMM (dwgemm.hip)
   int dwgemm_min_blocks = 384;                        // one 160 KB block per CU: below ~1.5 rounds (latent level) dw + GEMM is faster
@@ -484,6 +486,7 @@ static void pack_all(TurtleHandle* h) {
   Packer pk; pk.bf16 = h->bf16();
   ModelW& M = h->mw;
   M.reduce_split = false;
+  M.down_wf = NONE;
   const int d = A.dim;
   M.stem_w = pk.f32(dvec(W(h, "input_projection.weight")));
   if (has(h, "input_projection.bias")) M.stem_b = pk.f32(dvec(W(h, "input_projection.bias")));
@@ -516,6 +519,21 @@ static void pack_all(TurtleHandle* h) {
   for (int i = 0; i < 3; ++i) {
     const int c = d << i;                 // down i: level i channels -> c/2 (then unshuffle x4)
     M.down[i] = pack_conv3(h, pk, downs[i], c, c / 2, false);
+    if (i == 0 && pk.bf16 && c == 64) {
+      // A fragments of the tiled kernel: fragment (ct, s), lane l: output channel 16 ct + (l & 15),
+      // k = 32 s + 8 (l >> 4) + j -> (tap = k / c, ci = k % c); weight [c/2][c][3][3]
+      const auto& dwt = W(h, std::string(downs[i]) + ".weight");
+      const int co_n = c / 2, ks = 9 * c / 32;
+      std::vector<double> f((size_t)(co_n / 16) * ks * 64 * 8, 0.0);
+      for (int ct = 0; ct < co_n / 16; ++ct)
+        for (int s2 = 0; s2 < ks; ++s2)
+          for (int l = 0; l < 64; ++l)
+            for (int j = 0; j < 8; ++j) {
+              const int k = s2 * 32 + (l >> 4) * 8 + j, tap = k / c, ci = k - tap * c, co = ct * 16 + (l & 15);
+              f[(((size_t)ct * ks + s2) * 64 + l) * 8 + j] = dwt[((size_t)co * c + ci) * 9 + tap];
+            }
+      M.down_wf = pk.bf16tab(f);
+    }
     const int cu = d << (3 - i);          // up i: level (3-i) channels -> 2c, shuffled to c/2
     M.up[i] = pack_conv3(h, pk, ups[i], cu, 2 * cu, true);
     const int cr = cu;                    // reduce: cat(up c/2, skip c/2) = cu -> cu/2
@@ -1436,6 +1454,18 @@ struct Runner {
     int H = Hp, Wd = Wp;
     e1 = level(0, e1, a1, H, Wd);
     auto down = [&](int i, const T* x, int c, T* y, int H0, int W0) {
+      if (i == 0 && ES == 2 && h->down_tile && h->mw.down_wf != NONE) {
+        if (dry()) return;
+        DownTileArgs dt{};
+        dt.x = x; dt.ldx = c; dt.Cin = c; dt.wfrag = h->ptr(h->mw.down_wf); dt.out = y; dt.ldo = 2 * c;
+        dt.nimg = B; dt.H = H0; dt.W = W0;
+        if (down_tile_ok(dt)) {
+          tag("down_tile nimg=%d H=%d W=%d C=%d", B, H0, W0, c);
+          launch(TURTLE_K_GEMM, ES * (double)B * H0 * W0 * (c + c / 2), 2.0 * B * H0 * W0 * (c / 2) * 9.0 * c,
+                 [&] { launch_down_tile(dt, st); });
+          return;
+        }
+      }
       gemm(h->mw.down[i], src1(x, c, 0, 9 * c), (int64_t)B * H0 * W0, H0 * W0, W0, y, 2 * c, 0, nullptr, 0, 0, 0,
            STORE_UNSHUFFLE, nullptr, 0, 1, -1, nullptr, 1, c);
     };
@@ -1582,6 +1612,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     }
     else if (n == "ffn") h->ffn = value != 0;
     else if (n == "gram_dw") h->gram_dw = value != 0;
+    else if (n == "down_tile") h->down_tile = value != 0;
     else if (n == "sab_db") h->sab_db = value != 0;
     else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
