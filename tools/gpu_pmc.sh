@@ -8,7 +8,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-psnr"
-KRE='dwgemm_kernel|ffn_kernel|fused2_kernel|dw_rows_kernel|gemm_pn_kernel|gram_dw_kernel'
+KRE='dwgemm_kernel|ffn_kernel|fused2_kernel|dw_rows_kernel|gemm_pn_kernel'
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/fetch -o run -- python3 $BENCH > $OUT/fetch.log 2>&1 &&
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/write -o run -- python3 $BENCH > $OUT/write.log 2>&1
 rc=$?; echo "pmc rc=$rc"; [ $rc -ne 0 ] && exit $rc
@@ -21,6 +21,5 @@ python3 tools/pmc_traffic.py $OUT \
   'fused2 mode=2 nimg=1 H=544 W=960 C=128 N1=640 N2=128 ln=1 ndst=0@@fused2_kernel<2, 128,' \
   'fused2 mode=1 nimg=1 H=1088 W=1920 C=64 N1=128 N2=64 ln=1 ndst=0@@fused2_kernel<1, 64,' \
   'fused2 mode=1 nimg=1 H=544 W=960 C=128 N1=256 N2=128 ln=1 ndst=0@@fused2_kernel<1, 128,' \
-  'gram_dw B=1 HW=130560 c=256 heads=4 nchunk=135@@gram_dw_kernel:276480' \
   > $OUT/pmc_traffic.json
 rc=$?; python3 -c "import json; d=json.load(open('$OUT/pmc_traffic.json')); print(d['source_hash'], json.dumps(d['per_tag'], indent=0)[:1500])"; exit $rc

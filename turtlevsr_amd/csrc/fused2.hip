@@ -67,7 +67,7 @@ TURTLE_DEV f32x4 ld_f4(const float* p) {
   return f32x4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
 }
 
-template <int CM, int R, int HPM, int N1M, int EXTRA = 0>
+template <int CM, int R, int HPM, int N1M>
 struct F2L {
   // row pads: conflict-free ds_read_b128 fragment reads on gfx950's lane grouping for X (+32 B),
   // 2-way reads / writes for G (+16 B), checked against the MI355X LDS bank rules
@@ -78,8 +78,7 @@ struct F2L {
   static constexpr int OFF_TAP = OFF_ST + NXP * 8;       // depthwise taps, bf16 pairs [5][N1]
   static constexpr int OFF_VEC = OFF_TAP + 5 * N1M * 4;  // s, t + b1, dw bias: [3][N1] fp32
   static constexpr int OFF_G = OFF_VEC + 3 * N1M * 4;
-  static constexpr int OFF_X2 = OFF_G + (HPM ? R * 16 * GP : 0);   // F_GATEOUT: per-wave gelu(x1) strips
-  static constexpr int BYTES = OFF_X2 + EXTRA;
+  static constexpr int BYTES = OFF_G + (HPM ? R * 16 * GP : 0);
 };
 
 // MODE, input width CM (= GEMM2 width), tile rows R (multiple of 3), waves NW, hidden channels per
@@ -91,7 +90,7 @@ struct F2L {
 // walk instead of staged in LDS: 32 * N1M fewer LDS bytes per block, i.e. more blocks per CU
 template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE, int TPB = 1, bool TG = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void fused2_kernel(FusedArgs a) {
-  using L = F2L<CM, R, HPM, TG ? 0 : N1M, MODE == F_GATEOUT ? NW * R * 512 : 0>;
+  using L = F2L<CM, R, HPM, TG ? 0 : N1M>;
   constexpr int KS = CM / 32;                       // GEMM1 K steps
   static_assert((R + 4) * 16 * L::XP <= L::BYTES, "the walk's last trip reads two rows past the X tile");
   constexpr int NT = NW * 64;
@@ -384,42 +383,6 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         unit(u + NW, wb);
       }
     }
-  } else if constexpr (MODE == F_GATEOUT) {
-    // ---- GatedFeedForward up to the gate: out[:, h] = gelu(dw(x1)) * dw(x2) for hidden units,
-    // the x1 walk parks gelu(x1) in a wave-private LDS strip ([row][grp][px] x 8 B: conflict-free),
-    // the x2 walk multiplies and stores (dst[0]: [pixel][hidden]) ----
-    const int hid = a.hidden, nunit = hid / 16;
-    char* park = smem + L::OFF_X2 + wid * R * 512 + grp * 128 + px * 8;
-    const FusedDst D = a.dst[0];
-    bf16* dp = reinterpret_cast<bf16*>(D.p);
-    bf16x8 wa[KS], wb[KS];
-    if (wid < nunit) load_w1(wa, wid * 16);
-    for (int u = wid; u < nunit; u += NW) {
-      load_w1(wb, hid + u * 16);                     // x2 fragments fly during the x1 walk
-      walk(u * 16, wa, [&](int orow, const f32x4& d) {
-        bf16x4 g;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-              const f32x2 r = gelu_bf16_2(f32x2{d[2 * h], d[2 * h + 1]});
-              g[2 * h] = (bf16)r.x; g[2 * h + 1] = (bf16)r.y;
-            }
-        *reinterpret_cast<bf16x4*>(park + orow * 512) = g;
-      });
-      if (u + NW < nunit) load_w1(wa, (u + NW) * 16);
-      const int64_t colpart = (int64_t)xg * D.ld + D.off + u * 16 + grp * 4;
-      walk(hid + u * 16, wb, [&](int orow, const f32x4& d) {
-        const bf16x4 g1 = *reinterpret_cast<const bf16x4*>(park + orow * 512);
-        const int y = y0 + orow;
-        if (!out_lane || y >= a.H) return;
-        bf16x4 g;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-              const f32x2 r = f32x2{(float)g1[2 * h], (float)g1[2 * h + 1]} * f32x2{d[2 * h], d[2 * h + 1]};
-              g[2 * h] = (bf16)r.x; g[2 * h + 1] = (bf16)r.y;
-            }
-        *reinterpret_cast<bf16x4*>(dp + ((int64_t)img * a.H + y) * a.W * D.ld + colpart) = g;
-      });
-    }
   } else {
     // ---- passes of `up` units: phase A (units -> G tile), then GEMM2 into per-wave accumulators;
     // wave w owns output tiles w, w + NW, .. for every row (W2 fragments prefetched per pass) ----
@@ -538,20 +501,17 @@ static void f2_launch(const FusedArgs& a0, hipStream_t st) {
   FusedArgs a = a0;
   a.up = HPM / 16;
   // widest GEMM1 the per-channel tables hold: 2 int(2.5 C) (gate), 2C (ReducedAttn), 6C (CHM
-  // [qk | v | qkv]); at C = 256 the dw-only tables stop at 3C (qkv, kv) to fit 2 blocks per CU
-  constexpr int N1M = (MODE == F_GATE || MODE == F_GATEOUT) ? 5 * CM : (MODE == F_GELU ? 2 * CM : (CM >= 256 ? 3 * CM : 6 * CM));
+  // [qk | v | qkv])
+  constexpr int N1M = MODE == F_GATE ? 5 * CM : (MODE == F_GELU ? 2 * CM : 6 * CM);
   const int64_t tiles = (int64_t)a.nimg * ((a.H + R - 1) / R) * ((a.W + F2_TX - 1) / F2_TX);
   const int64_t blocks = (tiles + TPB - 1) / TPB;
   hipLaunchKernelGGL((fused2_kernel<MODE, CM, R, NW, HPM, N1M, WPE, TPB, TG>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, a);
 }
 
 bool fused2_ok(const FusedArgs& a) {
-  if ((a.C != 64 && a.C != 128 && a.C != 256) || a.N1 % 16 || !a.dww2) return false;
-  const int n1max = (a.mode == F_GATE || a.mode == F_GATEOUT) ? 5 * a.C
-                    : (a.mode == F_GELU ? 2 * a.C : (a.C >= 256 ? 3 * a.C : 6 * a.C));
+  if ((a.C != 64 && a.C != 128) || a.N1 % 16 || !a.dww2) return false;
+  const int n1max = a.mode == F_GATE ? 5 * a.C : (a.mode == F_GELU ? 2 * a.C : 6 * a.C);
   if (a.N1 > n1max) return false;
-  if (a.mode == F_GATEOUT) return a.C == 256 && a.ndst == 1 && a.hidden % 16 == 0 && a.N1 == 2 * a.hidden;
-  if (a.C == 256 && a.mode != F_DWONLY) return false;
   if (a.mode == F_DWONLY) return a.ndst >= 1;
   if (a.N2 % 16 || a.N2 > 128 || a.N2 != a.C) return false;
   if (a.res != a.x || a.ldx != a.C || a.offx != 0) return false;   // residual = the block input
@@ -566,14 +526,7 @@ void launch_fused2(const FusedArgs& a, hipStream_t st) {
   // defaults (v = 0) are the fastest measured per shape family on MI355X (tools/f2bench, 1080p);
   // v = 1..5 are the alternatives of the last sweep (profiles/r02h_f2bench_sweep.log)
   const int v = a.dbg;
-  if (a.mode == F_GATEOUT) {
-    if (v == 1) f2_launch<F_GATEOUT, 256, 6, 8, 0, 2>(a, st);
-    else f2_launch<F_GATEOUT, 256, 3, 8, 0, 2>(a, st);
-  } else if (a.mode == F_DWONLY && a.C == 256) {
-    if (v == 1) f2_launch<F_DWONLY, 256, 6, 4, 0, 2>(a, st);
-    else if (v == 2) f2_launch<F_DWONLY, 256, 3, 8, 0, 2>(a, st);
-    else f2_launch<F_DWONLY, 256, 3, 4, 0, 2>(a, st);
-  } else if (a.mode == F_DWONLY) {
+  if (a.mode == F_DWONLY) {
     if (a.C == 64) {
       switch (v) {
         case 1: f2_launch<F_DWONLY, 64, 15, 4, 0, 4>(a, st); break;

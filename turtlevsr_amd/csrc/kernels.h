@@ -124,7 +124,6 @@ struct SabGatherArgs {             // out = sum_c w_c v[key_c], dilated token ->
 bool sab_av_mfma_ok(const SabGatherArgs& a);
 void launch_sab_av_mfma(const SabGatherArgs& a, hipStream_t st);   // bf16
 template <typename T> void launch_sab_gather(const SabGatherArgs& a, hipStream_t st);
-template <typename T> void launch_sab_gather_tile(const SabGatherArgs& a, hipStream_t st);
 
 #define TURTLE_MAX_SEG 6
 struct GramSeg {                   // ch key columns per head from a pixel-major source
@@ -137,19 +136,6 @@ struct GramArgs {
   float* part;                     // [B*heads][nchunk][ch*ncol + ch + ncol]
 };
 template <typename T> void launch_gram(const GramArgs& a, hipStream_t st);
-
-// attn.hip gram_dw: the channel-attention Gram with the q / k depthwise 3x3 computed on the fly
-// from the raw qkv map (bf16, one key segment, 64 channels per head): the dw'd q / k never reach HBM
-struct GramDwArgs {
-  const void* in; int64_t ld; int qoff, koff;   // raw q channel h*ch+i at qoff, k at koff
-  const float* w; const float* bias; int Cw;    // taps [9][Cw] fp32 (q channels then k), bias [Cw]; Cw = 2 C
-  int B, heads, ch, H, W;
-  int RB, nstrip, nband;                        // chunk = (strip of 32 columns, band of RB rows): nchunk = nstrip * nband
-  float* part;                                  // [B*heads][nchunk][ch*ch + 2 ch] as gram_kernel
-};
-bool gram_dw_ok(const GramDwArgs& a);
-void gram_dw_geometry(GramDwArgs& a);           // sets RB / nstrip / nband from B, heads, H, W
-void launch_gram_dw(const GramDwArgs& a, hipStream_t st);
 
 struct AttnFinArgs {               // per-row Gram reduction + softmax
   const float* part; int nchunk;
@@ -174,8 +160,6 @@ struct WeffArgs {                  // W_eff[b][o][col] = sum_i Wp[o][h*ch+i] * A
   void* weff;                      // [B][C][Keff] storage type
 };
 template <typename T> void launch_weff(const WeffArgs& a, hipStream_t st);
-// Gram reduction + row softmax + W_eff fold in two launches (no A round trip)
-template <typename T> void launch_attn_weff(const AttnFinArgs& f, const WeffArgs& a, hipStream_t st);
 
 struct FhrCacheArgs {              // latent FHR cache roll: keep last Rnew rows of [old R ; cur ch]
   const void* old; int R;          // [B][P][heads][R] (R may be 0)
@@ -217,7 +201,7 @@ bool launch_ending_mfma(const EndArgs& a, hipStream_t st);
 [[noreturn]] void kernel_arg_error(const char* what);
 void launch_stem_mfma(const StemArgs& a, hipStream_t st);
 
-enum FusedMode { F_DWONLY = 0, F_GELU = 1, F_GATE = 2, F_GATEOUT = 3 };   // F_GATEOUT: fused2 only
+enum FusedMode { F_DWONLY = 0, F_GELU = 1, F_GATE = 2 };
 struct FusedDst {                  // F_DWONLY output for channels [cbeg, cend)
   void* p; int64_t ld; int off; int cbeg, cend, ccount; int tok_ws; int64_t tok_stride;
 };
@@ -242,18 +226,6 @@ struct FusedArgs {                 // fused.hip: [LN ->] pw -> dw3x3 -> [act -> 
 template <typename T> void launch_fused(const FusedArgs& a, hipStream_t st);
 bool fused2_ok(const FusedArgs& a);                               // fused2.hip (bf16 row walk)
 void launch_fused2(const FusedArgs& a, hipStream_t st);
-
-struct PwdwArgs {                  // pwdw.hip: [LN ->] pw (C -> N1) -> dw3x3 [-> gelu(x1)*x2], bf16
-  const void* x; int64_t ldx; int offx; int C;   // input pixel-major [nimg][H][W][ldx]
-  int nimg, H, W;
-  const void* w1; int N1;          // [N1][C] (LN affine folded)
-  int ln; const float* ln_s; const float* ln_t; const float* b1;
-  const float* dww; const float* dwb;   // [9][N1] fp32, [N1]
-  int gate;                        // 0: out = dw (N1 channels); 1: gelu(dw[:h]) * dw[h:] (h = N1/2)
-  void* out; int64_t ldo; int offo;
-};
-bool pwdw_ok(const PwdwArgs& a);
-void launch_pwdw(const PwdwArgs& a, hipStream_t st);
 
 struct DwGemmArgs {                // dwgemm.hip: out = res + b + W [gelu(dw(x1)) * dw(x2) | dw(x)], bf16
   const void* in; int64_t ldi; int offi;   // hidden map, pixel-major [nimg][H][W][ldi]; x1 at offi, x2 at offi + K

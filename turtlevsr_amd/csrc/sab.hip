@@ -500,148 +500,6 @@ void launch_sab_gather(const SabGatherArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------
-// sparse A.v, query-tiled: block = 8 x 8 query tokens x a 128-element chunk of D x one (b, t).
-// The 41 L1-ball keys of every query of the tile lie in the 16 x 16 token square around it, so
-// that square's value rows (16 x 16 x 256 B = 64 KB) are staged in LDS once by LDS-DMA and the
-// ball candidates (listed first by sab_prep) are read from there; only the <= 5 top-k keys outside
-// the ball come from L2. Against one wave per query this cuts the L2 traffic ~6x (each value row
-// was re-read by ~41 queries). 16 lanes (8 elements each) per query; writes the inverse dilated
-// regroup (turtle_t1_arch.py:602-604) straight into the pixel-major aligned frame.
-// ------------------------------------------------------------------------------------------
-constexpr int SG_T = 8;                      // query tile side (tokens)
-constexpr int SG_S = SG_T + 8;               // staged key square side (ball radius 4)
-constexpr int SG_CH = 128;                   // D elements per block
-
-template <typename T>
-__global__ __launch_bounds__(256) void sab_gather_tile_kernel(SabGatherArgs a) {
-  constexpr int VEC = Vec<T>::N, ES = sizeof(T);
-  constexpr int LPQ = SG_CH / VEC;           // lanes per query (16 bf16, 32 fp32 -> 2 queries / 32 lanes)
-  constexpr int ROWB = SG_CH * ES;           // staged row bytes
-  extern __shared__ __attribute__((aligned(16))) char sv[];   // [SG_S * SG_S][ROWB]
-  const int D = a.ws * a.ws * a.C;
-  const int nch = (D + SG_CH - 1) / SG_CH;
-  const int tty = (a.th + SG_T - 1) / SG_T, ttx = (a.tw + SG_T - 1) / SG_T;
-  int lin = blockIdx.x;
-  {
-    const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
-    lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;
-  }
-  const int tile = lin % (tty * ttx);
-  int rest = lin / (tty * ttx);
-  const int bt = rest % (a.B * a.T);
-  const int chunk = rest / (a.B * a.T);
-  const int ti0 = (tile / ttx) * SG_T, tj0 = (tile % ttx) * SG_T;
-  const int t = bt % a.T, b = bt / a.T;
-  const T* v = reinterpret_cast<const T*>(a.v[0]);
-  int64_t vbs = a.v_bstride[0];
-#pragma unroll
-  for (int j = 1; j < TURTLE_MAX_T; ++j)
-    if (t == j) { v = reinterpret_cast<const T*>(a.v[j]); vbs = a.v_bstride[j]; }
-  v += (int64_t)b * vbs;
-  const int e_base = chunk * SG_CH;
-  const int tid = threadIdx.x;
-
-  // ---- stage the key square: 256 rows x ROWB, 16-byte pieces, rows outside the grid -> zeros ----
-  {
-    constexpr int PPR = ROWB / 16;            // pieces per row
-    constexpr int NP = SG_S * SG_S * PPR / 256;
-#pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int pc = tid + 256 * i, r = pc / PPR, k = pc - r * PPR;
-      const int ki = ti0 - 4 + r / SG_S, kj = tj0 - 4 + r % SG_S;
-      const int e = e_base + k * (16 / ES);
-      const bool ok = ki >= 0 && ki < a.th && kj >= 0 && kj < a.tw && e < D;
-      const uint4 q = ld16(ok ? reinterpret_cast<const void*>(v + (int64_t)(ki * a.tw + kj) * D + e) : g_zero_sab);
-      *reinterpret_cast<uint4*>(sv + r * ROWB + k * 16) = q;
-    }
-  }
-  __syncthreads();
-
-  // ---- per query: LPQ lanes x VEC elements ----
-  const int lq = tid % LPQ, qslot = tid / LPQ;                 // 256 / LPQ query slots per pass
-  constexpr int QPP = 256 / LPQ;
-  const int e0 = e_base + lq * VEC;
-  const bool eok = e0 < D;
-  const int e0c = eok ? e0 : 0;
-  const int Hl = a.th * a.ws, Wl = a.tw * a.ws;
-  T* out = reinterpret_cast<T*>(a.out) + (int64_t)bt * Hl * Wl * a.C;
-  for (int qb = 0; qb < SG_T * SG_T; qb += QPP) {
-    const int ql = qb + qslot;
-    const int ti = ti0 + ql / SG_T, tj = tj0 + ql % SG_T;
-    const bool qok = ti < a.th && tj < a.tw;
-    const int n = qok ? ti * a.tw + tj : 0;
-    const int64_t qi = (int64_t)bt * a.N + n;
-    const int cw_all = qok ? a.cnt[qi] : 0;
-    const int cnt = cw_all & 0xffff, nb = cw_all >> 16;
-    // candidate lists: the query's LPQ lanes hold its <= 48 (key, weight) pairs, broadcast per step
-    const int* ci = a.ci + qi * SAB_MAXC;
-    const float* cw = a.cw + qi * SAB_MAXC;
-    constexpr int NR = (SAB_MAXC + LPQ - 1) / LPQ;
-    int rci[NR];
-    float rcw[NR];
-#pragma unroll
-    for (int k = 0; k < NR; ++k) {
-      const int c = min(lq + LPQ * k, SAB_MAXC - 1);
-      rci[k] = ci[c];
-      rcw[k] = cw[c];
-    }
-    int cmax = cnt;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, __shfl_xor(cmax, o, 64));
-    float acc[VEC];
-#pragma unroll
-    for (int i = 0; i < VEC; ++i) acc[i] = 0.f;
-    const int qbase = (tid & 63) & ~(LPQ - 1);
-    for (int c = 0; c < cmax; ++c) {
-      const int k = c / LPQ, src = qbase + (c - k * LPQ);
-      int mk = rci[0];
-      float wk = rcw[0];
-#pragma unroll
-      for (int u = 1; u < NR; ++u) { mk = k == u ? rci[u] : mk; wk = k == u ? rcw[u] : wk; }
-      const int m = __shfl(mk, src, 64);
-      const float w = __shfl(wk, src, 64);
-      if (c < nb) {
-        // ball key (ki, kj) -> row of the staged square
-        const int ki = m / a.tw, kj = m - ki * a.tw;
-        const int r = (ki - ti0 + 4) * SG_S + (kj - tj0 + 4);
-        Vec<T> x;
-        x.load(reinterpret_cast<const T*>(sv + r * ROWB + lq * 16));
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) acc[i] = fmaf(w, x.v[i], acc[i]);
-      } else if (c < cnt) {
-        // top-k key outside the ball: from L2
-        Vec<T> x;
-        x.from_raw(ld16(v + (int64_t)m * D + e0c));
-#pragma unroll
-        for (int i = 0; i < VEC; ++i) acc[i] = fmaf(w, x.v[i], acc[i]);
-      }
-    }
-    if (qok && eok) {
-      const int sub = e0 / a.C, c0 = e0 - sub * a.C;
-      const int p1 = sub / a.ws, p2 = sub - p1 * a.ws;
-      Vec<T> o;
-#pragma unroll
-      for (int i = 0; i < VEC; ++i) o.v[i] = acc[i];
-      o.store(out + ((int64_t)(p1 * a.th + ti) * Wl + p2 * a.tw + tj) * a.C + c0);
-    }
-  }
-}
-
-template <typename T>
-void launch_sab_gather_tile(const SabGatherArgs& a, hipStream_t st) {
-  const int D = a.ws * a.ws * a.C;
-  const int nch = (D + SG_CH - 1) / SG_CH;
-  const int64_t blocks = (int64_t)nch * a.B * a.T * ((a.th + SG_T - 1) / SG_T) * ((a.tw + SG_T - 1) / SG_T);
-  const size_t lds = (size_t)SG_S * SG_S * SG_CH * sizeof(T);
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_gather_tile_kernel<T>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr = true;
-  }
-  hipLaunchKernelGGL(sab_gather_tile_kernel<T>, dim3((unsigned)blocks), dim3(256), lds, st, a);
-}
-
-// ------------------------------------------------------------------------------------------
 // sparse A.v on the matrix cores. The 41 L1-ball keys of the 8 x 8 query tokens of a tile all lie
 // in the 16 x 16 token square around it, so the ball part of A.v for the tile is a dense product
 //   O[64 q][e] = W'[64 q][256 square keys] . V[256 keys][e]          (41 non-zeros per W' row)
@@ -877,7 +735,5 @@ template void launch_sab_score<float>(const SabScoreArgs&, hipStream_t);
 template void launch_sab_score<bf16>(const SabScoreArgs&, hipStream_t);
 template void launch_sab_gather<float>(const SabGatherArgs&, hipStream_t);
 template void launch_sab_gather<bf16>(const SabGatherArgs&, hipStream_t);
-template void launch_sab_gather_tile<float>(const SabGatherArgs&, hipStream_t);
-template void launch_sab_gather_tile<bf16>(const SabGatherArgs&, hipStream_t);
 
 }  // namespace turtle

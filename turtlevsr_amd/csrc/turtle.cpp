@@ -315,21 +315,16 @@ struct TurtleHandle {
   bool loaded = false;
   bool fuse = getenv("TURTLE_NO_FUSE") == nullptr;   // block-level fused kernels (fused.hip)
   bool fused2 = true;                                 // bf16 row-walk fused kernels (fused2.hip) where eligible
-  bool fused2_wide = false;                           // fused2 at width 256 (level 3): correct, slower than GEMM + dw so far
   bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
   bool gemm_lds = true;                               // LDS-pipelined bf16 GEMM (gemm2.hip)
   bool gemm_pn = true;                                // resident-panel bf16 GEMM, K <= 512 (gemm3.hip)
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
-  bool attn_fuse = false;                             // row softmax folded into the W_eff kernel (attn.hip): slower so far
-  bool sab_tile = false;                              // query-tiled VALU SAB gather (sab.hip)
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   bool sab_db = false;                                // SAB A.v: double-buffered 1-block/CU variant (else 2 blocks / CU)
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
-  bool pwdw = false;                                  // fused pw -> dw (-> gate) for c >= 256 (pwdw.hip): off until it beats GEMM + dw
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
-  bool gram_dw = false;                               // ChannelAttention q / k depthwise inside the Gram kernel (attn.hip): measured slower, off
   int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
@@ -850,11 +845,10 @@ struct Runner {
       if (dsts.empty() || dsts.size() > 3) TFAIL(TURTLE_EINVAL, "fused dw-only needs 1..3 destinations");
       for (size_t i = 0; i < dsts.size(); ++i) f.dst[i] = dsts[i];
       f.ndst = (int)dsts.size();
-      bytes += ES * px * (mode == F_GATEOUT ? hidden : w1.N);
+      bytes += ES * px * w1.N;
     }
     if (dwp.C != w1.N) TFAIL(TURTLE_EINVAL, "fused: dw width != pointwise width");
-    if ((C > 128 || mode == F_GATEOUT) && !(ES == 2 && h->fused2 && fused2_ok(f)))
-      TFAIL(TURTLE_EINVAL, "fused: input width > 128 needs the bf16 row-walk kernel");
+    if (C > 128) TFAIL(TURTLE_EINVAL, "fused: input width > 128");
     tag("fused mode=%d nimg=%d H=%d W=%d C=%d N1=%d N2=%d ln=%d ndst=%d", mode, nimg, H, Wd, C, w1.N, f.N2, f.ln, f.ndst);
     const bool rw = ES == 2 && h->fused2 && fused2_ok(f);
     if (rw) tag("fused2 mode=%d nimg=%d H=%d W=%d C=%d N1=%d N2=%d ln=%d ndst=%d", mode, nimg, H, Wd, C, w1.N, f.N2, f.ln, f.ndst);
@@ -863,37 +857,11 @@ struct Runner {
       else launch_fused<T>(f, st);
     });
   }
-  // fused2.hip at input width 256 (level 3): [LN ->] pw -> dw (qkv, kv) or pw -> dw -> gate
-  // (GatedFeedForward up to project_out), bf16 only
-  bool can_fused2_wide(int c, int mode, int n1, int hidden) const {
-    if (ES != 2 || !h->fuse || !h->fused2 || !h->fused2_wide || c != 256) return false;
-    if (mode == F_GATEOUT) return n1 == 2 * hidden && n1 <= 5 * c && hidden % 16 == 0;
-    return mode == F_DWONLY && n1 % 16 == 0 && n1 <= 3 * c;
-  }
   // fused.hip handles input widths <= 128 in 16-channel slices and 32-deep GEMM2 K steps
   bool can_fuse(int c, int mode, int n1, int hidden) const {
     if (!h->fuse || c > 128 || c % 16) return false;
     if (mode == F_DWONLY) return n1 % 16 == 0;
     return hidden % 32 == 0;
-  }
-  // [LN ->] pw -> dw3x3 [-> gelu(x1)*x2] in one kernel, bf16, input widths multiple of 64 (pwdw.hip)
-  bool can_pwdw(int c, int n1, bool gate) const {
-    if (!h->pwdw || ES != 2 || c % 64) return false;
-    const int hid = gate ? n1 / 2 : n1;
-    return gate ? hid % 64 == 0 : hid % 128 == 0;
-  }
-  void pwdw(const GemmW& w1, const DwW& dwp, const T* x, int64_t ldx, int offx, int C, int nimg, int H, int Wd, int gate,
-            T* out, int64_t ldo, int offo) {
-    if (dry()) return;
-    if (dwp.C != w1.N) TFAIL(TURTLE_EINVAL, "pwdw: dw width != pointwise width");
-    PwdwArgs p{};
-    p.x = x; p.ldx = ldx; p.offx = offx; p.C = C; p.nimg = nimg; p.H = H; p.W = Wd;
-    p.w1 = h->ptr(w1.w); p.N1 = w1.N; p.ln = w1.ln; p.ln_s = h->fptr(w1.s); p.ln_t = h->fptr(w1.t); p.b1 = h->fptr(w1.bias);
-    p.dww = h->fptr(dwp.w); p.dwb = h->fptr(dwp.bias); p.gate = gate; p.out = out; p.ldo = ldo; p.offo = offo;
-    if (!pwdw_ok(p)) TFAIL(TURTLE_EINVAL, "pwdw: unsupported shape");
-    const double px = (double)nimg * H * Wd, hid = gate ? w1.N / 2 : w1.N;
-    tag("pwdw gate=%d nimg=%d H=%d W=%d C=%d N1=%d", gate, nimg, H, Wd, C, w1.N);
-    launch(TURTLE_K_FUSED, ES * px * (C + hid), 2.0 * px * C * w1.N + 18.0 * px * w1.N, [&] { launch_pwdw(p, st); });
   }
   // out (+)= W [gelu(dw(x1)) * dw(x2) | dw(x)] + bias (+ res) with the depthwise computed in the
   // GEMM's operand prologue (dwgemm.hip); returns false (nothing launched) where not eligible
@@ -965,32 +933,17 @@ struct Runner {
   struct Seg { const void* base; int64_t ld; int off; int hstride; int mul, add; int norm; int64_t col; int colh; };
 
   // channel attention core: Gram over (q, key segments), softmax, W_eff, then out = x + W_eff [v srcs]
-  // the q / k depthwise inside the Gram kernel (attn.hip gram_dw): bf16, one key segment, 64
-  // channels per head (shape-only, same in the sizing dry run)
-  bool can_gram_dw(int c, int heads) const { return ES == 2 && h->gram_dw && heads > 0 && c == 64 * heads; }
-
-  // qkdw: q, k are the RAW projections (q at qoff, k at segs[0].off of the same map) and their
-  // depthwise runs inside the Gram (gram_dw); otherwise q / segs are already depthwise'd
   void chan_attn(const BlockW& bw, const Blk& b, const T* q, int64_t ldq, int qoff, const std::vector<Seg>& segs,
                  const SrcList& vsrc, int HW, int Wimg, T* x, float* kinv, int cur_seg,
-                 const DwW* vdw = nullptr, const T* vraw = nullptr, int64_t ldv = 0, int offv = 0, const DwW* qkdw = nullptr) {
+                 const DwW* vdw = nullptr, const T* vraw = nullptr, int64_t ldv = 0, int offv = 0) {
     const int c = b.dim, ch = c / b.heads, nseg = (int)segs.size(), ncol = nseg * ch;
     if (ncol > 512 || nseg > TURTLE_MAX_SEG) TFAIL(TURTLE_EINVAL, "channel attention: more than 512 key columns");
-    GramDwArgs gd{};
-    int nchunk, chunk = 0;
-    if (qkdw) {
-      if (nseg != 1 || ch != 64) TFAIL(TURTLE_EINVAL, "channel attention: gram_dw needs one 64-channel key segment");
-      gd.B = B; gd.heads = b.heads; gd.ch = ch; gd.H = HW / Wimg; gd.W = Wimg;
-      gram_dw_geometry(gd);
-      nchunk = gd.nstrip * gd.nband;
-    } else {
-      // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each, whole
-      // 128-pixel steps of the bf16 Gram
-      nchunk = std::max(1, std::min((HW + 255) / 256, std::max(1, h->gram_blocks / (B * b.heads))));
-      chunk = (HW + nchunk - 1) / nchunk;
-      chunk = (chunk + 127) / 128 * 128;
-      nchunk = (HW + chunk - 1) / chunk;
-    }
+    // pixel splits: ~1024 blocks over all (b, head) at large maps, >= 256 pixels each, whole
+    // 128-pixel steps of the bf16 Gram
+    int nchunk = std::max(1, std::min((HW + 255) / 256, std::max(1, h->gram_blocks / (B * b.heads))));
+    int chunk = (HW + nchunk - 1) / nchunk;
+    chunk = (chunk + 127) / 128 * 128;
+    nchunk = (HW + chunk - 1) / chunk;
     const int stride = ch * ncol + ch + ncol;
     float* part = fbuf((int64_t)B * b.heads * nchunk * stride);
     float* red = fbuf((int64_t)B * b.heads * stride);
@@ -998,14 +951,6 @@ struct Runner {
     T* weff = buf((int64_t)B * c * vsrc.Ktot);
     if (dry()) return;
     if (ch > 128) TFAIL(TURTLE_EINVAL, "channel attention: more than 128 channels per head");
-    if (qkdw) {
-      gd.in = q; gd.ld = ldq; gd.qoff = qoff; gd.koff = segs[0].off;
-      gd.w = h->fptr(qkdw->w); gd.bias = h->fptr(qkdw->bias); gd.Cw = qkdw->C; gd.part = part;
-      if (!gram_dw_ok(gd) || segs[0].base != q || segs[0].ld != ldq) TFAIL(TURTLE_EINVAL, "channel attention: gram_dw not eligible");
-      tag("gram_dw B=%d HW=%d c=%d heads=%d nchunk=%d", B, HW, c, b.heads, nchunk);
-      launch(TURTLE_K_ATTN, ES * (double)B * HW * 2 * c, 2.0 * B * b.heads * ch * ch * (double)HW + 36.0 * B * HW * c,
-             [&] { launch_gram_dw(gd, st); });
-    }
     GramArgs g{};
     g.q = q; g.ldq = ldq; g.qoff = qoff; g.nseg = nseg;
     unsigned mask = 0;
@@ -1014,11 +959,9 @@ struct Runner {
       if (segs[s].norm) mask |= 1u << s;
     }
     g.B = B; g.heads = b.heads; g.ch = ch; g.HW = HW; g.nchunk = nchunk; g.chunk = chunk; g.part = part;
-    if (!qkdw) {
-      tag("gram B=%d HW=%d c=%d heads=%d nseg=%d nchunk=%d", B, HW, c, b.heads, nseg, nchunk);
-      launch(TURTLE_K_ATTN, ES * (double)B * HW * c * (1 + nseg), 2.0 * B * b.heads * ch * ncol * (double)HW,
-             [&] { launch_gram<T>(g, st); });
-    }
+    tag("gram B=%d HW=%d c=%d heads=%d nseg=%d nchunk=%d", B, HW, c, b.heads, nseg, nchunk);
+    launch(TURTLE_K_ATTN, ES * (double)B * HW * c * (1 + nseg), 2.0 * B * b.heads * ch * ncol * (double)HW,
+           [&] { launch_gram<T>(g, st); });
     AttnFinArgs f{};
     f.part = part; f.nchunk = nchunk; f.B = B; f.heads = b.heads; f.ch = ch; f.nseg = nseg;
     f.norm_mask = mask; f.tau = h->fptr(bw.tau); f.kinv = kinv; f.cur_seg = cur_seg; f.red = red; f.attn = attn;
@@ -1026,17 +969,11 @@ struct Runner {
     we.attn = attn; we.wp = h->fptr(bw.wp); we.B = B; we.heads = b.heads; we.ch = ch; we.nseg = nseg; we.C = c;
     for (int s = 0; s < nseg; ++s) { we.seg_col[s] = segs[s].col; we.seg_hstride[s] = segs[s].colh; }
     we.Keff = vsrc.Ktot; we.weff = weff;
-    if (h->attn_fuse) {
-      tag("attn_weff nbh=%d ch=%d ncol=%d nchunk=%d C=%d", B * b.heads, ch, ncol, nchunk, c);
-      launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride + ES * (double)B * c * vsrc.Ktot,
-             2.0 * B * c * (double)b.heads * ncol * ch, [&] { launch_attn_weff<T>(f, we, st); });
-    } else {
-      tag("attn_rows nbh=%d ch=%d ncol=%d nchunk=%d", B * b.heads, ch, ncol, nchunk);
-      launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride, 0, [&] { launch_attn_finalize(f, st); });
-      tag("weff B=%d C=%d heads=%d ncol=%d", B, c, b.heads, ncol);
-      launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot + 4.0 * B * b.heads * ch * ncol, 2.0 * B * c * (double)b.heads * ncol * ch,
-             [&] { launch_weff<T>(we, st); });
-    }
+    tag("attn_rows nbh=%d ch=%d ncol=%d nchunk=%d", B * b.heads, ch, ncol, nchunk);
+    launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride, 0, [&] { launch_attn_finalize(f, st); });
+    tag("weff B=%d C=%d heads=%d ncol=%d", B, c, b.heads, ncol);
+    launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot + 4.0 * B * b.heads * ch * ncol, 2.0 * B * c * (double)b.heads * ncol * ch,
+           [&] { launch_weff<T>(we, st); });
     if (vdw) {
       // v's depthwise folded into the W_eff GEMM's operand prologue (dwgemm.hip): out = x + W_eff dw(v) + b
       if (!dwgemm(*vdw, 0, vraw, ldv, offv, B, HW / Wimg, Wimg, c, weff, c, (int64_t)c * c, c, h->fptr(bw.po_bias), x, c,
@@ -1070,30 +1007,13 @@ struct Runner {
       T* t2 = buf(P * 3 * c);
       const int ch = c / b.heads;
       std::vector<Seg> segs{{t2, 3 * c, c, ch, 1, 0, 1, 0, ch}};
-      if (!can_fuse(c, F_DWONLY, 3 * c, 0) && !can_fused2_wide(c, F_DWONLY, 3 * c, 0) && !can_pwdw(c, 3 * c, false) &&
-          can_dwgemm_v(c, B, H, Wd)) {
+      if (!can_fuse(c, F_DWONLY, 3 * c, 0) && can_dwgemm_v(c, B, H, Wd)) {
         // qkv GEMM, depthwise of q,k only; v's depthwise runs inside the W_eff GEMM (dwgemm.hip)
         T* t1 = buf(P * 3 * c);
         gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
-        if (can_gram_dw(c, b.heads)) {
-          // q, k's depthwise inside the Gram kernel: the dw'd q / k map is never stored
-          std::vector<Seg> rsegs{{t1, 3 * c, c, ch, 1, 0, 1, 0, ch}};
-          chan_attn(bw, b, t1, 3 * c, 0, rsegs, src1(t1, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1, &bw.a_dw_v, t1, 3 * c,
-                    2 * c, &bw.a_dw_qk);
-        } else {
-          dw(bw.a_dw_qk, t1, 3 * c, 0, t2, 3 * c, 0, B, H, Wd, DW_PLAIN);
-          chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t1, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1, &bw.a_dw_v, t1, 3 * c,
-                    2 * c);
-        }
-      } else if (!can_fuse(c, F_DWONLY, 3 * c, 0) && !can_fused2_wide(c, F_DWONLY, 3 * c, 0) && !can_pwdw(c, 3 * c, false) &&
-                 can_gram_dw(c, b.heads)) {
-        // (latent level) qkv GEMM, v's depthwise alone, q / k's inside the Gram kernel
-        T* t1 = buf(P * 3 * c);
-        gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
-        dw(bw.a_dw_v, t1, 3 * c, 2 * c, t2, 3 * c, 2 * c, B, H, Wd, DW_PLAIN);
-        std::vector<Seg> rsegs{{t1, 3 * c, c, ch, 1, 0, 1, 0, ch}};
-        chan_attn(bw, b, t1, 3 * c, 0, rsegs, src1(t2, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1, nullptr, nullptr, 0, 0,
-                  &bw.a_dw_qk);
+        dw(bw.a_dw_qk, t1, 3 * c, 0, t2, 3 * c, 0, B, H, Wd, DW_PLAIN);
+        chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t1, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1, &bw.a_dw_v, t1, 3 * c,
+                  2 * c);
       } else {
         qkv_dw(bw, x, c, t2, B, H, Wd);
         chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t2, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1);
@@ -1110,14 +1030,6 @@ struct Runner {
       if (can_fuse(c, F_GATE, 2 * hd, hd)) {
         fused(F_GATE, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, &bw.f_out, x, xalt, {});
         std::swap(x, xalt);
-      } else if (can_fused2_wide(c, F_GATEOUT, 2 * hd, hd)) {
-        T* t2 = buf(P * hd);
-        fused(F_GATEOUT, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, nullptr, nullptr, nullptr, {dst_map(t2, hd, 0, 0, hd)});
-        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
-      } else if (can_pwdw(c, 2 * hd, true)) {
-        T* t2 = buf(P * hd);
-        pwdw(bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, 1, t2, hd, 0);
-        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
       } else if (can_dwgemm_cb(c, hd, B, H, Wd)) {
         // project_in stores the hidden map channel-blocked ([2 hd / 16][P][16]): each dwgemm K step
         // then reads contiguous 32-byte pixel rows
@@ -1149,11 +1061,9 @@ struct Runner {
 
   // LN(x) -> qkv 1x1 -> qkv_dwconv into `out` [P][3c] (fused, or GEMM + dw)
   void qkv_dw(const BlockW& bw, const T* x, int c, T* out, int nimg, int H, int Wd) {
-    if (can_fuse(c, F_DWONLY, 3 * c, 0) || can_fused2_wide(c, F_DWONLY, 3 * c, 0)) {
+    if (can_fuse(c, F_DWONLY, 3 * c, 0)) {
       fused(F_DWONLY, bw.a_in, bw.a_dw, x, c, 0, c, nimg, H, Wd, 3 * c, nullptr, nullptr, nullptr,
             {dst_map(out, 3 * c, 0, 0, 3 * c)});
-    } else if (can_pwdw(c, 3 * c, false)) {
-      pwdw(bw.a_in, bw.a_dw, x, c, 0, c, nimg, H, Wd, 0, out, 3 * c, 0);
     } else {
       const int64_t P = (int64_t)nimg * H * Wd;
       T* t1 = buf(P * 3 * c);
@@ -1374,7 +1284,6 @@ struct Runner {
       launch(TURTLE_K_SAB_AV, ES * ((double)B * NT * N * D + (double)B * NT * HW * c),
              2.0 * B * NT * (double)N * 46 * D, [&] {
                if (h->sab_mfma && ES == 2 && sab_av_mfma_ok(ga)) launch_sab_av_mfma(ga, st);
-               else if (h->sab_tile) launch_sab_gather_tile<T>(ga, st);
                else launch_sab_gather<T>(ga, st);
              });
     }
@@ -1386,11 +1295,9 @@ struct Runner {
     const int c = b.dim, HW = H * Wd, ch = c / b.heads;
     const int64_t P = (int64_t)B * HW;
     // kv = (W_kv W_po) xs over the B*T aligned frames, then dw3x3 per frame
-    if (can_fuse(c, F_DWONLY, 2 * c, 0) || can_fused2_wide(c, F_DWONLY, 2 * c, 0)) {
+    if (can_fuse(c, F_DWONLY, 2 * c, 0)) {
       fused(F_DWONLY, bw.kv, bw.kv_dw, xs, c, 0, c, B * NT, H, Wd, 2 * c, nullptr, nullptr, nullptr,
             {dst_map(kvd, 2 * c, 0, 0, 2 * c)});
-    } else if (can_pwdw(c, 2 * c, false)) {
-      pwdw(bw.kv, bw.kv_dw, xs, c, 0, c, B * NT, H, Wd, 0, kvd, 2 * c, 0);
     } else {
       T* kv = buf(P * NT * 2 * c);
       gemm(bw.kv, src1(xs, c, 0, c), P * NT, HW, Wd, kv, 2 * c, 0);
@@ -1611,7 +1518,6 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
       if (h->loaded) pack_all(h);
     }
     else if (n == "ffn") h->ffn = value != 0;
-    else if (n == "gram_dw") h->gram_dw = value != 0;
     else if (n == "down_tile") h->down_tile = value != 0;
     else if (n == "sab_db") h->sab_db = value != 0;
     else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;
@@ -1619,13 +1525,9 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
     else if (n == "gemm_ar") h->gemm_ar = value != 0;
     else if (n == "gemm_kt") h->gemm_kt = value != 0;
-    else if (n == "attn_fuse") h->attn_fuse = value != 0;
-    else if (n == "pwdw") h->pwdw = value != 0;
-    else if (n == "sab_tile") h->sab_tile = value != 0;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
     else if (n == "stem_mfma") h->stem_mfma = value != 0;
     else if (n == "fused2") h->fused2 = value != 0;
-    else if (n == "fused2_wide") h->fused2_wide = value != 0;
     else TFAIL(TURTLE_EINVAL, "unknown option '" + n + "'");
   });
 }

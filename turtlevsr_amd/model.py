@@ -31,6 +31,7 @@ strides (P*heads*rows, rows, 1, heads*rows)); incoming caches of any layout are 
 from __future__ import annotations
 
 import ctypes as C
+import operator
 from typing import List, Optional
 
 import torch
@@ -40,6 +41,8 @@ from . import _lib
 from .arch import resolve
 from .params import TurtleParams
 from .train import TrainGraph
+
+_VERSION = operator.attrgetter("_version")
 
 _DT = {"fp32": (_lib.DTYPE_F32, torch.float32), "bf16": (_lib.DTYPE_BF16, torch.bfloat16)}
 
@@ -92,9 +95,12 @@ class TurtleHIP(TrainGraph, TurtleParams):
         return _DT[self._dtype_name][1]
 
     def _signature(self):
-        ps = list(self.parameters())
-        dev = ps[0].device
-        return (dev, self._dtype_name, sum(p._version for p in ps), tuple(p.data_ptr() for p in ps[:4]))
+        # parameter list cached once (Parameter objects survive .to() / load_state_dict); the
+        # version sum catches in-place updates, the leading data pointers catch device moves
+        ps = self.__dict__.get("_plist")
+        if ps is None:
+            ps = self.__dict__["_plist"] = list(self.parameters())
+        return (ps[0].device, self._dtype_name, sum(map(_VERSION, ps)), tuple(p.data_ptr() for p in ps[:4]))
 
     def refresh_weights(self):
         """Pack the current parameters into the device layout (done automatically on change)."""
@@ -109,6 +115,7 @@ class TurtleHIP(TrainGraph, TurtleParams):
                 self._handle = _Handle(_lib.config_from_arch(self.arch, self.sr, _DT[self._dtype_name][0]))
             self._handle_dev = dev
             self._ws = None
+            self.__dict__["_layouts"] = {}
         h = self._handle.h
         with torch.cuda.device(dev):
             for name, t in self.state_dict().items():
@@ -123,6 +130,17 @@ class TurtleHIP(TrainGraph, TurtleParams):
 
     # ---------------------------------------------------------------------------------------
     def cache_layout(self, B: int, H: int, W: int, t_in: List[int]):
+        key = (B, H, W, tuple(t_in))
+        memo = self.__dict__.setdefault("_layouts", {})   # reset with the handle (refresh_weights)
+        res = memo.get(key)
+        if res is None:
+            res = self._cache_layout(B, H, W, t_in)
+            if len(memo) > 64:
+                memo.clear()
+            memo[key] = res
+        return res
+
+    def _cache_layout(self, B: int, H: int, W: int, t_in: List[int]):
         L = _lib.lib()
         kind = (C.c_int * 8)()
         ks = (C.c_int64 * 40)()
@@ -229,7 +247,7 @@ class TurtleHIP(TrainGraph, TurtleParams):
 
     # ---------------------------------------------------------------------------------------
     def set_option(self, name: str, value: int):
-        """Kernel-selection switch (turtle_set_option): 'fuse', 'panel_gemm', 'gemm_lds', 'pwdw', 'sab_tile', 'sab_mfma', 'stem_mfma', 'dw_rows', 'blaslt'. Same results."""
+        """Kernel-selection switch (turtle_set_option): 'fuse', 'panel_gemm', 'gemm_lds', 'sab_mfma', 'stem_mfma', 'dw_rows', 'blaslt', .... Same results."""
         if self._handle is None or self._sig is None:
             self.refresh_weights()
         _lib.check(_lib.lib().turtle_set_option(self._handle.h, name.encode(), int(value)))
