@@ -307,10 +307,12 @@ void launch_attn_finalize(const AttnFinArgs& a, hipStream_t st) {
 }
 
 // Fold the attention into the projection, one block per (32 output channels, 64 key columns,
-// b*h): W_eff[b][o][col(j)] = sum_i Wp[o][h*ch + i] * A[i][j] (A and Wp slabs staged in LDS by
-// coalesced loads), so project_out(A v) becomes one GEMM over the K-concatenated value sources.
+// b*h): W_eff[b][o][col(j)] = sum_i Wp[o][h*ch + i] * A[i][j] (A and Wp slabs staged in LDS), so
+// project_out(A v) becomes one GEMM over the K-concatenated value sources. The launch is tiny
+// (tens of blocks) and latency-bound: every slab load of a thread is issued before the first LDS
+// store (16-byte loads from clamped addresses, zeroed after), one HBM / L2 round trip per block.
 constexpr int WF_MAXCH = 128;
-template <typename T>
+template <typename T, bool V4>
 __global__ __launch_bounds__(256) void attn_weff_kernel(WeffArgs a) {
   __shared__ __attribute__((aligned(16))) float sA[WF_MAXCH][64];
   __shared__ __attribute__((aligned(16))) float sW[WF_MAXCH][32];    // [i][o]
@@ -319,13 +321,50 @@ __global__ __launch_bounds__(256) void attn_weff_kernel(WeffArgs a) {
   const int b = bh / a.heads, h = bh % a.heads;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float* A = a.attn + (int64_t)bh * ch * ncol;
-  for (int e = tid; e < ch * 64; e += 256) {
-    const int i = e >> 6, jj = e & 63;
-    sA[i][jj] = j0 + jj < ncol ? A[i * ncol + j0 + jj] : 0.f;
-  }
-  for (int e = tid; e < 32 * ch; e += 256) {
-    const int oo = e / ch, i = e - oo * ch;
-    sW[i][oo] = o0 + oo < a.C ? a.wp[(int64_t)(o0 + oo) * a.C + h * ch + i] : 0.f;
+  if constexpr (V4) {
+    // A slab [ch][64]: 16 float4 per row; Wp slab [32][ch]: ch / 4 float4 per output row
+    constexpr int NA = WF_MAXCH * 16 / 256, NW = 32 * WF_MAXCH / 4 / 256;
+    const int nwr = ch / 4;                                    // float4 per Wp row
+    float4 ra[NA], rw[NW];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int e = tid + 256 * k, i = min(e >> 4, ch - 1), c = min(j0 + (e & 15) * 4, ncol - 4);
+      ra[k] = *reinterpret_cast<const float4*>(A + (int64_t)i * ncol + c);
+    }
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int e = tid + 256 * k, oo = e / nwr, i4 = e - oo * nwr;
+      const int o = min(o0 + oo, a.C - 1);
+      rw[k] = *reinterpret_cast<const float4*>(a.wp + (int64_t)o * a.C + h * ch + min(i4, nwr - 1) * 4);
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int e = tid + 256 * k, i = e >> 4, jj = (e & 15) * 4;
+      if (i < ch) {
+        const bool ok = j0 + jj < ncol;
+        *reinterpret_cast<float4*>(&sA[i][jj]) = ok ? ra[k] : float4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+      const int e = tid + 256 * k, oo = e / nwr, i4 = e - oo * nwr;
+      if (oo < 32) {
+        const bool ok = o0 + oo < a.C;
+        sW[4 * i4][oo] = ok ? rw[k].x : 0.f;
+        sW[4 * i4 + 1][oo] = ok ? rw[k].y : 0.f;
+        sW[4 * i4 + 2][oo] = ok ? rw[k].z : 0.f;
+        sW[4 * i4 + 3][oo] = ok ? rw[k].w : 0.f;
+      }
+    }
+  } else {
+    for (int e = tid; e < ch * 64; e += 256) {
+      const int i = e >> 6, jj = e & 63;
+      sA[i][jj] = j0 + jj < ncol ? A[i * ncol + j0 + jj] : 0.f;
+    }
+    for (int e = tid; e < 32 * ch; e += 256) {
+      const int oo = e / ch, i = e - oo * ch;
+      sW[i][oo] = o0 + oo < a.C ? a.wp[(int64_t)(o0 + oo) * a.C + h * ch + i] : 0.f;
+    }
   }
   __syncthreads();
   const int jj = lane, og = wid * 8;
@@ -358,8 +397,10 @@ __global__ __launch_bounds__(256) void attn_weff_kernel(WeffArgs a) {
 template <typename T>
 void launch_weff(const WeffArgs& a, hipStream_t st) {
   const int ncol = a.nseg * a.ch;
-  hipLaunchKernelGGL(attn_weff_kernel<T>, dim3((unsigned)((a.C + 31) / 32), (unsigned)((ncol + 63) / 64), (unsigned)(a.B * a.heads)),
-                     dim3(256), 0, st, a);
+  const dim3 grid((unsigned)((a.C + 31) / 32), (unsigned)((ncol + 63) / 64), (unsigned)(a.B * a.heads));
+  // 16-byte slab loads need 4-aligned rows: ch, C (and so ncol) multiples of 4
+  if (a.ch % 4 == 0 && a.C % 4 == 0 && a.ch <= WF_MAXCH) hipLaunchKernelGGL((attn_weff_kernel<T, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_weff_kernel<T, false>), grid, dim3(256), 0, st, a);
 }
 
 template void launch_gram<float>(const GramArgs&, hipStream_t);
