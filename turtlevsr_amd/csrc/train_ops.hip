@@ -604,13 +604,34 @@ __global__ __launch_bounds__(256) void rgemm_f32_kernel(const float* __restrict_
     }
 }
 
+// Sum of the split partials: c[i] (+)= sum_k part[k][i]. Block = EL consecutive entries x (256 / EL)
+// split groups; each lane keeps 8 loads in flight and the group sums meet in LDS in a fixed order
+// (deterministic). Few entries with many splits (small weights over many pixels: n = 4096,
+// nsplit = 1024) take EL = 16, i.e. 16 groups, so a thread walks nsplit / 16 partials instead of
+// all of them.
+template <int EL>
 __global__ __launch_bounds__(256) void rgemm_reduce_kernel(const float* __restrict__ part, float* __restrict__ c, int64_t n,
                                                            int nsplit, int accumulate) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  float s = accumulate ? c[i] : 0.f;
-  for (int k = 0; k < nsplit; ++k) s += part[(int64_t)k * n + i];
-  c[i] = s;
+  constexpr int G = 256 / EL;
+  __shared__ float ps[G][EL];
+  const int lane = threadIdx.x % EL, g = threadIdx.x / EL;
+  const int64_t i = (int64_t)blockIdx.x * EL + lane;
+  const float* p = part + (i < n ? i : n - 1);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = g;
+  for (; k + 7 * G < nsplit; k += 8 * G) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += p[(int64_t)(k + u * G) * n];
+  }
+  for (; k < nsplit; k += G) s[0] += p[(int64_t)k * n];
+  ps[g][lane] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (g == 0 && i < n) {
+    float t = accumulate ? c[i] : 0.f;
+#pragma unroll
+    for (int q = 0; q < G; ++q) t += ps[q][lane];
+    c[i] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -901,7 +922,10 @@ int turtle_train_rgemm(const void* a, int64_t lda, const void* b, int64_t ldb, f
     hipLaunchKernelGGL(rgemm_f32_kernel, grid, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, part, img_px,
                        (int)nimg, N, K, P, ppb);
   const int64_t n = nimg * N * K;
-  hipLaunchKernelGGL(rgemm_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, part, c, n, (int)nsplit, accumulate);
+  if ((n + 63) / 64 >= 512)
+    hipLaunchKernelGGL(rgemm_reduce_kernel<64>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, c, n, (int)nsplit, accumulate);
+  else
+    hipLaunchKernelGGL(rgemm_reduce_kernel<16>, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, part, c, n, (int)nsplit, accumulate);
   return (int)hipGetLastError();
 }
 
