@@ -22,6 +22,7 @@ as bf16 (cast in, cast back). There is no CPU path: a CPU tensor or a missing li
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import torch
 
@@ -215,6 +216,43 @@ def _gemm_into(x, ldx, w, img_px, bias, P, K, N):
     return y
 
 
+class _WCast:
+    """A shared weight in the GEMM dtype (`wg`) and its transpose for the input gradient (`wt`,
+    built on first use). One entry per leaf parameter (or a view of one: the [N, K] reshape of a
+    conv weight), reused while the parameter's version is unchanged: the 5 frames of a clip (and
+    the forward / backward of each) stop re-casting and re-transposing the same weight; the
+    optimizer's in-place update bumps the version (a view shares its base's counter)."""
+    __slots__ = ("ref", "version", "dtype", "wg", "wt")
+
+    def __init__(self, base, w, gdt):
+        self.ref, self.version, self.dtype = weakref.ref(base), w._version, gdt
+        self.wg = w.detach().to(gdt).contiguous()
+        self.wt = None
+
+    def transposed(self):
+        if self.wt is None:
+            self.wt = self.wg.transpose(-1, -2).contiguous()
+        return self.wt
+
+
+_WCACHE: dict = {}
+
+
+def _weight_cast(w, gdt):
+    """(wg, entry): the cached cast of a 2-D weight that is a leaf parameter or a view of one, or a
+    fresh cast (entry None) for computed weights (scaled, per-image)."""
+    base = w if w.is_leaf else w._base
+    if w.dim() != 2 or not isinstance(base, torch.nn.Parameter):
+        return w.to(gdt).contiguous(), None
+    key = (id(base), tuple(w.shape), w.stride(), w.storage_offset())
+    e = _WCACHE.get(key)
+    if e is None or e.ref() is not base or e.version != w._version or e.dtype != gdt or e.wg.device != w.device:
+        if len(_WCACHE) > 4096:
+            _WCACHE.clear()
+        e = _WCACHE[key] = _WCast(base, w, gdt)
+    return e.wg, e
+
+
 class _Conv1x1(torch.autograd.Function):
     """y = x W^T + b on NHWC rows; W [N, K] (shared) or [B, N, K] (one set per image)."""
 
@@ -225,7 +263,7 @@ class _Conv1x1(torch.autograd.Function):
         xg, ldx = rows(x.to(gdt))
         B, K, H, W = xg.shape
         N = w.shape[-2]
-        wg = w.to(gdt).contiguous()
+        wg, ctx.wcache = _weight_cast(w, gdt)
         b32 = None if b is None else b.float().contiguous()
         y = _gemm_into(xg, ldx, wg, H * W, b32, B * H * W, K, N)
         ctx.save_for_backward(xg, wg)
@@ -241,7 +279,7 @@ class _Conv1x1(torch.autograd.Function):
         dy, lddy = rows(dy.to(xg.dtype))
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            wt = wg.transpose(-1, -2).contiguous()               # [.., K, N]
+            wt = ctx.wcache.transposed() if ctx.wcache is not None else wg.transpose(-1, -2).contiguous()   # [.., K, N]
             dx = _gemm_into(dy, lddy, wt, HW, None, P, N, K).to(ctx.in_dt)
         if ctx.needs_input_grad[1]:
             if wg.dim() == 3:
