@@ -124,26 +124,27 @@ int turtle_profile_end(TurtleHandle* h, double out[4 * TURTLE_K_COUNT]);
  * region to the one launch shape being measured. */
 int turtle_profile_filter(TurtleHandle* h, const char* tag);
 
-/* Kernel-selection switches (performance A/B only; every setting computes the same function).
- *   "fuse"        1 (default): block-level fused pointwise->depthwise->pointwise kernels where
- *                 the input width is <= 128; 0: separate GEMM + depthwise launches
- *   "panel_gemm"  1 (default): panel GEMM for bf16 plain 1x1 convolutions with K <= 512;
- *                 0: K-loop GEMM everywhere
- *   "gemm_pn"     1 (default): persistent resident-panel bf16 GEMM for 1x1 convolutions with
- *                 K in {64, 128, 256, 384, 512} and N % 64 == 0 (LayerNorm applied to the LDS
- *                 panel in place); 0: the kernels below
- *   "gemm_lds"    1 (default): LDS-pipelined bf16 GEMM (global_load_lds double buffering)
- *                 wherever its alignment rules hold; 0: panel / K-loop GEMMs
- *   "pwdw"        0 (default; 1 = on): pointwise GEMM -> depthwise 3x3 (-> gate) in one kernel for bf16
- *                 input widths that are multiples of 64 not covered by "fuse"; 0: GEMM + depthwise
- *   "stem_mfma"   1 (default): input_projection / ending 3x3 convolutions on the matrix cores (bf16,
- *                 dim 64); 0: VALU kernels
- *   "sab_mfma"    1 (default): SAB sparse A.v on the matrix cores (bf16): per 8x8 query tile the
- *                 ball part is a dense [64 x 256] x [256 x D] product, top-k tail added per query
- *   "sab_tile"    0 (default; 1 = on, when sab_mfma is off or fp32): VALU A.v over 8x8 query
- *                 tiles with the ball key rows staged in LDS; 0: one wave per query
- *   "dw_rows"     1 (default): row-sweeping depthwise 3x3 kernel (rolling 3-row window per
- *                 thread); 0: per-pixel 9-tap gather kernel
+/* Kernel-selection switches (performance A/B only; every setting computes the same function;
+ * defaults in brackets). Names and semantics are those turtle_set_option (turtle.cpp) accepts:
+ *   "fuse"         [1] block-level fused kernels (fused2.hip row walk / fused.hip) for input widths <= 128
+ *   "fused2"       [1] the bf16 row-walk fused kernel (fused2.hip); 0: the round-1 fused.hip kernel
+ *   "ffn"          [1] FeedForward in one kernel (ffn.hip) at widths 64 / 128 (bf16)
+ *   "gemm_pn"      [1] persistent resident-panel GEMM for LN-folded 1x1 convolutions, K <= 512
+ *   "gemm_ar"      [1] A-resident per-panel GEMM for the K = 256 residual projections
+ *   "gemm_kt"      [1] 2-D tiled deep-ring GEMM (3x3 up/down convolutions, K >= 640, small maps)
+ *   "gemm_lds"     [1] LDS-pipelined GEMM (fallback where the kernels above do not apply)
+ *   "panel_gemm"   [1] register-panel GEMM fallback; 0: K-loop GEMM
+ *   "blaslt"       [1] hipBLASLt for the latent-level plain projections it wins (blas.cpp)
+ *   "dwgemm"       [1] depthwise as the operand prologue of the following GEMM (dwgemm.hip)
+ *   "dwgemm_attn"  [1] ... for the level-3 channel attention's v path (W_eff GEMM)
+ *   "dwgemm_cb"    [1] ... for the level-3 GatedFeedForward, hidden map stored channel-blocked
+ *   "dwgemm_min_blocks" [384] minimum block count for a dwgemm launch
+ *   "dw_rows"      [1] row-sweeping depthwise kernel; 0: per-pixel 9-tap gather kernel
+ *   "down_tile"    [1] LDS-tiled level-1 Downsample (spatial.hip)
+ *   "stem_mfma"    [1] input_projection / ending 3x3 on the matrix cores (bf16, dim 64)
+ *   "sab_mfma"     [1] SAB sparse A.v on the matrix cores (bf16)
+ *   "sab_db"       [0] SAB A.v double-buffered at one block per CU; 0: two blocks per CU
+ *   "split_out"    [1] output-adjacent weights (ending, reduce_chan_level1) as split bf16 pairs
  * Unknown names return TURTLE_EINVAL. */
 int turtle_set_option(TurtleHandle* h, const char* name, int value);
 

@@ -1157,15 +1157,21 @@ struct Runner {
       T0KnormArgs ka{kcur, cstride, kpos, B, N, (int)D};
       tag("t0_knorm B=%d N=%d D=%d", B, N, (int)D);
       launch(TURTLE_K_OTHER, ES * ((double)B * N * D * 3 + (double)N * D), 0, [&] { launch_t0_knorm<T>(ka, st); });
-      if (Tnew > 1) {   // keep the last Tnew-1 cached frames (reference: cat then [-ntc:])
+      if (Tnew > 1) {   // keep the last Tnew-1 cached frames (reference: cat then [-ntc:]); in place: no copy
         const int keep = Tnew - 1, first = Tin - keep;
-        tag("sab_cache_shift keep=%d N=%d", keep, N);
-        launch(TURTLE_K_OTHER, 4.0 * ES * B * keep * (double)N * D, 0, [&] {
-          HIPCHK(hipMemcpy2DAsync(kout, (size_t)cstride * ES, kin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
-                                  (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
-          HIPCHK(hipMemcpy2DAsync(vout, (size_t)cstride * ES, vin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
-                                  (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
-        });
+        const bool kin_place = B == 1 && kout == kin + (int64_t)first * N * D;
+        const bool vin_place = B == 1 && vout == vin + (int64_t)first * N * D;
+        if (!kin_place || !vin_place) {
+          tag("sab_cache_shift keep=%d N=%d", keep, N);
+          launch(TURTLE_K_OTHER, 2.0 * ES * B * keep * (double)N * D * ((kin_place ? 0 : 1) + (vin_place ? 0 : 1)), 0, [&] {
+            if (!kin_place)
+              HIPCHK(hipMemcpy2DAsync(kout, (size_t)cstride * ES, kin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
+                                      (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
+            if (!vin_place)
+              HIPCHK(hipMemcpy2DAsync(vout, (size_t)cstride * ES, vin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
+                                      (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
+          });
+        }
       }
       // out = v of every frame, back to pixel-major frames (b, t) -> image b*NT + t
       T0UntokArgs ua{};
@@ -1244,15 +1250,22 @@ struct Runner {
       wa.out = kout + (int64_t)(Tnew - 1) * N * d2; wa.out_img_stride = (int64_t)Tnew * N * d2;
       launch(TURTLE_K_WINDOW, wbytes, wflops, [&] { launch_window<T>(wa, st); });
       // keep the last Tnew-1 cached frames in the new cache (reference: cat then [-ntc:])
+      // (a kept frame already in place - the caller's frame arena, model.py _sab_out - is not copied)
       if (Tnew > 1) {
         const int keep = Tnew - 1, first = Tin - keep;
-        tag("sab_cache_shift keep=%d N=%d", keep, N);
-        launch(TURTLE_K_OTHER, 2.0 * ES * B * keep * (double)N * (d2 + D), 0, [&] {
-          HIPCHK(hipMemcpy2DAsync(kout, (size_t)Tnew * N * d2 * ES, kin + (int64_t)first * N * d2, (size_t)Tin * N * d2 * ES,
-                                  (size_t)keep * N * d2 * ES, B, hipMemcpyDeviceToDevice, st));
-          HIPCHK(hipMemcpy2DAsync(vout, (size_t)Tnew * N * D * ES, vin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
-                                  (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
-        });
+        const bool kin_place = B == 1 && kout == kin + (int64_t)first * N * d2;
+        const bool vin_place = B == 1 && vout == vin + (int64_t)first * N * D;
+        if (!kin_place || !vin_place) {
+          tag("sab_cache_shift keep=%d N=%d", keep, N);
+          launch(TURTLE_K_OTHER, 2.0 * ES * B * keep * (double)N * ((kin_place ? 0 : d2) + (vin_place ? 0 : D)), 0, [&] {
+            if (!kin_place)
+              HIPCHK(hipMemcpy2DAsync(kout, (size_t)Tnew * N * d2 * ES, kin + (int64_t)first * N * d2, (size_t)Tin * N * d2 * ES,
+                                      (size_t)keep * N * d2 * ES, B, hipMemcpyDeviceToDevice, st));
+            if (!vin_place)
+              HIPCHK(hipMemcpy2DAsync(vout, (size_t)Tnew * N * D * ES, vin + (int64_t)first * N * D, (size_t)Tin * N * D * ES,
+                                      (size_t)keep * N * D * ES, B, hipMemcpyDeviceToDevice, st));
+          });
+        }
       }
       if (NT > TURTLE_MAX_T) TFAIL(TURTLE_EINVAL, "too many cached frames");
       SabScoreArgs sa{};

@@ -94,9 +94,17 @@ class TurtleHIP(TrainGraph, TurtleParams):
     def compute_dtype(self) -> torch.dtype:
         return _DT[self._dtype_name][1]
 
+    def __setattr__(self, name, value):
+        # a parameter / submodule (re)assigned on this module invalidates the cached parameter list
+        if isinstance(value, (nn.Parameter, nn.Module)):
+            self.__dict__.pop("_plist", None)
+        super().__setattr__(name, value)
+
     def _signature(self):
-        # parameter list cached once (Parameter objects survive .to() / load_state_dict); the
-        # version sum catches in-place updates, the leading data pointers catch device moves
+        # parameter list cached (Parameter objects survive .to() and in-place loads; it is dropped
+        # by load_state_dict - assign=True swaps the objects -, refresh_weights and attribute
+        # assignment); the version sum catches in-place updates, the leading data pointers catch
+        # device moves and `.data` rebinding
         ps = self.__dict__.get("_plist")
         if ps is None:
             ps = self.__dict__["_plist"] = list(self.parameters())
@@ -105,6 +113,7 @@ class TurtleHIP(TrainGraph, TurtleParams):
     def refresh_weights(self):
         """Pack the current parameters into the device layout (done automatically on change)."""
         L = _lib.lib()
+        self.__dict__.pop("_plist", None)
         dev = next(self.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("TurtleHIP runs on a ROCm device only: call .to('cuda') first")
@@ -116,6 +125,7 @@ class TurtleHIP(TrainGraph, TurtleParams):
             self._handle_dev = dev
             self._ws = None
             self.__dict__["_layouts"] = {}
+            self.__dict__["_arenas"] = {}
         h = self._handle.h
         with torch.cuda.device(dev):
             for name, t in self.state_dict().items():
@@ -127,6 +137,7 @@ class TurtleHIP(TrainGraph, TurtleParams):
     def _load_from_state_dict(self, *args, **kw):
         super()._load_from_state_dict(*args, **kw)
         self._sig = None
+        self.__dict__.pop("_plist", None)
 
     # ---------------------------------------------------------------------------------------
     def cache_layout(self, B: int, H: int, W: int, t_in: List[int]):
@@ -206,8 +217,7 @@ class TurtleHIP(TrainGraph, TurtleParams):
                 k_out[i] = torch.empty_strided(s4, self._fhr_strides(s4), dtype=cdt, device=dev)
                 v_out[i] = torch.empty_strided(s4, self._fhr_strides(s4), dtype=cdt, device=dev)
             elif kind[i] == 2:
-                k_out[i] = torch.empty(kshape[i], dtype=cdt, device=dev)
-                v_out[i] = torch.empty(vshape[i], dtype=cdt, device=dev)
+                k_out[i], v_out[i] = self._sab_out(i, kshape[i], vshape[i], t_in[i], k_in[i], v_in[i], cdt, dev)
         s = 4 if self.sr else 1
         out = torch.empty(B, Cc, H * s, W * s, dtype=torch.float32, device=dev)
         ws = self._workspace(B, H, W, dev)
@@ -224,6 +234,34 @@ class TurtleHIP(TrainGraph, TurtleParams):
         # keep inputs alive until the stream has consumed them (caller-owned caches are freed lazily)
         self._keepalive = (inp, k_in, v_in)
         return out, k_out, v_out
+
+    # SAB history slots (B = 1): the returned k / v are views of a per-slot frame arena, laid out
+    # so that the new cache's kept frames ARE the incoming cache's last frames - the library then
+    # skips the roll copy (turtle.cpp chm: source == destination) and only writes the current frame.
+    # Every arena frame is written once and never again (the history stays immutable for callers
+    # holding older caches); an incoming cache that is not the arena's latest (a branched or
+    # moved history, B > 1) gets a fresh arena that the library fills by copying.
+    _ARENA_EXTRA = 6
+
+    def _sab_out(self, i, ks, vs, tin, kin, vin, cdt, dev):
+        if ks[0] != 1:
+            return torch.empty(ks, dtype=cdt, device=dev), torch.empty(vs, dtype=cdt, device=dev)
+        arenas = self.__dict__.setdefault("_arenas", {})
+        tnew = ks[1]
+        first = tin - (tnew - 1)                  # first incoming frame kept in the new cache
+        a = arenas.get(i)
+        if a is not None and tin > 0 and a["k"].dtype == cdt and a["k"].device == dev and \
+                tuple(a["k"].shape[1:]) == tuple(ks[2:]) and tuple(a["v"].shape[1:]) == tuple(vs[2:]):
+            s0 = a["next"] - tin                  # arena index of the incoming cache's frame 0
+            if s0 >= 0 and s0 + first + tnew <= a["k"].shape[0] and \
+                    kin.data_ptr() == a["k"][s0].data_ptr() and vin.data_ptr() == a["v"][s0].data_ptr():
+                b = s0 + first
+                a["next"] = b + tnew
+                return a["k"][b:b + tnew].unsqueeze(0), a["v"][b:b + tnew].unsqueeze(0)
+        cap = tnew + self._ARENA_EXTRA
+        a = arenas[i] = dict(k=torch.empty((cap,) + tuple(ks[2:]), dtype=cdt, device=dev),
+                             v=torch.empty((cap,) + tuple(vs[2:]), dtype=cdt, device=dev), next=tnew)
+        return a["k"][:tnew].unsqueeze(0), a["v"][:tnew].unsqueeze(0)
 
     @staticmethod
     def _check_caches(kind, kshape, vshape, t_in, k_cached, v_cached):

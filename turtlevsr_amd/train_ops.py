@@ -22,9 +22,8 @@ as bf16 (cast in, cast back). There is no CPU path: a CPU tensor or a missing li
 from __future__ import annotations
 
 import ctypes as C
-import weakref
-
 import torch
+from torch.utils.weak import WeakIdKeyDictionary
 
 from . import _lib
 
@@ -49,6 +48,7 @@ def lib():
     L.turtle_train_rgemm_workspace.argtypes = [i64, ci, ci, i64]
     L.turtle_train_rgemm_workspace.restype = sz
     L.turtle_train_rgemm.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, i64, ci, ci, vp, sz, vp]
+    L.turtle_train_colsumsq.argtypes = [vp, i64, vp, i64, ci, i64, ci, vp]
     _train = L
     return L
 
@@ -219,13 +219,15 @@ def _gemm_into(x, ldx, w, img_px, bias, P, K, N):
 class _WCast:
     """A shared weight in the GEMM dtype (`wg`) and its transpose for the input gradient (`wt`,
     built on first use). One entry per leaf parameter (or a view of one: the [N, K] reshape of a
-    conv weight), reused while the parameter's version is unchanged: the 5 frames of a clip (and
-    the forward / backward of each) stop re-casting and re-transposing the same weight; the
-    optimizer's in-place update bumps the version (a view shares its base's counter)."""
-    __slots__ = ("ref", "version", "dtype", "wg", "wt")
+    conv weight), reused while the parameter's version and storage are unchanged: the 5 frames of
+    a clip (and the forward / backward of each) stop re-casting and re-transposing the same weight;
+    the optimizer's in-place update bumps the version (a view shares its base's counter), a
+    ``p.data = t`` rebinding changes the data pointer. Writes through ``p.data.copy_()`` bump
+    neither: call ``clear_weight_cache()`` after such a write (training ABI)."""
+    __slots__ = ("version", "ptr", "dtype", "wg", "wt")
 
-    def __init__(self, base, w, gdt):
-        self.ref, self.version, self.dtype = weakref.ref(base), w._version, gdt
+    def __init__(self, w, gdt):
+        self.version, self.ptr, self.dtype = w._version, w.data_ptr(), gdt
         self.wg = w.detach().to(gdt).contiguous()
         self.wt = None
 
@@ -235,7 +237,14 @@ class _WCast:
         return self.wt
 
 
-_WCACHE: dict = {}
+# keyed weakly on the base Parameter (identity, not tensor equality): an entry - and the device
+# memory of its casts - goes with its parameter, so `del net` frees everything
+_WCACHE = WeakIdKeyDictionary()
+
+
+def clear_weight_cache():
+    """Drop every cached weight cast (after parameter writes that bypass the version counter)."""
+    _WCACHE.clear()
 
 
 def _weight_cast(w, gdt):
@@ -244,12 +253,13 @@ def _weight_cast(w, gdt):
     base = w if w.is_leaf else w._base
     if w.dim() != 2 or not isinstance(base, torch.nn.Parameter):
         return w.to(gdt).contiguous(), None
-    key = (id(base), tuple(w.shape), w.stride(), w.storage_offset())
-    e = _WCACHE.get(key)
-    if e is None or e.ref() is not base or e.version != w._version or e.dtype != gdt or e.wg.device != w.device:
-        if len(_WCACHE) > 4096:
-            _WCACHE.clear()
-        e = _WCACHE[key] = _WCast(base, w, gdt)
+    per = _WCACHE.get(base)
+    if per is None:
+        per = _WCACHE[base] = {}
+    key = (tuple(w.shape), w.stride(), w.storage_offset())
+    e = per.get(key)
+    if e is None or e.version != w._version or e.ptr != w.data_ptr() or e.dtype != gdt or e.wg.device != w.device:
+        e = per[key] = _WCast(w, gdt)
     return e.wg, e
 
 
