@@ -245,6 +245,23 @@ bool dwgemm_ok(const DwGemmArgs& g);
 int64_t dwgemm_blocks(const DwGemmArgs& g);
 void launch_dwgemm(const DwGemmArgs& g, hipStream_t st);
 
+// tilepd.hip: LN -> pointwise (C = 256) -> depthwise 3x3 (-> gelu gate) with the hidden map kept on
+// chip (bf16 in / out, fp32 accumulation)
+enum TilePdMode { TP_DW = 0, TP_GATE = 2 };
+struct TilePdArgs {
+  const void* x; int64_t ldx; int offx; int C;   // input [nimg][H][W][ldx], C channels at offx
+  int nimg, H, W;
+  const void* w1; int N1;                        // [N1][C] bf16 (LayerNorm-folded when ln)
+  int ln, centred;                               // LayerNorm prologue; centred: WithBias (BiasFree: x * rstd)
+  const float* tb;                               // [N1] GEMM1 epilogue W1 b_ln + b1 (null: 0)
+  const void* dww16; const float* dwb;           // [9][N1] bf16 taps, [N1] fp32 bias or null
+  int mode;                                      // TP_GATE: hid = N1 / 2 outputs gelu(dw h1) * dw h2; TP_DW: N1 outputs
+  void* out; int64_t ldo; int offo;              // [nimg][H][W][ldo] bf16
+  int dbg;                                       // tools/tpbench ablations (0 in the product path)
+};
+bool tilepd_ok(const TilePdArgs& a);
+int64_t tilepd_blocks(const TilePdArgs& a);
+void launch_tilepd(const TilePdArgs& a, hipStream_t st);
 
 struct FfnArgs {                   // ffn.hip: out = x + g2 * (W2 gelu(LN-folded W1 x) + b2), bf16, C in {64, 128}
   const void* x; void* out;        // [M][C] pixel-major; out may alias x

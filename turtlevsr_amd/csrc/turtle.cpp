@@ -326,6 +326,8 @@ struct TurtleHandle {
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
   int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
+  bool tilepd = true;                                 // level-3 LN -> pointwise -> depthwise (-> gate) in one kernel (tilepd.hip)
+  int tilepd_min_blocks = 256;                        // one block per CU: below one full round the GEMM + dw path stays
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
   bool down_tile = true;                              // level-1 Downsample as the LDS-tiled conv kernel (spatial.hip down_tile_kernel)
@@ -914,6 +916,28 @@ struct Runner {
            2.0 * px * N * K + 18.0 * px * cin, [&] { launch_dwgemm(a, st); });
     return true;
   }
+  // LN -> pointwise -> depthwise (-> gate) with the hidden map on chip (tilepd.hip), input width 256
+  // (shape-only, same in the dry run)
+  bool can_tilepd(int c, int n1, int nimg, int H, int Wd) const {
+    if (ES != 2 || !h->tilepd || c != 256 || n1 % 32 || n1 > 1536) return false;
+    TilePdArgs a{};
+    a.nimg = nimg; a.H = H; a.W = Wd;
+    return tilepd_blocks(a) >= h->tilepd_min_blocks;
+  }
+  void tilepd(int mode, const GemmW& w1, const DwW& dwp, const T* x, int c, T* out, int64_t ldo, int nimg, int H, int Wd) {
+    if (dry()) return;
+    TilePdArgs a{};
+    a.x = x; a.ldx = c; a.offx = 0; a.C = c; a.nimg = nimg; a.H = H; a.W = Wd;
+    a.w1 = h->ptr(w1.w); a.N1 = w1.N; a.ln = w1.ln ? 1 : 0; a.centred = h->arch.cfg.layernorm_biasfree ? 0 : 1;
+    a.tb = w1.ln ? h->fptr(w1.tb) : h->fptr(w1.bias);
+    a.dww16 = h->ptr(dwp.w16); a.dwb = h->fptr(dwp.bias); a.mode = mode;
+    a.out = out; a.ldo = ldo; a.offo = 0;
+    if (dwp.C != w1.N || w1.K != c) TFAIL(TURTLE_EINVAL, "tilepd: depthwise / pointwise widths disagree");
+    if (!tilepd_ok(a)) TFAIL(TURTLE_EINVAL, "tilepd: arguments outside the kernel's contract");
+    const double px = (double)nimg * H * Wd, nout = mode == TP_GATE ? w1.N / 2 : w1.N;
+    tag("tilepd mode=%d nimg=%d H=%d W=%d C=%d N1=%d", mode, nimg, H, Wd, c, w1.N);
+    launch(TURTLE_K_FUSED, ES * px * (c + nout), 2.0 * px * c * w1.N + 18.0 * px * w1.N, [&] { launch_tilepd(a, st); });
+  }
   // FeedForward in one kernel (ffn.hip): bf16, widths 64 / 128 (shape-only, same in the dry run)
   bool can_ffn(int c) const { return ES == 2 && h->ffn && (c == 64 || c == 128); }
   void ffn(const BlockW& bw, T* x, int64_t P, int c) {
@@ -1007,7 +1031,12 @@ struct Runner {
       T* t2 = buf(P * 3 * c);
       const int ch = c / b.heads;
       std::vector<Seg> segs{{t2, 3 * c, c, ch, 1, 0, 1, 0, ch}};
-      if (!can_fuse(c, F_DWONLY, 3 * c, 0) && can_dwgemm_v(c, B, H, Wd)) {
+      if (!can_fuse(c, F_DWONLY, 3 * c, 0) && can_tilepd(c, 3 * c, B, H, Wd)) {
+        // LN -> qkv -> qkv_dwconv in one kernel (the 3c-channel qkv map never reaches HBM), then the
+        // Gram and the W_eff GEMM over the depthwised q, k, v
+        tilepd(TP_DW, bw.a_in, bw.a_dw, x, c, t2, 3 * c, B, H, Wd);
+        chan_attn(bw, b, t2, 3 * c, 0, segs, src1(t2, 3 * c, 2 * c, c), HW, Wd, x, nullptr, -1);
+      } else if (!can_fuse(c, F_DWONLY, 3 * c, 0) && can_dwgemm_v(c, B, H, Wd)) {
         // qkv GEMM, depthwise of q,k only; v's depthwise runs inside the W_eff GEMM (dwgemm.hip)
         T* t1 = buf(P * 3 * c);
         gemm(bw.a_in, src1(x, c, 0, c), P, HW, Wd, t1, 3 * c, 0);
@@ -1030,6 +1059,12 @@ struct Runner {
       if (can_fuse(c, F_GATE, 2 * hd, hd)) {
         fused(F_GATE, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, &bw.f_out, x, xalt, {});
         std::swap(x, xalt);
+      } else if (can_tilepd(c, 2 * hd, B, H, Wd)) {
+        // LN -> project_in -> dwconv -> gelu gate in one kernel (the 2h-channel hidden map stays on
+        // chip), G [P][h] -> project_out GEMM with the residual
+        T* t2 = buf(P * hd);
+        tilepd(TP_GATE, bw.f_in, bw.f_dw, x, c, t2, hd, B, H, Wd);
+        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
       } else if (can_dwgemm_cb(c, hd, B, H, Wd)) {
         // project_in stores the hidden map channel-blocked ([2 hd / 16][P][16]): each dwgemm K step
         // then reads contiguous 32-byte pixel rows
@@ -1531,6 +1566,8 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
       if (h->loaded) pack_all(h);
     }
     else if (n == "ffn") h->ffn = value != 0;
+    else if (n == "tilepd") h->tilepd = value != 0;
+    else if (n == "tilepd_min_blocks") h->tilepd_min_blocks = (int)value;
     else if (n == "down_tile") h->down_tile = value != 0;
     else if (n == "sab_db") h->sab_db = value != 0;
     else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;
