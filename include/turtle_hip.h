@@ -135,6 +135,11 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
  *   "gemm_lds"     [1] LDS-pipelined GEMM (fallback where the kernels above do not apply)
  *   "panel_gemm"   [1] register-panel GEMM fallback; 0: K-loop GEMM
  *   "blaslt"       [1] hipBLASLt for the latent-level plain projections it wins (blas.cpp)
+ *   "tilepd"       [1] level-3 LN -> pointwise -> depthwise with the hidden map on chip (tilepd.hip:
+ *                  channel-attention qkv + qkv_dwconv)
+ *   "tilepd_gate"  [0] ... also the GatedFeedForward's project_in + dwconv + gelu gate (slower than pn + dwgemm)
+ *   "tilepd_cb"    [1] its GatedFeedForward output channel-blocked for the project_out GEMM
+ *   "tilepd_min_blocks" [256] minimum tile count for a tilepd launch (one block per CU)
  *   "dwgemm"       [1] depthwise as the operand prologue of the following GEMM (dwgemm.hip)
  *   "dwgemm_attn"  [1] ... for the level-3 channel attention's v path (W_eff GEMM)
  *   "dwgemm_cb"    [1] ... for the level-3 GatedFeedForward, hidden map stored channel-blocked

@@ -4,7 +4,7 @@
 //         -L turtlevsr_amd/lib -lturtle_hip -Wl,-rpath,turtlevsr_amd/lib -o tools/tpbench
 //   ./tools/tpbench [reps] [only-shape]
 // Prints the average launch time (HIP events) of the product kernel and of its ablations (dbg bits:
-// 1 no GEMM1, 2 no depthwise / gate, 4 stores to the sink line, 8 no LayerNorm pass).
+// 1 no GEMM1, 2 no depthwise / gate, 8 no LayerNorm, 16 no stores - results folded into a checksum).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -72,9 +72,9 @@ int main(int argc, char** argv) {
     TilePdArgs a{};
     a.x = dx; a.ldx = C; a.offx = 0; a.C = C; a.nimg = 1; a.H = sh.H; a.W = sh.W;
     a.w1 = dw; a.N1 = sh.N1; a.ln = 1; a.centred = 1; a.tb = (const float*)dtb; a.dww16 = dt; a.dwb = nullptr;
-    a.mode = sh.mode; a.out = dout; a.ldo = nout; a.offo = 0;
+    a.mode = sh.mode; a.out = dout; a.ldo = nout; a.offo = 0; a.cb_px = sh.mode == TP_GATE ? P : 0;
     const double flops = 2.0 * P * C * sh.N1 + 18.0 * P * sh.N1, bytes = 2.0 * P * (C + nout);
-    const int dbgs[] = {0, 1, 2, 4, 8, 1 | 2, 1 | 2 | 4, 2 | 4};
+    const int dbgs[] = {0, 1, 2, 8, 3, 16, 17, 18, 19, 24};
     for (int d : dbgs) {
       a.dbg = d;
       const float us = time_it([&] { launch_tilepd(a, 0); }, reps);

@@ -235,4 +235,5 @@ struct SrcList {
   SrcDesc s[TURTLE_MAX_SRC];
   int n;
   int Ktot;
+  int64_t cb_px;   // > 0: the (single) source is channel-blocked [Ktot / 16][cb_px][16] (base, off 0), 2-D tiled GEMM only
 };

@@ -529,6 +529,7 @@ static void launch_panel(const GemmArgs& g, hipStream_t st) {
 
 // the panel kernel applies to bf16 plain stores with K <= 512 (one LDS panel)
 static bool panel_ok(const GemmArgs& g) {
+  if (g.a.cb_px) return false;                   // channel-blocked operand: 2-D tiled kernel only
   // 32-bit in-panel offsets: rows x leading dimension must stay below 2^31 elements
   const int64_t big = (int64_t)1 << 30;
   return g.allow_panel && !g.conv3 && g.store_mode == STORE_NHWC && g.N % 16 == 0 && g.a.Ktot % 8 == 0 && g.a.Ktot >= 8 &&
@@ -558,6 +559,11 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
   if (g.store_mode == STORE_CB16) {                // produced only for the pn kernel (turtle.cpp)
     if (sizeof(T) != 2 || !gemm_pn_ok(g)) kernel_arg_error("channel-blocked GEMM store needs the bf16 pn kernel");
     launch_gemm_pn(g, st);
+    return;
+  }
+  if (g.a.cb_px) {                                 // channel-blocked operand (tilepd.hip): 2-D tiled kernel only
+    if (sizeof(T) != 2 || !gemm_kt_ok(g)) kernel_arg_error("channel-blocked GEMM operand needs the bf16 2-D tiled kernel");
+    launch_gemm_kt(g, st);
     return;
   }
   if constexpr (sizeof(T) == 2) {

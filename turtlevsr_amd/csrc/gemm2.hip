@@ -337,6 +337,7 @@ __global__ __launch_bounds__(256, 2) void gemm_lds_kernel(GemmArgs g) {
 // Eligible: bf16, every 16-byte operand chunk inside one source and 16-byte aligned, N % 8 == 0
 // (whole 16-byte output chunks; PixelShuffle needs N/4 % 8 == 0), conv3 taps aligned to BK.
 bool gemm_lds_ok(const GemmArgs& g) {
+  if (g.a.cb_px) return false;                   // channel-blocked operand: 2-D tiled kernel only
   if (!g.allow_lds || g.N % 8 || g.ldo % 8 || g.offo % 8) return false;
   // measured (tools/kbench, MI355X): the panel kernel stays ahead for LayerNorm GEMMs with K <= 256
   // (its single panel load amortises the statistics), this kernel wins everywhere else

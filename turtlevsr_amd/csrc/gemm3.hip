@@ -367,6 +367,7 @@ static size_t pn_lds_bytes(int bm, int kp, int N, bool scale) {
 static int pn_wn(int N, bool res) { return (N % 256 == 0 && !res) ? 8 : (N % 128 == 0 ? 4 : 2); }
 
 bool gemm_pn_ok(const GemmArgs& g) {
+  if (g.a.cb_px) return false;                   // channel-blocked operand: 2-D tiled kernel only
   if (!g.allow_pn || g.conv3) return false;
   if (g.store_mode == STORE_CB16) {
     if (g.res || g.offo || g.N % 16 || g.cb_px != g.M || g.scale) return false;
@@ -627,6 +628,7 @@ static ArCfg ar_cfg(int K) {
 }
 
 bool gemm_ar_ok(const GemmArgs& g) {
+  if (g.a.cb_px) return false;                   // channel-blocked operand: 2-D tiled kernel only
   if (!g.allow_ar || g.conv3 || g.store_mode != STORE_NHWC || g.gelu || g.scale) return false;
   const ArCfg c = ar_cfg(g.a.Ktot);
   if (!c.bm || g.N % (64 * c.ntw) || g.N > 8192) return false;

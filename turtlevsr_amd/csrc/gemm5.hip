@@ -157,7 +157,9 @@ __global__ __launch_bounds__(WM * WN * 64, (WM * WN <= 4) ? 2 : 1) void gemm_kt_
       const bool inb = !g.conv3 || (y >= 0 && y < Himg && x >= 0 && x < g.Wimg);
       const bool ok = a_ok[i] && inb && k0 + a_cc[i] < K;
       const int pix = (a_img[i] * smul + sadd) * g.HW + a_p[i] + dy * g.Wimg + dx;
-      const bf16* src = base + (int64_t)pix * sld + soff + a_cc[i];
+      // channel-blocked source: channel k of pixel p at ((k / 16) cb_px + p) 16 + k % 16
+      const bf16* src = g.a.cb_px ? base + ((((int64_t)((k0 + a_cc[i]) >> 4) * g.a.cb_px + pix) << 4) + ((k0 + a_cc[i]) & 15))
+                                  : base + (int64_t)pix * sld + soff + a_cc[i];
       kt_dma16(ok ? reinterpret_cast<const void*>(src) : reinterpret_cast<const void*>(g_zero_kt), sA + (i * NW + wid) * 1024);
     }
 #pragma unroll
@@ -326,6 +328,9 @@ bool gemm_kt_ok(const GemmArgs& g) {
   if (reinterpret_cast<uintptr_t>(g.out) % 16 || reinterpret_cast<uintptr_t>(g.w) % 16 ||
       (g.res && reinterpret_cast<uintptr_t>(g.res) % 16))
     return false;
+  if (g.a.cb_px)                                  // channel-blocked A (tilepd.hip output): one plain source
+    return !g.conv3 && g.a.n == 1 && g.a.s[0].off == 0 && g.a.s[0].img_mul == 1 && g.a.s[0].img_add == 0 &&
+           g.a.Ktot % 16 == 0 && g.a.cb_px >= g.M && reinterpret_cast<uintptr_t>(g.a.s[0].base) % 16 == 0;
   if (g.conv3) return g.cin % 32 == 0 && g.a.n == 1 && g.a.s[0].ld % 8 == 0 && g.a.s[0].off % 8 == 0;
   for (int j = 0; j < g.a.n; ++j) {
     if (g.a.s[j].K % 8 || g.a.s[j].ld % 8 || g.a.s[j].off % 8 || reinterpret_cast<uintptr_t>(g.a.s[j].base) % 16) return false;

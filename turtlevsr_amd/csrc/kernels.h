@@ -256,7 +256,8 @@ struct TilePdArgs {
   const float* tb;                               // [N1] GEMM1 epilogue W1 b_ln + b1 (null: 0)
   const void* dww16; const float* dwb;           // [9][N1] bf16 taps, [N1] fp32 bias or null
   int mode;                                      // TP_GATE: hid = N1 / 2 outputs gelu(dw h1) * dw h2; TP_DW: N1 outputs
-  void* out; int64_t ldo; int offo;              // [nimg][H][W][ldo] bf16
+  void* out; int64_t ldo; int offo;              // [nimg][H][W][ldo] bf16 (cb_px == 0)
+  int64_t cb_px;                                 // > 0: channel-blocked output [channels / 16][cb_px][16] (ldo / offo unused)
   int dbg;                                       // tools/tpbench ablations (0 in the product path)
 };
 bool tilepd_ok(const TilePdArgs& a);

@@ -326,7 +326,10 @@ struct TurtleHandle {
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
   int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
-  bool tilepd = true;                                 // level-3 LN -> pointwise -> depthwise (-> gate) in one kernel (tilepd.hip)
+  bool tilepd = true;                                 // level-3 LN -> qkv -> qkv_dwconv in one kernel (tilepd.hip)
+  bool tilepd_gate = false;                           // ... and the GatedFeedForward's project_in -> dwconv -> gate (slower
+                                                      // than the pn GEMM + dwgemm pair it replaces: profiles/r04h_*)
+  bool tilepd_cb = true;                              // tilepd GATE output channel-blocked (read by the 2-D tiled GEMM)
   int tilepd_min_blocks = 256;                        // one block per CU: below one full round the GEMM + dw path stays
   bool ffn = true;                                    // FeedForward as one kernel at widths 64 / 128 (ffn.hip)
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
@@ -765,8 +768,8 @@ struct Runner {
       gl.a = src1(xn, a.Ktot, 0, a.Ktot); gl.ln = 0; gl.ln_s = gl.ln_t = nullptr; gl.bias = h->fptr(w.tb);
     }
     const bool lt = ln_cand ? use_blas(gl) : use_blas(g);
-    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
-        res != nullptr, store, a.n, lt ? " lt" : "");
+    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
+        res != nullptr, store, a.n, a.cb_px ? " cb" : "", lt ? " lt" : "");
     launch(TURTLE_K_GEMM, bytes + (ln_cand && lt ? 2.0 * ES * M * a.Ktot : 0.0), 2.0 * M * g.N * a.Ktot, [&] {
       if (lt && ln_cand) {
         LnRowsArgs la{a.s[0].base, a.s[0].ld, a.s[0].off, xn, a.Ktot, M, a.Ktot, h->arch.cfg.layernorm_biasfree ? 0 : 1};
@@ -783,7 +786,7 @@ struct Runner {
   // prologue, activation, scale, 3x3 or multi-source operand; K >= 512, or <= 140k pixels x >= 256
   // output channels. Per-image weight sets (W_eff) run one call per image.
   bool use_blas(const GemmArgs& g) {
-    if (ES != 2 || !h->blaslt || g.conv3 || g.ln || g.gelu || g.scale || g.store_mode != STORE_NHWC || g.a.n != 1)
+    if (ES != 2 || !h->blaslt || g.a.cb_px || g.conv3 || g.ln || g.gelu || g.scale || g.store_mode != STORE_NHWC || g.a.n != 1)
       return false;
     const SrcDesc& s = g.a.s[0];
     if (s.img_mul != 1 || s.img_add != 0 || s.K != g.a.Ktot) return false;
@@ -924,14 +927,15 @@ struct Runner {
     a.nimg = nimg; a.H = H; a.W = Wd;
     return tilepd_blocks(a) >= h->tilepd_min_blocks;
   }
-  void tilepd(int mode, const GemmW& w1, const DwW& dwp, const T* x, int c, T* out, int64_t ldo, int nimg, int H, int Wd) {
+  void tilepd(int mode, const GemmW& w1, const DwW& dwp, const T* x, int c, T* out, int64_t ldo, int nimg, int H, int Wd,
+              int64_t cb_px = 0) {
     if (dry()) return;
     TilePdArgs a{};
     a.x = x; a.ldx = c; a.offx = 0; a.C = c; a.nimg = nimg; a.H = H; a.W = Wd;
     a.w1 = h->ptr(w1.w); a.N1 = w1.N; a.ln = w1.ln ? 1 : 0; a.centred = h->arch.cfg.layernorm_biasfree ? 0 : 1;
     a.tb = w1.ln ? h->fptr(w1.tb) : h->fptr(w1.bias);
     a.dww16 = h->ptr(dwp.w16); a.dwb = h->fptr(dwp.bias); a.mode = mode;
-    a.out = out; a.ldo = ldo; a.offo = 0;
+    a.out = out; a.ldo = ldo; a.offo = 0; a.cb_px = cb_px;
     if (dwp.C != w1.N || w1.K != c) TFAIL(TURTLE_EINVAL, "tilepd: depthwise / pointwise widths disagree");
     if (!tilepd_ok(a)) TFAIL(TURTLE_EINVAL, "tilepd: arguments outside the kernel's contract");
     const double px = (double)nimg * H * Wd, nout = mode == TP_GATE ? w1.N / 2 : w1.N;
@@ -1059,12 +1063,17 @@ struct Runner {
       if (can_fuse(c, F_GATE, 2 * hd, hd)) {
         fused(F_GATE, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, &bw.f_out, x, xalt, {});
         std::swap(x, xalt);
-      } else if (can_tilepd(c, 2 * hd, B, H, Wd)) {
+      } else if (h->tilepd_gate && can_tilepd(c, 2 * hd, B, H, Wd)) {
         // LN -> project_in -> dwconv -> gelu gate in one kernel (the 2h-channel hidden map stays on
         // chip), G [P][h] -> project_out GEMM with the residual
+        // (G channel-blocked [h / 16][P][16]: a unit's output row is one 448-byte run; the 2-D tiled
+        // GEMM reads it as its A operand)
         T* t2 = buf(P * hd);
-        tilepd(TP_GATE, bw.f_in, bw.f_dw, x, c, t2, hd, B, H, Wd);
-        gemm(bw.f_out, src1(t2, hd, 0, hd), P, HW, Wd, x, c, 0, x, c, 0);
+        const bool cb = h->tilepd_cb && h->gemm_kt;      // the channel-blocked operand needs the 2-D tiled GEMM
+        tilepd(TP_GATE, bw.f_in, bw.f_dw, x, c, t2, hd, B, H, Wd, cb ? P : 0);
+        SrcList gs = src1(t2, hd, 0, hd);
+        gs.cb_px = cb ? P : 0;
+        gemm(bw.f_out, gs, P, HW, Wd, x, c, 0, x, c, 0);
       } else if (can_dwgemm_cb(c, hd, B, H, Wd)) {
         // project_in stores the hidden map channel-blocked ([2 hd / 16][P][16]): each dwgemm K step
         // then reads contiguous 32-byte pixel rows
@@ -1567,6 +1576,8 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     }
     else if (n == "ffn") h->ffn = value != 0;
     else if (n == "tilepd") h->tilepd = value != 0;
+    else if (n == "tilepd_cb") h->tilepd_cb = value != 0;
+    else if (n == "tilepd_gate") h->tilepd_gate = value != 0;
     else if (n == "tilepd_min_blocks") h->tilepd_min_blocks = (int)value;
     else if (n == "down_tile") h->down_tile = value != 0;
     else if (n == "sab_db") h->sab_db = value != 0;
