@@ -254,8 +254,12 @@ def gen_train(t1):
     the 0 * sum(p) term. Stores the loss and, per parameter, its gradient's checksum + samples
     (full tensors for a few)."""
     torch.set_num_threads(8)
+    only = [a for a in sys.argv[1:] if a.startswith("train_")]
     for name, opt, shape, seed in [("train_tiny", tiny_opt(), (2, 4, 3, 64, 64), 21),
-                                   ("train_tiny_hetero", tiny_opt(**HETERO), (1, 4, 3, 64, 64), 22)]:
+                                   ("train_tiny_hetero", tiny_opt(**HETERO), (1, 4, 3, 64, 64), 22),
+                                   ("train_gopro", gopro_opt(), (1, 2, 3, 64, 64), 23)]:
+        if only and name not in only:
+            continue
         torch.manual_seed(0)
         model = t1.make_model(opt).train()
         fill(model, seed)
@@ -303,8 +307,8 @@ if __name__ == "__main__":
         gen_blocks(t1)
     if "clips" in which:
         gen_clips(t1, sr)
-    if "train" in which:
-        gen_train(t1)
+    if "train" in which or any(w.startswith("train_") for w in which):
+        gen_train(t1)   # `gen_golden.py train_gopro`: that fixture only
     named = [w for w in which if w.startswith("clip_")]   # e.g. `gen_golden.py clip_gopro_256`
     if named:
         gen_clips(t1, sr, only=named)

@@ -49,7 +49,7 @@ def _check_grads(net, g, rtol, atol):
     return n
 
 
-@pytest.mark.parametrize("name", ["train_tiny", "train_tiny_hetero"])
+@pytest.mark.parametrize("name", ["train_tiny", "train_tiny_hetero", "train_gopro"])
 def test_graph_gradients_match_reference(name):
     torch.set_num_threads(8)
     g, meta = load(name)
@@ -308,9 +308,10 @@ def test_hip_train_ops_match_autograd(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["train_tiny", "train_tiny_hetero"])
+@pytest.mark.parametrize("name", ["train_tiny", "train_tiny_hetero", "train_gopro"])
 def test_hip_training_graph_matches_reference_gradients(name):
-    """fp32 on the GPU with the HIP kernels: loss and every parameter gradient vs the reference."""
+    """fp32 on the GPU with the HIP kernels: loss and every parameter gradient vs the reference
+    (train_gopro: GoPro widths, 59 M parameters, 2 frames of 64x64 with BPTT through the caches)."""
     g, meta = load(name)
     net = _net(meta, None, "cuda")                   # default op set: HipOps
     tr = Trainer(net, amp=None)
@@ -395,3 +396,33 @@ def test_dropin_module_reference_loop_gpu_fp32_and_fp16():
     with torch.no_grad():
         out, _, _ = net.eval()(torch.stack([lq[:, 0], lq[:, 0]], 1).float())
     assert torch.isfinite(out).all()
+
+
+@pytest.mark.gpu
+def test_config5_bf16_step_8x5x256_through_trainer():
+    """SURVEY §8 config 5 as specified: the GoPro network, B = 8 clips x 5 frames of 256x256 per GPU,
+    one bf16-autocast step through Trainer (video_restoration_model.py:78-108). Loss and every
+    gradient finite; the first-step loss equals the same graph on the ATen op set (torch ops, same
+    device, same bf16 autocast) to bf16 tolerance; AdamW moves the weights."""
+    import yaml
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "options",
+                           "Turtle_Deblur_Gopro.yml")) as f:
+        opt = yaml.safe_load(f)
+    lq = torch.from_numpy(synthetic_frames((8, 5, 3, 256, 256), 51, name="lq")).cuda()
+    gt = (lq + 0.05 * torch.from_numpy(synthetic_frames((8, 5, 3, 256, 256), 52, name="gt")).cuda()).clamp(0, 1)
+    ref_net = _net(dict(opt=opt, seed=5), AtenOps, "cuda")
+    with torch.no_grad():
+        l_aten = float(Trainer(ref_net, amp="bf16").loss(lq, gt))
+    del ref_net
+    net = _net(dict(opt=opt, seed=5), None, "cuda")
+    tr = Trainer(net, amp="bf16", lr=1e-4)
+    before = {k: p.detach().clone() for k, p in net.named_parameters()}
+    loss = tr.loss(lq, gt)
+    (loss + 0 * sum(p.sum() for p in net.parameters())).backward()
+    torch.cuda.synchronize()
+    l_hip = float(loss.detach())
+    assert np.isfinite(l_hip) and l_hip == pytest.approx(l_aten, rel=2e-2), (l_hip, l_aten)
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in net.parameters())
+    tr.opt.step()
+    moved = sum(int(not torch.equal(before[k], p.detach())) for k, p in net.named_parameters())
+    assert moved > 0.9 * len(before)

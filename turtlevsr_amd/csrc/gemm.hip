@@ -556,8 +556,10 @@ static void launch_cfg(const GemmArgs& g, hipStream_t st) {
 
 template <typename T>
 void launch_gemm(const GemmArgs& g, hipStream_t st) {
-  if (g.store_mode == STORE_CB16) {                // produced only for the pn kernel (turtle.cpp)
-    if (sizeof(T) != 2 || !gemm_pn_ok(g)) kernel_arg_error("channel-blocked GEMM store needs the bf16 pn kernel");
+  if (g.store_mode == STORE_CB16) {                // produced only for the pn / g8 kernels (turtle.cpp)
+    if constexpr (sizeof(T) == 2)
+      if (gemm8_ok(g)) { launch_gemm8(g, st); return; }
+    if (sizeof(T) != 2 || !gemm_pn_ok(g)) kernel_arg_error("channel-blocked GEMM store needs the bf16 pn or g8 kernel");
     launch_gemm_pn(g, st);
     return;
   }
@@ -567,6 +569,7 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
     return;
   }
   if constexpr (sizeof(T) == 2) {
+    if (gemm8_ok(g)) { launch_gemm8(g, st); return; }   // allow_g8: the caller's per-shape choice (turtle.cpp)
     // measured per shape class (tools/kbench, MI355X): the 2-D tiled kernel for the resampling 3x3
     // convolutions and K >= 640 (incl. the five-source W_eff GEMM), the A-resident kernel for the
     // K = 256 residual projections, else the persistent panel kernel

@@ -40,6 +40,7 @@ struct GemmArgs {
   int dbg;                         // tools/kbench ablations of the pn kernel (0 in the product path)
   unsigned long long* stamps;      // tools/kbench s_memtime stamps of the pn kernel (null in the product path)
   int64_t cb_px;                   // STORE_CB16: pixels per 16-channel block (= M)
+  int allow_g8;                    // 256 x 256 four-phase kernel permitted (turtle_set_option "gemm8")
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
 bool gemm_lds_ok(const GemmArgs& g);                              // gemm2.hip (bf16)
@@ -50,6 +51,8 @@ bool gemm_ar_ok(const GemmArgs& g);                               // gemm3.hip (
 void launch_gemm_ar(const GemmArgs& g, hipStream_t st);
 bool gemm_kt_ok(const GemmArgs& g);                               // gemm5.hip (bf16)
 void launch_gemm_kt(const GemmArgs& g, hipStream_t st);
+bool gemm8_ok(const GemmArgs& g);                                 // gemm8.hip (bf16)
+void launch_gemm8(const GemmArgs& g, hipStream_t st);
 
 enum DwMode { DW_PLAIN = 0, DW_GELU = 1, DW_GATE = 2 };
 struct DwArgs {

@@ -321,6 +321,8 @@ struct TurtleHandle {
   bool gemm_pn = true;                                // resident-panel bf16 GEMM, K <= 512 (gemm3.hip)
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
+  int gemm8 = 0;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 in place of
+                                                      // hipBLASLt, 2 every eligible projection
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   bool sab_db = false;                                // SAB A.v: double-buffered 1-block/CU variant (else 2 blocks / CU)
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
@@ -754,7 +756,7 @@ struct Runner {
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store; g.cb_px = store == STORE_CB16 ? M : 0;
     g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel; g.allow_lds = h->gemm_lds; g.allow_pn = h->gemm_pn;
     g.allow_ar = h->gemm_ar; g.allow_kt = h->gemm_kt;
-    if (store == STORE_CB16 && (ES != 2 || !gemm_pn_ok(g)))
+    if (store == STORE_CB16 && (ES != 2 || !gemm_pn_ok(g)) && !(ES == 2 && h->gemm8 == 2 && gemm8_ok((g.allow_g8 = 1, g))))
       TFAIL(TURTLE_EINVAL, "channel-blocked store needs the pn GEMM (M " + std::to_string(M) + " N " + std::to_string(g.N) +
                                " K " + std::to_string(a.Ktot) + " HW " + std::to_string(HW) + ")");
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
@@ -767,9 +769,14 @@ struct Runner {
     if (ln_cand) {
       gl.a = src1(xn, a.Ktot, 0, a.Ktot); gl.ln = 0; gl.ln_s = gl.ln_t = nullptr; gl.bias = h->fptr(w.tb);
     }
-    const bool lt = ln_cand ? use_blas(gl) : use_blas(g);
-    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
-        res != nullptr, store, a.n, a.cb_px ? " cb" : "", lt ? " lt" : "");
+    bool lt = ln_cand ? use_blas(gl) : use_blas(g);
+    if (ES == 2 && h->gemm8) {
+      g.allow_g8 = 1;
+      if (gemm8_ok(g) && (h->gemm8 == 2 || lt)) lt = false;
+      else g.allow_g8 = 0;
+    }
+    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s%s%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
+        res != nullptr, store, a.n, a.cb_px ? " cb" : "", lt ? " lt" : "", g.allow_g8 ? " g8" : "");
     launch(TURTLE_K_GEMM, bytes + (ln_cand && lt ? 2.0 * ES * M * a.Ktot : 0.0), 2.0 * M * g.N * a.Ktot, [&] {
       if (lt && ln_cand) {
         LnRowsArgs la{a.s[0].base, a.s[0].ld, a.s[0].off, xn, a.Ktot, M, a.Ktot, h->arch.cfg.layernorm_biasfree ? 0 : 1};
@@ -1586,6 +1593,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
     else if (n == "gemm_ar") h->gemm_ar = value != 0;
     else if (n == "gemm_kt") h->gemm_kt = value != 0;
+    else if (n == "gemm8") h->gemm8 = (int)value;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
     else if (n == "stem_mfma") h->stem_mfma = value != 0;
     else if (n == "fused2") h->fused2 = value != 0;
