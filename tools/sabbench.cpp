@@ -27,6 +27,7 @@ static uint16_t f2bf(float f) {
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 10;
+  const int waves = argc > 3 ? atoi(argv[3]) : 4;    // ./sabbench reps nsplit(0: default) waves
   const int th = 68, tw = 120, N = th * tw;
   const int ds[] = {128, 256, 512}, Ts[] = {3, 4, 4};
   const int dbgs[] = {0, 1, 3, 7};
@@ -54,7 +55,8 @@ int main(int argc, char** argv) {
     a.q = q; a.q_bstride = 0;
     for (int t = 0; t < T; ++t) { a.k[t] = k[t]; a.k_bstride[t] = 0; }
     a.B = 1; a.T = T; a.N = N; a.d = d; a.th = th; a.tw = tw;
-    a.nsplit = argc > 2 ? atoi(argv[2]) : sab_score_nsplit(1, T, N, d);
+    a.waves = waves;
+    a.nsplit = argc > 2 && atoi(argv[2]) > 0 ? atoi(argv[2]) : sab_score_nsplit(1, T, N, d, waves);
     a.tau = tau;
     CK(hipMalloc(&a.topv, (size_t)T * a.nsplit * N * 5 * 4));
     CK(hipMalloc(&a.topi, (size_t)T * a.nsplit * N * 5 * 4));

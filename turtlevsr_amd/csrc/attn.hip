@@ -303,7 +303,7 @@ void launch_attn_finalize(const AttnFinArgs& a, hipStream_t st) {
   const int ncol = a.nseg * a.ch, stride = a.ch * ncol + a.ch + ncol, nbh = a.B * a.heads;
   hipLaunchKernelGGL(gram_sum_kernel, dim3((unsigned)((stride + 63) / 64), (unsigned)nbh), dim3(256), 0, st, a.part, a.red,
                      a.nchunk, stride);
-  hipLaunchKernelGGL(attn_row_kernel, dim3((unsigned)((a.ch + 3) / 4), (unsigned)nbh), dim3(256), 0, st, a);
+  if (!a.sum_only) hipLaunchKernelGGL(attn_row_kernel, dim3((unsigned)((a.ch + 3) / 4), (unsigned)nbh), dim3(256), 0, st, a);
 }
 
 // Fold the attention into the projection, one block per (32 output channels, 64 key columns,
@@ -403,9 +403,137 @@ void launch_weff(const WeffArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL((attn_weff_kernel<T, false>), grid, dim3(256), 0, st, a);
 }
 
+// attn_row_kernel folded into the W_eff kernel (one launch fewer per attention site, the attention
+// matrix never written): every block stages its head's reduced Gram sums (ch x ncol <= 8192 floats)
+// and norms in LDS with all loads in flight at once, recomputes the row softmax over all ncol key
+// columns and keeps its own 64 columns; the Wp slab loads are in flight meanwhile. Same per-element
+// arithmetic as attn_row_kernel + attn_weff_kernel<T, true>.
+constexpr int WFF_MAXG = 8192, WFF_MAXCOL = 128;
+template <typename T>
+__global__ __launch_bounds__(256) void attn_weff_fin_kernel(WeffArgs a, AttnFinArgs f) {
+  __shared__ __attribute__((aligned(16))) float sA[WF_MAXCH][64];
+  __shared__ __attribute__((aligned(16))) float sW[WF_MAXCH][32];    // [i][o]
+  __shared__ __attribute__((aligned(16))) float sG[WFF_MAXG];        // [i][j] Gram sums
+  __shared__ float sN[256];                                          // |q_i|^2, then |k_j|^2
+  __shared__ float sX[4 * 256];                                      // sink of the out-of-range slab stores
+  const int ch = a.ch, ncol = a.nseg * ch, stride = ch * ncol + ch + ncol;
+  const int o0 = blockIdx.x * 32, j0 = blockIdx.y * 64, bh = blockIdx.z;
+  const int b = bh / a.heads, h = bh % a.heads;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float* R = f.red + (int64_t)bh * stride;
+  const float tau = f.tau[h];
+  // every load of the block first: Wp slab [32][ch], the Gram slab, the norms
+  constexpr int NW = 32 * WF_MAXCH / 4 / 256, NG = WFF_MAXG / 4 / 256;
+  const int nwr = ch / 4, ng4 = ch * ncol / 4;
+  float4 rw[NW], rg[NG];
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const int e = tid + 256 * k, oo = e / nwr, i4 = e - oo * nwr;
+    const int o = min(o0 + oo, a.C - 1);
+    rw[k] = *reinterpret_cast<const float4*>(a.wp + (int64_t)o * a.C + h * ch + min(i4, nwr - 1) * 4);
+  }
+#pragma unroll
+  for (int k = 0; k < NG; ++k) rg[k] = *reinterpret_cast<const float4*>(R + 4 * min(tid + 256 * k, ng4 - 1));
+  const float rn = R[ch * ncol + min(tid, ch + ncol - 1)];
+  // unconditional LDS stores (entries past the slab are never read; out-of-range W rows go to the
+  // sink): a store under a branch would pull its load down next to it, one L2 round trip each
+#pragma unroll
+  for (int k = 0; k < NG; ++k) *reinterpret_cast<float4*>(&sG[4 * (tid + 256 * k)]) = rg[k];
+  sN[tid] = rn;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const int e = tid + 256 * k, oo = e / nwr, i4 = e - oo * nwr;
+    const bool ok = o0 + oo < a.C;
+    float* d0 = oo < 32 ? &sW[4 * i4][oo] : &sX[tid];
+    const int st = oo < 32 ? 32 : 256;
+    d0[0] = ok ? rw[k].x : 0.f;
+    d0[st] = ok ? rw[k].y : 0.f;
+    d0[2 * st] = ok ? rw[k].z : 0.f;
+    d0[3 * st] = ok ? rw[k].w : 0.f;
+  }
+  __syncthreads();
+  // column scales (the same for every row): 1 / |k_j| for normalised segments
+  constexpr int KC = WFF_MAXCOL / 64;
+  float kv[KC];
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const int jc = min(lane + 64 * k, ncol - 1), sgm = jc / ch;
+    kv[k] = ((f.norm_mask >> sgm) & 1) ? 1.f / fmaxf(sqrtf(sN[ch + jc]), 1e-12f) : 1.f;
+  }
+  if (blockIdx.x == 0 && f.kinv && f.cur_seg >= 0 && wid == 0) {
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int j = lane + 64 * k;
+      if (j >= j0 && j < j0 + 64 && j >= f.cur_seg * ch && j < (f.cur_seg + 1) * ch)
+        f.kinv[(int64_t)b * a.heads * ch + h * ch + (j - f.cur_seg * ch)] = kv[k];
+    }
+  }
+  for (int i = wid; i < ch; i += 4) {
+    const float qn = tau / fmaxf(sqrtf(sN[i]), 1e-12f);
+    float lg[KC];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      const int j = lane + 64 * k;
+      lg[k] = j < ncol ? sG[i * ncol + min(j, ncol - 1)] * qn * kv[k] : -INFINITY;
+      mx = fmaxf(mx, lg[k]);
+    }
+    mx = wave_max(mx);
+    float sum = 0.f, mine = 0.f;
+#pragma unroll
+    for (int k = 0; k < KC; ++k) {
+      lg[k] = lane + 64 * k < ncol ? expf(lg[k] - mx) : 0.f;
+      sum += lg[k];
+      mine = (int)blockIdx.y == k ? lg[k] : mine;
+    }
+    const float inv = 1.f / wave_sum(sum);
+    sA[i][lane] = j0 + lane < ncol ? mine * inv : 0.f;
+  }
+  __syncthreads();
+  const int jj = lane, og = wid * 8;
+  float acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = 0.f;
+  for (int i = 0; i < ch; ++i) {
+    const float av = sA[i][jj];
+    const float4 w0 = *reinterpret_cast<const float4*>(&sW[i][og]);
+    const float4 w1 = *reinterpret_cast<const float4*>(&sW[i][og + 4]);
+    acc[0] = fmaf(w0.x, av, acc[0]); acc[1] = fmaf(w0.y, av, acc[1]);
+    acc[2] = fmaf(w0.z, av, acc[2]); acc[3] = fmaf(w0.w, av, acc[3]);
+    acc[4] = fmaf(w1.x, av, acc[4]); acc[5] = fmaf(w1.y, av, acc[5]);
+    acc[6] = fmaf(w1.z, av, acc[6]); acc[7] = fmaf(w1.w, av, acc[7]);
+  }
+  const int col = j0 + jj;
+  if (col >= ncol) return;
+  const int sg = col / ch, j = col - sg * ch;
+  int64_t scol = a.seg_col[0];
+  int shs = a.seg_hstride[0];
+#pragma unroll
+  for (int q = 1; q < TURTLE_MAX_SEG; ++q)
+    if (sg == q) { scol = a.seg_col[q]; shs = a.seg_hstride[q]; }
+  T* W = reinterpret_cast<T*>(a.weff) + (int64_t)b * a.C * a.Keff + scol + (int64_t)h * shs + j;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (o0 + og + u < a.C) W[(int64_t)(o0 + og + u) * a.Keff] = from_f<T>(acc[u]);
+}
+
+bool weff_fin_ok(const WeffArgs& a) {
+  const int ncol = a.nseg * a.ch;
+  return a.ch % 4 == 0 && a.C % 4 == 0 && a.ch <= WF_MAXCH && ncol <= WFF_MAXCOL && a.ch * ncol <= WFF_MAXG;
+}
+
+template <typename T>
+void launch_weff_fin(const WeffArgs& a, const AttnFinArgs& f, hipStream_t st) {
+  const int ncol = a.nseg * a.ch;
+  const dim3 grid((unsigned)((a.C + 31) / 32), (unsigned)((ncol + 63) / 64), (unsigned)(a.B * a.heads));
+  hipLaunchKernelGGL((attn_weff_fin_kernel<T>), grid, dim3(256), 0, st, a, f);
+}
+
 template void launch_gram<float>(const GramArgs&, hipStream_t);
 template void launch_gram<bf16>(const GramArgs&, hipStream_t);
 template void launch_weff<float>(const WeffArgs&, hipStream_t);
 template void launch_weff<bf16>(const WeffArgs&, hipStream_t);
+template void launch_weff_fin<float>(const WeffArgs&, const AttnFinArgs&, hipStream_t);
+template void launch_weff_fin<bf16>(const WeffArgs&, const AttnFinArgs&, hipStream_t);
 
 }  // namespace turtle

@@ -101,9 +101,10 @@ struct SabScoreArgs {
   int* topi;
   float* ballv;                    // [B*T][N][41] scores of the L1-ball keys (|di|+|dj| <= 4)
   int dbg;                         // tools/sabbench ablations (0 in the product path)
+  int waves;                       // 4 or 8 waves (64 / 128 queries) per block; 0 = 4
 };
 template <typename T> void launch_sab_score(const SabScoreArgs& a, hipStream_t st);
-int sab_score_nsplit(int B, int T, int N, int d);
+int sab_score_nsplit(int B, int T, int N, int d, int waves = 4);
 
 constexpr int SAB_MAXC = 48;       // candidate slots per query (41 ball + 5 top-k, padded)
 struct SabPrepArgs {               // candidates + clipped softmax per (b, t, query)
@@ -149,6 +150,7 @@ struct AttnFinArgs {               // per-row Gram reduction + softmax
   int cur_seg;
   float* red;                      // scratch [B*heads][ch*ncol + ch + ncol] summed partials
   float* attn;                     // [B*heads][ch][ncol]
+  int sum_only;                    // 1: only the reduction (the softmax runs inside attn_weff_fin)
 };
 void launch_attn_finalize(const AttnFinArgs& a, hipStream_t st);
 int attn_nsplit(int nchunk);
@@ -163,6 +165,10 @@ struct WeffArgs {                  // W_eff[b][o][col] = sum_i Wp[o][h*ch+i] * A
   void* weff;                      // [B][C][Keff] storage type
 };
 template <typename T> void launch_weff(const WeffArgs& a, hipStream_t st);
+// row softmax + W_eff in one launch (reads f.red, ignores a.attn): needs ch % 4 == 0, C % 4 == 0,
+// ch <= 128, ncol <= 128, ch * ncol <= 8192
+bool weff_fin_ok(const WeffArgs& a);
+template <typename T> void launch_weff_fin(const WeffArgs& a, const AttnFinArgs& f, hipStream_t st);
 
 struct FhrCacheArgs {              // latent FHR cache roll: keep last Rnew rows of [old R ; cur ch]
   const void* old; int R;          // [B][P][heads][R] (R may be 0)

@@ -126,10 +126,14 @@ TURTLE_DEV int div_tw(int m, int tw, float inv) {
 // key tiles of KT rows are staged in a 2-slot LDS ring (register staging, one barrier per tile).
 // QG = 2 would let every staged key fragment feed two query groups (half the L2 -> LDS key traffic).
 // ------------------------------------------------------------------------------------------
-template <typename T, int KT, int QK, int QG>
-__global__ __launch_bounds__(256) void sab_score_kernel(SabScoreArgs a) {
+// NWQ waves per block (4 or 8): with 8, one staged key tile feeds 128 queries instead of 64, which
+// halves the key stream from L2 / the Infinity Cache (the key set of a 1080p frame, 8 MB at d = 512,
+// does not fit one XCD's L2)
+template <typename T, int KT, int QK, int QG, int NWQ = 4>
+__global__ __launch_bounds__(NWQ * 64) void sab_score_kernel(SabScoreArgs a) {
   using FR = typename Frag<T>::type;
-  constexpr int KF = Frag<T>::K, VEC = Vec<T>::N, ES = sizeof(T), MT = KT / 16, QB = 64 * QG;
+  constexpr int NT = NWQ * 64;
+  constexpr int KF = Frag<T>::K, VEC = Vec<T>::N, ES = sizeof(T), MT = KT / 16, QB = 16 * NWQ * QG;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ROW = a.d * ES + 16;
   char* sK0 = smem;
@@ -183,14 +187,14 @@ __global__ __launch_bounds__(256) void sab_score_kernel(SabScoreArgs a) {
   const int ntile = (N + KT - 1) / KT;
   const int tb = ks * ntile / a.nsplit, te = (ks + 1) * ntile / a.nsplit;
   const int cv = d / VEC;                      // vectors per key row
-  constexpr int NVMAX = KT * (QK * KF / VEC) / 256;
-  const int nv = KT * cv / 256;                // staged vectors per thread (<= NVMAX)
+  constexpr int NVMAX = KT * (QK * KF / VEC) / NT;
+  const int nv = KT * cv / NT;                 // staged vectors per thread (<= NVMAX)
   uint4 stg[NVMAX];
   auto load_tile = [&](int it) {
 #pragma unroll
     for (int i = 0; i < NVMAX; ++i) {
       if (i < nv) {
-        const int v = tid + 256 * i, r = v / cv, e = (v - r * cv) * VEC;
+        const int v = tid + NT * i, r = v / cv, e = (v - r * cv) * VEC;
         const int m = min(it * KT + r, N - 1);
         stg[i] = ld16(k + (int64_t)m * d + e);
       }
@@ -200,7 +204,7 @@ __global__ __launch_bounds__(256) void sab_score_kernel(SabScoreArgs a) {
 #pragma unroll
     for (int i = 0; i < NVMAX; ++i) {
       if (i < nv) {
-        const int v = tid + 256 * i, r = v / cv, e = (v - r * cv) * VEC;
+        const int v = tid + NT * i, r = v / cv, e = (v - r * cv) * VEC;
         *reinterpret_cast<uint4*>(dst + r * ROW + e * ES) = stg[i];
       }
     }
@@ -313,34 +317,42 @@ __global__ __launch_bounds__(256) void sab_score_kernel(SabScoreArgs a) {
 // SIMD and the halved grid needs more key splits, i.e. more top-5 warm-ups); kept for tuning.
 static int sab_qg(int) { return 1; }
 
-int sab_score_nsplit(int B, int T, int N, int d) {
+int sab_score_nsplit(int B, int T, int N, int d, int waves) {
   // as many key splits as keep the whole grid resident in one round: each split restarts the
   // top-5 warm-up, a second round of blocks costs more than the split saves (tools/sabbench:
   // d = 128 / T = 3 / N = 8160 best at 2 splits = 768 blocks = 3 per CU, d >= 256 at 1)
-  const int qb = 64 * sab_qg(d);
+  const int nw = waves == 8 ? 8 : 4;
+  const int qb = 16 * nw * sab_qg(d);
   const int blocks = B * T * ((N + qb - 1) / qb);
-  const int cap = 256 * (d <= 128 ? 3 : 2);        // resident score blocks on MI355X (LDS / VGPRs)
+  const int cap = 256 * (d <= 128 ? 3 : 2) * 4 / nw;   // resident score blocks on MI355X (LDS / VGPRs)
   const int ntile = (N + 63) / 64;
   return std::max(1, std::min(cap / std::max(1, blocks), std::min(8, ntile)));
 }
 
-template <typename T, int KT, int QK, int QG>
+template <typename T, int KT, int QK, int QG, int NWQ = 4>
 static void launch_score_cfg(const SabScoreArgs& a, hipStream_t st) {
-  const size_t lds = 2 * (size_t)KT * (a.d * sizeof(T) + 16) + 64 * QG * 4 * SAB_K * 8;
-  const int nqt = (a.N + 64 * QG - 1) / (64 * QG);
+  constexpr int QB = 16 * NWQ * QG;
+  const size_t lds = 2 * (size_t)KT * (a.d * sizeof(T) + 16) + QB * 4 * SAB_K * 8;
+  const int nqt = (a.N + QB - 1) / QB;
   static bool attr = false;                        // > 64 KB of dynamic LDS must be opted into
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_score_kernel<T, KT, QK, QG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_score_kernel<T, KT, QK, QG, NWQ>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL((sab_score_kernel<T, KT, QK, QG>), dim3((unsigned)(a.B * a.T * nqt * a.nsplit)), dim3(256), lds, st, a);
+  hipLaunchKernelGGL((sab_score_kernel<T, KT, QK, QG, NWQ>), dim3((unsigned)(a.B * a.T * nqt * a.nsplit)), dim3(NWQ * 64), lds, st, a);
 }
 
 template <typename T>
 void launch_sab_score(const SabScoreArgs& a, hipStream_t st) {
   // d = 2c in {128, 256, 512} for the GoPro widths; K tiles of 64 keys (32 at d = 512: LDS ring)
   constexpr int KF = Frag<T>::K;
+  if (a.waves == 8) {
+    if (a.d <= 128) launch_score_cfg<T, 64, 128 / KF, 1, 8>(a, st);
+    else if (a.d <= 256) launch_score_cfg<T, 64, 256 / KF, 1, 8>(a, st);
+    else launch_score_cfg<T, 32, 512 / KF, 1, 8>(a, st);
+    return;
+  }
   if (a.d <= 128) launch_score_cfg<T, 64, 128 / KF, 1>(a, st);
   else if (a.d <= 256) launch_score_cfg<T, 64, 256 / KF, 1>(a, st);
   else launch_score_cfg<T, 32, 512 / KF, 1>(a, st);

@@ -321,6 +321,8 @@ struct TurtleHandle {
   bool gemm_pn = true;                                // resident-panel bf16 GEMM, K <= 512 (gemm3.hip)
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
+  int sab_waves = 4;                                  // waves per SAB score block: 4 (64 queries) or 8 (128)
+  bool attn_fin = true;                               // channel-attention softmax rows inside the W_eff kernel (attn.hip)
   int gemm8 = 0;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 in place of
                                                       // hipBLASLt, 2 every eligible projection
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
@@ -1004,11 +1006,13 @@ struct Runner {
     we.attn = attn; we.wp = h->fptr(bw.wp); we.B = B; we.heads = b.heads; we.ch = ch; we.nseg = nseg; we.C = c;
     for (int s = 0; s < nseg; ++s) { we.seg_col[s] = segs[s].col; we.seg_hstride[s] = segs[s].colh; }
     we.Keff = vsrc.Ktot; we.weff = weff;
-    tag("attn_rows nbh=%d ch=%d ncol=%d nchunk=%d", B * b.heads, ch, ncol, nchunk);
+    const bool fin = h->attn_fin && weff_fin_ok(we);   // softmax rows inside the W_eff launch
+    f.sum_only = fin;
+    tag("attn_rows nbh=%d ch=%d ncol=%d nchunk=%d%s", B * b.heads, ch, ncol, nchunk, fin ? " sum" : "");
     launch(TURTLE_K_ATTN, 4.0 * B * b.heads * (double)nchunk * stride, 0, [&] { launch_attn_finalize(f, st); });
-    tag("weff B=%d C=%d heads=%d ncol=%d", B, c, b.heads, ncol);
+    tag("weff B=%d C=%d heads=%d ncol=%d%s", B, c, b.heads, ncol, fin ? " fin" : "");
     launch(TURTLE_K_ATTN, ES * (double)B * c * vsrc.Ktot + 4.0 * B * b.heads * ch * ncol, 2.0 * B * c * (double)b.heads * ncol * ch,
-           [&] { launch_weff<T>(we, st); });
+           [&] { if (fin) launch_weff_fin<T>(we, f, st); else launch_weff<T>(we, st); });
     if (vdw) {
       // v's depthwise folded into the W_eff GEMM's operand prologue (dwgemm.hip): out = x + W_eff dw(v) + b
       if (!dwgemm(*vdw, 0, vraw, ldv, offv, B, HW / Wimg, Wimg, c, weff, c, (int64_t)c * c, c, h->fptr(bw.po_bias), x, c,
@@ -1266,9 +1270,11 @@ struct Runner {
     T* q2f = buf(P * d2);
     T* k2f = buf(P * d2);
     T* qtok = buf((int64_t)B * N * d2);
-    const int nsplit = sab_score_nsplit(B, NT, N, d2);
-    float* topv = fbuf((int64_t)B * NT * nsplit * N * 5);
-    int* topi = reinterpret_cast<int*>(fbuf((int64_t)B * NT * nsplit * N * 5));
+    const int nsplit = sab_score_nsplit(B, NT, N, d2, h->sab_waves);
+    // partial lists sized for either block size, so the sab_waves switch never changes the workspace
+    const int nsplit_ws = std::max(sab_score_nsplit(B, NT, N, d2, 4), sab_score_nsplit(B, NT, N, d2, 8));
+    float* topv = fbuf((int64_t)B * NT * nsplit_ws * N * 5);
+    int* topi = reinterpret_cast<int*>(fbuf((int64_t)B * NT * nsplit_ws * N * 5));
     float* ballv = fbuf((int64_t)B * NT * N * 41);
     int* ccnt = reinterpret_cast<int*>(fbuf((int64_t)B * NT * N));
     int* cidx = reinterpret_cast<int*>(fbuf((int64_t)B * NT * N * SAB_MAXC));
@@ -1321,7 +1327,7 @@ struct Runner {
       if (NT > TURTLE_MAX_T) TFAIL(TURTLE_EINVAL, "too many cached frames");
       SabScoreArgs sa{};
       sa.q = qtok; sa.q_bstride = (int64_t)N * d2; sa.B = B; sa.T = NT; sa.N = N; sa.d = d2;
-      sa.th = th; sa.tw = tw; sa.nsplit = nsplit;
+      sa.th = th; sa.tw = tw; sa.nsplit = nsplit; sa.waves = h->sab_waves;
       sa.tau = h->fptr(bw.sab_tau); sa.topv = topv; sa.topi = topi; sa.ballv = ballv;
       SabGatherArgs ga{};
       ga.B = B; ga.T = NT; ga.N = N; ga.th = th; ga.tw = tw; ga.ws = ws; ga.C = c;
@@ -1594,6 +1600,8 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm_ar") h->gemm_ar = value != 0;
     else if (n == "gemm_kt") h->gemm_kt = value != 0;
     else if (n == "gemm8") h->gemm8 = (int)value;
+    else if (n == "attn_fin") h->attn_fin = value != 0;
+    else if (n == "sab_waves") h->sab_waves = (int)value;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
     else if (n == "stem_mfma") h->stem_mfma = value != 0;
     else if (n == "fused2") h->fused2 = value != 0;
