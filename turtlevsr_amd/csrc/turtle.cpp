@@ -322,7 +322,7 @@ struct TurtleHandle {
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
   int sab_waves = 4;                                  // waves per SAB score block: 4 (64 queries) or 8 (128)
-  bool attn_fin = true;                               // channel-attention softmax rows inside the W_eff kernel (attn.hip)
+  bool attn_fin = false;                              // channel-attention softmax rows inside the W_eff kernel (attn.hip)
   int gemm8 = 0;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 in place of
                                                       // hipBLASLt, 2 every eligible projection
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
