@@ -31,6 +31,8 @@
 //   * weight rows are placed in LDS in pn's permuted order (MFMA row 4g+e of sub-tile s <- channel
 //     8g+4s+e of a 32-channel group) by choosing each DMA lane's source row, so a lane's
 //     accumulators hold 8 CONSECUTIVE channels of one pixel: 16-byte residual loads and stores.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -350,6 +352,358 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   }
 }
 
+// ---- persistent form ("g8p"): one block per CU walks tiles lin, lin + G, .. as ONE stream of K
+// tiles (step s = tile-local index x nk + t), so the four-phase schedule never drains: the units of
+// the next tile's first two K tiles are in flight during the current tile's last phases and its
+// epilogue. Per tile, the epilogue's per-channel vectors (LN s / t, bias, scale; 4 x 1 KB) go to an
+// LDS slot by LDS-DMA at phase 1 of the previous tile's last K tile (every wave issues one: waves w
+// and w + 4 copy the same vector), so the epilogue issues no global loads but the residual's. The
+// LN statistics are written to LDS at the tile's last K tile (phase 1 / 3) and read in its
+// epilogue after the phase-4 barrier (each group reads only its own pixel half). Needs nk >= 2
+// (a slot / statistics row is rewritten one K tile after its last read at the earliest).
+constexpr int G8P_VEC = 2 * G8_BUF + 2 * 256 * 4;        // 2 slots x [4 vectors][256] fp32
+constexpr int G8P_BYTES = G8P_VEC + 2 * 4 * 256 * 4;
+
+template <bool LN, bool RES>
+__global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* s_mu = reinterpret_cast<float*>(smem + 2 * G8_BUF);
+  float* s_rs = s_mu + 256;
+  const float* s_vec = reinterpret_cast<const float*>(smem + G8P_VEC);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 2, wn = wid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  const int ntn = (g.N + 255) / 256;
+  const int tpi = g.wstride ? (g.HW + 255) / 256 : 0;
+  const int ntm = g.wstride ? (int)(g.M / g.HW) * tpi : (int)((g.M + 255) / 256);
+  const int ntiles = ntm * ntn;
+  const int G = gridDim.x;
+  int lin = blockIdx.x;
+  {
+    const int q = G / 8, r = G % 8, x = lin % 8, y = lin / 8;
+    lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;
+  }
+  const int K = g.a.Ktot, nk = (K + 63) / 64;
+  const int ntl = (ntiles - lin + G - 1) / G;      // tiles of this block (G <= ntiles)
+  const int nsteps = ntl * nk;
+  // tile-local index -> geometry (wave-uniform; computed once per tile, the divisions are not cheap)
+  struct Geo { int64_t m0, mlim; int n0; int64_t woff; };
+  auto geo = [&](int tl) __attribute__((always_inline)) {
+    Geo r;
+    const int tile = lin + min(tl, ntl - 1) * G;
+    const int nt = tile % ntn, mt = tile / ntn;
+    if (g.wstride) {
+      const int im = mt / tpi;
+      r.m0 = (int64_t)im * g.HW + (int64_t)(mt - im * tpi) * 256;
+      r.mlim = min(g.M, (int64_t)(im + 1) * g.HW);
+      r.woff = (int64_t)(im / g.wdiv) * g.wstride;
+    } else {
+      r.m0 = (int64_t)mt * 256;
+      r.mlim = g.M;
+      r.woff = 0;
+    }
+    r.n0 = nt * 256;
+    return r;
+  };
+
+  // DMA geometry (as gemm8_kernel): unit row of instruction i, source chunk, W channel offsets
+  const int kc = (((lane & 7) ^ (((wid & 1) << 2) | (lane >> 4))) & 7) * 8;
+  // unit row of DMA instruction i: (8 i + wid) 8 + lane / 8 (recomputed per issue: registers)
+  auto unit_row = [&](int i) __attribute__((always_inline)) { return (i * 8 + wid) * 8 + (lane >> 3); };
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  const bf16* W0 = reinterpret_cast<const bf16*>(g.w);
+
+  // unit u of step (tl, t) of tile geometry q; zero line past the block's last step / beyond K
+  auto issue = [&](int tl, int t, const Geo& q, int u) __attribute__((always_inline)) {
+    const int k0 = t * 64;
+    const uint32_t dst = lds_base + ((tl * nk + t) & 1) * G8_BUF + u * G8_UNIT + wid * 1024;
+    const bool live = tl < ntl && k0 + kc < K;
+    const int64_t m0 = q.m0, mlim = q.mlim;
+    const int n0 = q.n0;
+    if (u == U_XA || u == U_XB) {
+      const bf16* base = reinterpret_cast<const bf16*>(g.a.s[0].base);
+      int64_t sld = g.a.s[0].ld;
+      int soff = g.a.s[0].off, kb = 0, kbj = g.a.s[0].K;
+#pragma unroll
+      for (int j = 1; j < TURTLE_MAX_SRC; ++j) {
+        const bool hit = j < g.a.n && k0 >= kbj;
+        base = hit ? reinterpret_cast<const bf16*>(g.a.s[j].base) : base;
+        sld = hit ? g.a.s[j].ld : sld;
+        soff = hit ? g.a.s[j].off : soff;
+        kb = hit ? kbj : kb;
+        kbj += j < g.a.n ? g.a.s[j].K : 0;
+      }
+      const bf16* b2 = base + soff + (k0 - kb) + kc;
+      const int xo = u == U_XA ? 0 : 64;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int io = unit_row(i);
+        const int64_t m = m0 + (io >> 6) * 128 + (io & 63) + xo;
+        const int64_t mc = m < mlim ? m : m0;
+        uint64_t pa = reinterpret_cast<uint64_t>(b2 + mc * sld);
+        asm volatile("" : "+v"(pa));               // computed for every lane, then selected (no branch)
+        g8_dma16(live ? reinterpret_cast<const void*>(pa) : reinterpret_cast<const void*>(g_zero_g8), dst + i * 8192);
+      }
+    } else {
+      const bf16* Wp = W0 + q.woff;
+      const int wo = u == U_WA ? 0 : 32;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int io = unit_row(i);
+        const int n = n0 + (io >> 5) * 64 + g8_perm(wo + (io & 31));
+        uint64_t pa = reinterpret_cast<uint64_t>(Wp + (int64_t)min(n, g.N - 1) * g.ldw + k0 + kc);
+        asm volatile("" : "+v"(pa));
+        g8_dma16(live ? reinterpret_cast<const void*>(pa) : reinterpret_cast<const void*>(g_zero_g8), dst + i * 8192);
+      }
+    }
+  };
+  // per-channel vectors of tile tl -> slot tl & 1: wave w copies vector w & 3 (LN s, LN t, bias,
+  // scale; absent ones from the zero / one lines), lane l channels n0 + 4 l .. (clamped into N)
+  auto issue_vec = [&](int tl, const Geo& q) __attribute__((always_inline)) {
+    const int n0 = q.n0;
+    const int v = wid & 3;
+    const float* src = v == 0 ? g.ln_s : v == 1 ? g.ln_t : v == 2 ? g.bias : g.scale;
+    const float* dflt = v == 3 ? g.ones : g.zeros;
+    const float* p = src ? src + min(n0 + 4 * lane, g.N - 4) : dflt + 4 * lane;
+    g8_dma16(p, lds_base + G8P_VEC + (tl & 1) * 4096 + v * 1024);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int sw = (fr >> 1) & 7;
+  const int loff0 = fr * 128 + ((fq ^ sw) << 4), loff1 = fr * 128 + (((fq ^ sw) ^ 4) << 4);
+  auto frag = [&](const char* unit, int row0, int ks) __attribute__((always_inline)) {
+    return *reinterpret_cast<const bf16x8*>(unit + row0 * 128 + (ks ? loff1 : loff0));
+  };
+
+  float lsum[2] = {0.f, 0.f}, lsq[2] = {0.f, 0.f};
+  auto stats2 = [&](const bf16x8 (&xa)[2], const bf16x8 (&xb)[2]) __attribute__((always_inline)) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const bf16x2 one2 = __builtin_bit_cast(bf16x2, 0x3F803F80u);
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const u32x4 w = __builtin_bit_cast(u32x4, tt ? xb[ks] : xa[ks]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bf16x2 v2 = __builtin_bit_cast(bf16x2, w[e]);
+          lsum[tt] = __builtin_amdgcn_fdot2_f32_bf16(v2, one2, lsum[tt], false);
+          lsq[tt] = __builtin_amdgcn_fdot2_f32_bf16(v2, v2, lsq[tt], false);
+        }
+      }
+  };
+  auto stats = [&](const bf16x8 (&xf)[4][2]) __attribute__((always_inline)) {
+    if (wn & 1) stats2(xf[2], xf[3]);
+    else stats2(xf[0], xf[1]);
+  };
+  // the tile's statistics of this wave's two pixel tiles -> LDS (last K tile), sums reset
+  auto stats_out = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      float a = lsum[tt], q = lsq[tt];
+      a += __shfl_xor(a, 16, 64); a += __shfl_xor(a, 32, 64);
+      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      if (fq == 0) {
+        int fro = fr;                              // opaque: keeps hipcc from hoisting (and spilling)
+        asm volatile("" : "+v"(fro));              // the LDS addresses out of the tile loop
+        const int r = wm * 128 + (wn >= 2 ? 64 : 0) + 16 * (2 * (wn & 1) + tt) + fro;
+        const float mu = a / K;
+        s_mu[r] = mu;
+        s_rs[r] = rsqrtf(fmaxf(q / K - mu * mu, 0.f) + 1e-5f);
+      }
+      lsum[tt] = 0.f; lsq[tt] = 0.f;
+    }
+  };
+
+  // ---- epilogue of tile tl (registers + LDS only, but the residual) ----
+  auto epilogue = [&](int tl, const Geo& q) __attribute__((always_inline)) {
+    const int64_t m0 = q.m0, mlim = q.mlim;
+    const int n0 = q.n0;
+    int fro = fr, fqo = fq;                        // opaque lane indices (see stats_out)
+    asm volatile("" : "+v"(fro), "+v"(fqo));
+    const float* sv = s_vec + (tl & 1) * 1024;
+    bf16* o = reinterpret_cast<bf16*>(g.out);
+    const bf16* res = reinterpret_cast<const bf16*>(g.res);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int cl = wn * 64 + 32 * jj + 8 * fqo, c = n0 + cl;
+      if (c >= g.N) continue;
+      float fs[8], ft[8], fb[8], fc[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(sv + cl + 4 * h);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(sv + 256 + cl + 4 * h);
+        const f32x4 d = *reinterpret_cast<const f32x4*>(sv + 512 + cl + 4 * h);
+        const f32x4 e = *reinterpret_cast<const f32x4*>(sv + 768 + cl + 4 * h);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { fs[4 * h + i] = a[i]; ft[4 * h + i] = b[i]; fb[4 * h + i] = d[i]; fc[4 * h + i] = e[i]; }
+      }
+      uint4 rv[8];
+      if (RES) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int64_t m = m0 + wm * 128 + 16 * i + fro;
+          rv[i] = ld16(res + (m < mlim ? m : m0) * g.ldr + g.offr + c);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = wm * 128 + 16 * i + fro;
+        const int64_t m = m0 + r;
+        if (m >= mlim) continue;
+        const float mu = LN ? s_mu[r] : 0.f, rs = LN ? s_rs[r] : 1.f;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float x = acc[i][2 * jj + (e >> 2)][e & 3];
+          if (LN) x = rs * (x - mu * fs[e]) + ft[e];
+          x += fb[e];
+          if (g.gelu) x = gelu_bf16(x);
+          v[e] = x * fc[e];
+        }
+        if (RES) {
+          const uint32_t rw[4] = {rv[i].x, rv[i].y, rv[i].z, rv[i].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] += __uint_as_float(rw[e] << 16);
+            v[2 * e + 1] += __uint_as_float(rw[e] & 0xffff0000u);
+          }
+        }
+        bf16x8 ov;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+        const int64_t dst = g.store_mode == STORE_CB16 ? ((((int64_t)(c >> 4) * g.cb_px + m) << 4) + (c & 15)) : m * g.ldo + g.offo + c;
+        *reinterpret_cast<bf16x8*>(o + dst) = ov;
+      }
+    }
+  };
+
+  // ---- prologue: the first tile's vectors, then X-a, W-a, W-b, X-b of step 0, X-a, W-a of step 1 ----
+  // (steps 0 and 1 belong to tile 0: nk >= 2)
+  Geo q0 = geo(0);
+  issue_vec(0, q0);
+  issue(0, 0, q0, U_XA); issue(0, 0, q0, U_WA); issue(0, 0, q0, U_WB); issue(0, 0, q0, U_XB); issue(0, 1, q0, U_XA); issue(0, 1, q0, U_WA);
+  g8_vm<8>();
+  __builtin_amdgcn_s_barrier();
+  if (wm == 1) __builtin_amdgcn_s_barrier();
+
+#define G8_MFMA_BEGIN                                   \
+  __builtin_amdgcn_sched_barrier(0);                    \
+  __builtin_amdgcn_s_barrier();                         \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    \
+  __builtin_amdgcn_sched_barrier(0);                    \
+  __builtin_amdgcn_s_setprio(1);
+#define G8_MFMA_END                                     \
+  __builtin_amdgcn_s_setprio(0);                        \
+  __builtin_amdgcn_sched_barrier(0);                    \
+  __builtin_amdgcn_s_barrier();                         \
+  asm volatile("" ::: "memory");                        \
+  __builtin_amdgcn_sched_barrier(0);
+
+  // (tl, t) of steps s, s + 1, s + 2
+  int tl0 = 0, t0 = 0, tl1 = nk > 1 ? 0 : 1, t1 = nk > 1 ? 1 : 0;
+  int tl2 = t1 + 1 < nk ? tl1 : tl1 + 1, t2 = t1 + 1 < nk ? t1 + 1 : 0;
+  Geo q1 = tl1 == 0 ? q0 : geo(tl1), q2 = tl2 == tl1 ? q1 : geo(tl2);
+  bf16x8 xf[4][2], wa[2][2], wb[2][2];
+  for (int s = 0; s < nsteps; ++s) {
+    const char* ub = smem + (s & 1) * G8_BUF;
+    const bool last = t0 == nk - 1;                // the tile's last K tile
+    const bool vnext = t1 == 0;                    // step s + 1 starts a tile: its vectors go out at P1
+    // P1: X-a, W-a -> pixel tiles 0-3 x channel tiles 0-1
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) xf[i][ks] = frag(ub + U_XA * G8_UNIT, wm * 64 + 16 * i, ks);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) wa[j][ks] = frag(ub + U_WA * G8_UNIT, wn * 32 + 16 * j, ks);
+    g8_vm<6>();
+    if (vnext) issue_vec(tl1, q1);
+    issue(tl1, t1, q1, U_WB);
+    G8_MFMA_BEGIN
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][ks], xf[i][ks], acc[i][j], 0, 0, 0);
+    if (LN && wn < 2) {
+      stats(xf);
+      if (last) stats_out();
+    }
+    G8_MFMA_END
+    // P2: W-b -> pixel tiles 0-3 x channel tiles 2-3 (one more DMA outstanding after a vector issue)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) wb[j][ks] = frag(ub + U_WB * G8_UNIT, wn * 32 + 16 * j, ks);
+    if (vnext) g8_vm<7>(); else g8_vm<6>();
+    issue(tl1, t1, q1, U_XB);
+    G8_MFMA_BEGIN
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[j][ks], xf[i][ks], acc[i][2 + j], 0, 0, 0);
+    G8_MFMA_END
+    // P3: X-b -> pixel tiles 4-7 x channel tiles 2-3
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) xf[i][ks] = frag(ub + U_XB * G8_UNIT, wm * 64 + 16 * i, ks);
+    if (vnext) g8_vm<7>(); else g8_vm<6>();
+    issue(tl2, t2, q2, U_XA);
+    G8_MFMA_BEGIN
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[j][ks], xf[i][ks], acc[4 + i][2 + j], 0, 0, 0);
+    if (LN && wn >= 2) {
+      stats(xf);
+      if (last) stats_out();
+    }
+    G8_MFMA_END
+    // P4: (no reads) -> pixel tiles 4-7 x channel tiles 0-1
+    if (vnext) g8_vm<7>(); else g8_vm<6>();
+    issue(tl2, t2, q2, U_WA);
+    G8_MFMA_BEGIN
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][ks], xf[i][ks], acc[4 + i][j], 0, 0, 0);
+    G8_MFMA_END
+    if (last) {
+      epilogue(tl0, q0);
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    tl0 = tl1; t0 = t1; tl1 = tl2; t1 = t2;
+    q0 = q1; q1 = q2;
+    if (++t2 == nk) { t2 = 0; ++tl2; q2 = geo(tl2); }
+  }
+#undef G8_MFMA_BEGIN
+#undef G8_MFMA_END
+  if (wm == 0) __builtin_amdgcn_s_barrier();
+  g8_vm<0>();
+}
+
 // Eligible: bf16 NHWC store, 16-byte aligned rows, N % 8 == 0, sources with img_mul 1 / img_add 0
 // and every source but the last a multiple of 64 wide (a K tile never straddles two)
 bool gemm8_ok(const GemmArgs& g) {
@@ -370,14 +724,26 @@ bool gemm8_ok(const GemmArgs& g) {
   return true;
 }
 
+// g.allow_g8 == 2: the persistent form (nk >= 2), one block per CU (or per tile when fewer)
 void launch_gemm8(const GemmArgs& g, hipStream_t st) {
   const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + 255) / 256) : (g.M + 255) / 256;
   const int64_t nblk = mt * ((g.N + 255) / 256);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<false>), hipFuncAttributeMaxDynamicSharedMemorySize, G8_BYTES);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize, G8_BYTES);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<false>), hipFuncAttributeMaxDynamicSharedMemorySize, G8_BYTES);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize, G8_BYTES);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8p_kernel<false, false>), hipFuncAttributeMaxDynamicSharedMemorySize, G8P_BYTES);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8p_kernel<true, false>), hipFuncAttributeMaxDynamicSharedMemorySize, G8P_BYTES);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8p_kernel<false, true>), hipFuncAttributeMaxDynamicSharedMemorySize, G8P_BYTES);
     attr_set = true;
+  }
+  if (g.allow_g8 == 2 && g.a.Ktot > 64 && !(g.ln && g.res)) {
+    const int64_t grid = std::min<int64_t>(nblk, 256);
+    const dim3 gd((unsigned)grid);
+    if (g.ln) hipLaunchKernelGGL((gemm8p_kernel<true, false>), gd, dim3(512), G8P_BYTES, st, g);
+    else if (g.res) hipLaunchKernelGGL((gemm8p_kernel<false, true>), gd, dim3(512), G8P_BYTES, st, g);
+    else hipLaunchKernelGGL((gemm8p_kernel<false, false>), gd, dim3(512), G8P_BYTES, st, g);
+    return;
   }
   if (g.ln) hipLaunchKernelGGL((gemm8_kernel<true>), dim3((unsigned)nblk), dim3(512), G8_BYTES, st, g);
   else hipLaunchKernelGGL((gemm8_kernel<false>), dim3((unsigned)nblk), dim3(512), G8_BYTES, st, g);
