@@ -136,6 +136,7 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
  *   "panel_gemm"   [1] register-panel GEMM fallback; 0: K-loop GEMM
  *   "blaslt"       [1] hipBLASLt for the latent-level plain projections it wins (blas.cpp)
  *   "gemm8"        [0] 256 x 256 four-phase GEMM (gemm8.hip): 1 in place of hipBLASLt, 2 every eligible projection
+ *   "gemm8_ps"     [0] ... in its persistent form (one block per CU walks its tiles as one K-tile stream)
  *   "attn_fin"     [0] channel-attention row softmax inside the W_eff launch (attn.hip)
  *   "sab_waves"    [4] waves per SAB score block: 4 (64 queries) or 8 (128 queries per staged key tile)
  *   "tilepd"       [1] level-3 LN -> pointwise -> depthwise with the hidden map on chip (tilepd.hip:

@@ -323,6 +323,7 @@ struct TurtleHandle {
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
   int sab_waves = 4;                                  // waves per SAB score block: 4 (64 queries) or 8 (128)
   bool attn_fin = false;                              // channel-attention softmax rows inside the W_eff kernel (attn.hip)
+  bool gemm8_ps = false;                              // ... in its persistent form (one block per CU walks its tiles)
   int gemm8 = 0;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 in place of
                                                       // hipBLASLt, 2 every eligible projection
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
@@ -773,7 +774,7 @@ struct Runner {
     }
     bool lt = ln_cand ? use_blas(gl) : use_blas(g);
     if (ES == 2 && h->gemm8) {
-      g.allow_g8 = 1;
+      g.allow_g8 = h->gemm8_ps ? 2 : 1;           // 2: the persistent form (gemm8.hip)
       if (gemm8_ok(g) && (h->gemm8 == 2 || lt)) lt = false;
       else g.allow_g8 = 0;
     }
@@ -1600,6 +1601,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm_ar") h->gemm_ar = value != 0;
     else if (n == "gemm_kt") h->gemm_kt = value != 0;
     else if (n == "gemm8") h->gemm8 = (int)value;
+    else if (n == "gemm8_ps") h->gemm8_ps = value != 0;
     else if (n == "attn_fin") h->attn_fin = value != 0;
     else if (n == "sab_waves") h->sab_waves = (int)value;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
