@@ -4,7 +4,7 @@
 # Any outcome in which the command actually ran is returned as is (never re-run).
 #   bash tools/gpurun_wait.sh <timeout_s> '<command>'
 TO=$1; shift
-for i in 1 2 3 4 5 6; do
+for i in $(seq 1 ${GPURUN_TRIES:-6}); do
   /usr/local/graft/bin/gpurun --timeout "$TO" -- "$@" > gpurun_out/call.log 2>&1
   rc=$?
   tail -3 gpurun_out/call.log
