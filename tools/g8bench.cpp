@@ -29,7 +29,7 @@ static uint16_t f2bf(float f) {
 }
 static float bf2f(uint16_t b) { uint32_t u = (uint32_t)b << 16; float f; memcpy(&f, &u, 4); return f; }
 
-struct Shape { int64_t M; int N, K; int ln, res, gelu; const char* tag; int nsrc = 1, hw = 0; };
+struct Shape { int64_t M; int N, K; int ln, res, gelu; const char* tag; int nsrc = 1, hw = 0, conv3 = 0, Wimg = 1, store = 0; };
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
@@ -51,6 +51,10 @@ int main(int argc, char** argv) {
       {8160, 512, 512, 0, 1, 0, "small W_eff 8160", 1, 0},
       {2 * 32640, 512, 512, 0, 1, 0, "W_eff per-image x2", 1, 32640},
       {1000, 264, 200, 1, 1, 1, "ragged M N K"},
+      {130560, 512, 2304, 0, 0, 0, "L3 up conv3 shuffle", 1, 0, 1, 480, 1},
+      {522240, 256, 1152, 0, 0, 0, "L2 down conv3 unshuf", 1, 0, 1, 960, 2},
+      {32640, 1024, 4608, 0, 0, 0, "latent up conv3 shuffle", 1, 0, 1, 240, 1},
+      {130560, 256, 1152, 0, 1, 0, "L3 conv3 res NHWC", 1, 0, 1, 480, 0},
   };
   size_t maxA = 0, maxW = 0, maxO = 0;
   for (auto& s : shapes) {
@@ -99,7 +103,9 @@ int main(int argc, char** argv) {
     const int kin = s.K / s.nsrc;
     for (int j = 0; j < s.nsrc; ++j) g.a.s[j] = SrcDesc{(char*)A + (size_t)j * 128, kin + 64, 0, kin, 1, 0};
     if (s.nsrc == 1) g.a.s[0].ld = s.K;
-    g.M = s.M; g.N = s.N; g.HW = s.hw ? s.hw : (int)s.M; g.Wimg = 1;
+    if (s.conv3) g.a.s[0] = SrcDesc{A, s.K / 9, 0, s.K, 1, 0};
+    g.conv3 = s.conv3; g.cin = s.K / 9;
+    g.M = s.M; g.N = s.N; g.HW = s.hw ? s.hw : (int)s.M; g.Wimg = s.Wimg;
     g.w = Wt; g.ldw = s.K; g.wdiv = 1; g.wstride = s.hw ? (int64_t)s.N * s.K : 0;
     if (s.ln) {
       std::vector<float> rs(s.N, 0.f);
@@ -110,7 +116,7 @@ int main(int argc, char** argv) {
     g.ln = s.ln; g.ln_s = s.ln ? vec : nullptr; g.ln_t = s.ln ? vec + 4096 : nullptr;
     g.bias = vec + 8192; g.scale = nullptr; g.gelu = s.gelu;
     g.res = s.res ? R : nullptr; g.ldr = s.N; g.offr = 0;
-    g.ldo = s.N; g.offo = 0; g.store_mode = STORE_NHWC;
+    g.ldo = s.store == STORE_UNSHUFFLE ? s.N * 4 : (s.store == STORE_SHUFFLE ? s.N / 4 : s.N); g.offo = 0; g.store_mode = s.store;
     g.zeros = zeros; g.ones = ones;
     const size_t n = (size_t)s.M * s.N;
     double us[4] = {0, 0, 0, 0};
@@ -118,7 +124,7 @@ int main(int argc, char** argv) {
     GemmArgs g8 = g; g8.allow_g8 = 1; g8.out = Og8;
     if (!gemm8_ok(g8)) { printf("%-26s not eligible\n", s.tag); continue; }
     const bool kt_ok = gemm_kt_ok(gk);
-    const bool bl_ok = blas && s.nsrc == 1 && !s.gelu && !s.hw &&
+    const bool bl_ok = blas && s.nsrc == 1 && !s.gelu && !s.hw && !s.conv3 &&
                        blas_ready(blas, s.M, s.N, s.K, s.K, s.K, s.res ? s.N : 0, s.N, s.res != 0, true);
     LnRowsArgs la{A, s.K, 0, XN, s.K, s.M, s.K, 1};
     GemmArgs g8p = g8; g8p.allow_g8 = 2; g8p.out = Og8b;

@@ -101,6 +101,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   const int kc = (((lane & 7) ^ (((wid & 1) << 2) | (lane >> 4))) & 7) * 8;
   int xm[4];                        // pixel rows: X-a i0, i1, X-b i0, i1 (clamped into the tile's valid range)
   int wrow[4];                      // weight rows: W-a i0, i1, W-b i0, i1
+  int xyp[4];                       // implicit 3x3: (y << 16) | x of those pixels in their image
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int io = (i * 8 + wid) * 8 + (lane >> 3);
@@ -108,6 +109,15 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
     const int64_t ma = m0 + pr, mb = m0 + pr + 64;
     xm[i] = (int)(ma < mlim ? ma : m0);
     xm[2 + i] = (int)(mb < mlim ? mb : m0);
+    if (g.conv3) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int mm = xm[2 * h + i], p = mm % g.HW, y = p / g.Wimg;
+        xyp[2 * h + i] = (y << 16) | (p - y * g.Wimg);
+      }
+    } else {
+      xyp[i] = xyp[2 + i] = 0;
+    }
     const int wa = n0 + (io >> 5) * 64 + g8_perm(io & 31), wb = n0 + (io >> 5) * 64 + g8_perm(32 + (io & 31));
     wrow[i] = min(wa, g.N - 1);
     wrow[2 + i] = min(wb, g.N - 1);
@@ -133,12 +143,26 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
         kb = hit ? kbj : kb;
         kbj += j < g.a.n ? g.a.s[j].K : 0;
       }
-      const bf16* b2 = base + soff + (k0 - kb) + kc;
       const int o = u == U_XA ? 0 : 2;
+      if (g.conv3) {                              // tap-major K: tap = k0 / cin, its 64 channels
+        const int tap = k0 / g.cin, dy = tap / 3 - 1, dx = tap - (tap / 3) * 3 - 1;
+        const bf16* b2 = base + g.a.s[0].off + (k0 - tap * g.cin) + kc;
+        const int Himg = g.HW / g.Wimg;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        g8_dma16(live ? reinterpret_cast<const void*>(b2 + (int64_t)xm[o + i] * sld) : reinterpret_cast<const void*>(g_zero_g8),
-                 dst + i * 8192);
+        for (int i = 0; i < 2; ++i) {
+          const int y = (xyp[o + i] >> 16) + dy, x = (xyp[o + i] & 0xffff) + dx;
+          const bool ok = live && y >= 0 && y < Himg && x >= 0 && x < g.Wimg;
+          uint64_t pa = reinterpret_cast<uint64_t>(b2 + (int64_t)(xm[o + i] + dy * g.Wimg + dx) * sld);
+          asm volatile("" : "+v"(pa));
+          g8_dma16(ok ? reinterpret_cast<const void*>(pa) : reinterpret_cast<const void*>(g_zero_g8), dst + i * 8192);
+        }
+      } else {
+        const bf16* b2 = base + soff + (k0 - kb) + kc;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          g8_dma16(live ? reinterpret_cast<const void*>(b2 + (int64_t)xm[o + i] * sld) : reinterpret_cast<const void*>(g_zero_g8),
+                   dst + i * 8192);
+      }
     } else {
       const int o = u == U_WA ? 0 : 2;
 #pragma unroll
@@ -345,8 +369,27 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
       bf16x8 ov;
 #pragma unroll
       for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
-      // NHWC, or channel-blocked (STORE_CB16: channel k of pixel m at ((k / 16) cb_px + m) 16 + k % 16)
-      const int64_t dst = g.store_mode == STORE_CB16 ? ((((int64_t)(c >> 4) * g.cb_px + m) << 4) + (c & 15)) : m * g.ldo + g.offo + c;
+      // NHWC, channel-blocked (STORE_CB16: channel k of pixel m at ((k / 16) cb_px + m) 16 + k % 16),
+      // or PixelShuffle / PixelUnshuffle (the 3x3 resampling convolutions, as gemm5.hip)
+      int64_t dst;
+      if (g.store_mode == STORE_NHWC) {
+        dst = m * g.ldo + g.offo + c;
+      } else if (g.store_mode == STORE_CB16) {
+        dst = (((int64_t)(c >> 4) * g.cb_px + m) << 4) + (c & 15);
+      } else {
+        const int mi = (int)m, img = mi / g.HW, p = mi - img * g.HW;
+        const int Wi = g.Wimg, Hi = g.HW / Wi;
+        const int y = p / Wi, x = p - y * Wi;
+        if (g.store_mode == STORE_UNSHUFFLE) {
+          const int64_t dp = ((int64_t)img * (Hi / 2) + y / 2) * (Wi / 2) + x / 2;
+          const int sub = (y & 1) * 2 + (x & 1);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) o[dp * g.ldo + g.offo + (c + e) * 4 + sub] = ov[e];
+          continue;
+        }
+        const int Cq = g.N / 4, sp = c / Cq, cn = c - sp * Cq;
+        dst = (((int64_t)img * 2 * Hi + 2 * y + (sp >> 1)) * (2 * Wi) + 2 * x + (sp & 1)) * g.ldo + g.offo + cn;
+      }
       *reinterpret_cast<bf16x8*>(o + dst) = ov;
     }
   }
@@ -708,6 +751,14 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs g) {
 // and every source but the last a multiple of 64 wide (a K tile never straddles two)
 bool gemm8_ok(const GemmArgs& g) {
   if (g.store_mode == STORE_CB16 && (g.cb_px < g.M || g.N % 16 || g.wstride)) return false;
+  if (g.store_mode == STORE_SHUFFLE && ((g.N / 4) % 8 || g.N % 4)) return false;
+  if (g.conv3)                                    // implicit 3x3: one source, whole 64-channel K tiles per tap
+    return g.allow_g8 && g.a.n == 1 && g.cin % 64 == 0 && g.a.Ktot == 9 * g.cin && !g.ln && !g.wstride && g.N % 8 == 0 &&
+           g.ldo % 8 == 0 && g.offo % 8 == 0 && g.ldw % 8 == 0 && g.a.s[0].ld % 8 == 0 && g.a.s[0].off % 8 == 0 &&
+           g.a.s[0].img_mul == 1 && g.a.s[0].img_add == 0 && reinterpret_cast<uintptr_t>(g.a.s[0].base) % 16 == 0 &&
+           reinterpret_cast<uintptr_t>(g.out) % 16 == 0 && reinterpret_cast<uintptr_t>(g.w) % 16 == 0 &&
+           (!g.res || (g.ldr % 8 == 0 && g.offr % 8 == 0 && reinterpret_cast<uintptr_t>(g.res) % 16 == 0)) &&
+           g.Wimg > 0 && g.HW % g.Wimg == 0 && g.M % g.HW == 0 && g.HW / g.Wimg < 65536;
   if (!g.allow_g8 || (g.store_mode != STORE_NHWC && g.store_mode != STORE_CB16) || g.conv3 || g.a.cb_px || g.N % 8 || g.ldo % 8 || g.offo % 8 ||
       g.ldw % 8 || g.a.Ktot % 8 || g.a.n < 1)
     return false;
@@ -737,7 +788,7 @@ void launch_gemm8(const GemmArgs& g, hipStream_t st) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8p_kernel<false, true>), hipFuncAttributeMaxDynamicSharedMemorySize, G8P_BYTES);
     attr_set = true;
   }
-  if (g.allow_g8 == 2 && g.a.Ktot > 64 && !(g.ln && g.res)) {
+  if (g.allow_g8 == 2 && g.a.Ktot > 64 && !(g.ln && g.res) && !g.conv3 && (g.store_mode == STORE_NHWC || g.store_mode == STORE_CB16)) {
     const int64_t grid = std::min<int64_t>(nblk, 256);
     const dim3 gd((unsigned)grid);
     if (g.ln) hipLaunchKernelGGL((gemm8p_kernel<true, false>), gd, dim3(512), G8P_BYTES, st, g);
