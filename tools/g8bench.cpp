@@ -17,6 +17,10 @@
 
 using namespace turtle;
 
+#ifdef TURTLE_G8_ABLATIONS
+namespace turtle { void launch_gemm8_dbg(const GemmArgs& g, int dbg, hipStream_t st); }
+#endif
+
 #define CK(x)                                                                 \
   do {                                                                        \
     hipError_t e = (x);                                                       \
@@ -33,6 +37,7 @@ struct Shape { int64_t M; int N, K; int ln, res, gelu; const char* tag; int nsrc
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
+  const bool abl = argc > 2 && !strcmp(argv[2], "abl");   // ablation table (built with -DTURTLE_G8_ABLATIONS)
   const Shape shapes[] = {
       {32640, 2560, 512, 1, 0, 0, "latent GFFW project_in"},
       {32640, 1536, 512, 1, 0, 0, "latent qkv"},
@@ -128,6 +133,26 @@ int main(int argc, char** argv) {
                        blas_ready(blas, s.M, s.N, s.K, s.K, s.K, s.res ? s.N : 0, s.N, s.res != 0, true);
     LnRowsArgs la{A, s.K, 0, XN, s.K, s.M, s.K, 1};
     GemmArgs g8p = g8; g8p.allow_g8 = 2; g8p.out = Og8b;
+#ifdef TURTLE_G8_ABLATIONS
+    if (abl) {                     // 1 no MFMA, 2 no DMA, 4 no fragment reads, 8 no barriers, 16 no stores
+      if (s.conv3 || s.hw || s.nsrc > 1 || s.M < 30000) continue;
+      printf("%-26s", s.tag);
+      for (int dbg : {0, 1, 2, 4, 8, 16, 5, 6, 14, 7, 15, 22}) {
+        launch_gemm8_dbg(g8, dbg, 0);
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < reps; ++i) launch_gemm8_dbg(g8, dbg, 0);
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        printf(" d%d=%.1f", dbg, ms * 1e3 / reps);
+      }
+      printf("\n");
+      fflush(stdout);
+      continue;
+    }
+#endif
     for (int v = 0; v < 4; ++v) {
       if ((v == 1 && !kt_ok) || (v == 2 && !bl_ok)) continue;
       auto run = [&] {

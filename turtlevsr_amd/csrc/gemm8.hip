@@ -63,7 +63,9 @@ TURTLE_DEV int g8_perm(int r) { return 32 * (r >> 5) + 8 * ((r >> 2) & 3) + 4 * 
 
 }  // namespace
 
-template <bool LN>
+// DBG (tools/g8bench ablation builds only, 0 in the library): 1 no MFMA, 2 no LDS-DMA, 4 no fragment
+// reads, 8 no barriers in the K loop, 16 no epilogue stores
+template <bool LN, int DBG = 0>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* s_mu = reinterpret_cast<float*>(smem + 2 * G8_BUF);
@@ -154,20 +156,20 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
           const bool ok = live && y >= 0 && y < Himg && x >= 0 && x < g.Wimg;
           uint64_t pa = reinterpret_cast<uint64_t>(b2 + (int64_t)(xm[o + i] + dy * g.Wimg + dx) * sld);
           asm volatile("" : "+v"(pa));
-          g8_dma16(ok ? reinterpret_cast<const void*>(pa) : reinterpret_cast<const void*>(g_zero_g8), dst + i * 8192);
+          if constexpr (!(DBG & 2)) g8_dma16(ok ? reinterpret_cast<const void*>(pa) : reinterpret_cast<const void*>(g_zero_g8), dst + i * 8192);
         }
       } else {
         const bf16* b2 = base + soff + (k0 - kb) + kc;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
-          g8_dma16(live ? reinterpret_cast<const void*>(b2 + (int64_t)xm[o + i] * sld) : reinterpret_cast<const void*>(g_zero_g8),
+          if constexpr (!(DBG & 2)) g8_dma16(live ? reinterpret_cast<const void*>(b2 + (int64_t)xm[o + i] * sld) : reinterpret_cast<const void*>(g_zero_g8),
                    dst + i * 8192);
       }
     } else {
       const int o = u == U_WA ? 0 : 2;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        g8_dma16(live ? reinterpret_cast<const void*>(Wp + (int64_t)wrow[o + i] * g.ldw + k0 + kc) : reinterpret_cast<const void*>(g_zero_g8),
+        if constexpr (!(DBG & 2)) g8_dma16(live ? reinterpret_cast<const void*>(Wp + (int64_t)wrow[o + i] * g.ldw + k0 + kc) : reinterpret_cast<const void*>(g_zero_g8),
                  dst + i * 8192);
     }
   };
@@ -182,6 +184,12 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   const int sw = (fr >> 1) & 7;
   const int loff0 = fr * 128 + ((fq ^ sw) << 4), loff1 = fr * 128 + (((fq ^ sw) ^ 4) << 4);
   auto frag = [&](const char* unit, int row0, int ks) __attribute__((always_inline)) {
+    if constexpr ((DBG & 4) != 0) {
+      bf16x8 z;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = (bf16)(float)(row0 + ks + lane);
+      return z;
+    }
     return *reinterpret_cast<const bf16x8*>(unit + row0 * 128 + (ks ? loff1 : loff0));
   };
 
@@ -189,13 +197,15 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
   float lsum[2] = {0.f, 0.f}, lsq[2] = {0.f, 0.f};
   auto stats2 = [&](const bf16x8 (&xa)[2], const bf16x8 (&xb)[2]) __attribute__((always_inline)) {
     typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const bf16x2 one2 = __builtin_bit_cast(bf16x2, 0x3F803F80u);
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const u32x4 w = __builtin_bit_cast(u32x4, tt ? xb[ks] : xa[ks]);
+        // (uint4 members: element access on a bit-cast u32x4 vector here made hipcc read the first
+        // dword four times)
+        const uint4 q = __builtin_bit_cast(uint4, tt ? xb[ks] : xa[ks]);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const bf16x2 v2 = __builtin_bit_cast(bf16x2, w[e]);
@@ -218,14 +228,14 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 
 #define G8_MFMA_BEGIN                                   \
   __builtin_amdgcn_sched_barrier(0);                    \
-  __builtin_amdgcn_s_barrier();                         \
+  if constexpr (!(DBG & 8)) __builtin_amdgcn_s_barrier(); \
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    \
   __builtin_amdgcn_sched_barrier(0);                    \
   __builtin_amdgcn_s_setprio(1);
 #define G8_MFMA_END                                     \
   __builtin_amdgcn_s_setprio(0);                        \
   __builtin_amdgcn_sched_barrier(0);                    \
-  __builtin_amdgcn_s_barrier();                         \
+  if constexpr (!(DBG & 8)) __builtin_amdgcn_s_barrier(); \
   asm volatile("" ::: "memory");                        \
   __builtin_amdgcn_sched_barrier(0);
 
@@ -249,7 +259,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][ks], xf[i][ks], acc[i][j], 0, 0, 0);
+        for (int ks = 0; ks < 2; ++ks) if constexpr (!(DBG & 1)) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][ks], xf[i][ks], acc[i][j], 0, 0, 0);
     if (LN && wn < 2) stats(xf);
     G8_MFMA_END
     // P2: W-b -> pixel tiles 0-3 x channel tiles 2-3
@@ -265,7 +275,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[j][ks], xf[i][ks], acc[i][2 + j], 0, 0, 0);
+        for (int ks = 0; ks < 2; ++ks) if constexpr (!(DBG & 1)) acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[j][ks], xf[i][ks], acc[i][2 + j], 0, 0, 0);
     G8_MFMA_END
     // P3: X-b -> pixel tiles 4-7 x channel tiles 2-3
 #pragma unroll
@@ -280,7 +290,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[j][ks], xf[i][ks], acc[4 + i][2 + j], 0, 0, 0);
+        for (int ks = 0; ks < 2; ++ks) if constexpr (!(DBG & 1)) acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb[j][ks], xf[i][ks], acc[4 + i][2 + j], 0, 0, 0);
     if (LN && wn >= 2) stats(xf);
     G8_MFMA_END
     // P4: (no reads) -> pixel tiles 4-7 x channel tiles 0-1
@@ -292,7 +302,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][ks], xf[i][ks], acc[4 + i][j], 0, 0, 0);
+        for (int ks = 0; ks < 2; ++ks) if constexpr (!(DBG & 1)) acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[j][ks], xf[i][ks], acc[4 + i][j], 0, 0, 0);
     G8_MFMA_END
   }
 #undef G8_MFMA_BEGIN
@@ -390,7 +400,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(GemmArgs g) {
         const int Cq = g.N / 4, sp = c / Cq, cn = c - sp * Cq;
         dst = (((int64_t)img * 2 * Hi + 2 * y + (sp >> 1)) * (2 * Wi) + 2 * x + (sp & 1)) * g.ldo + g.offo + cn;
       }
-      *reinterpret_cast<bf16x8*>(o + dst) = ov;
+      if constexpr (!(DBG & 16)) *reinterpret_cast<bf16x8*>(o + dst) = ov;
     }
   }
 }
@@ -529,13 +539,15 @@ __global__ __launch_bounds__(512, 1) void gemm8p_kernel(GemmArgs g) {
   float lsum[2] = {0.f, 0.f}, lsq[2] = {0.f, 0.f};
   auto stats2 = [&](const bf16x8 (&xa)[2], const bf16x8 (&xb)[2]) __attribute__((always_inline)) {
     typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const bf16x2 one2 = __builtin_bit_cast(bf16x2, 0x3F803F80u);
 #pragma unroll
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const u32x4 w = __builtin_bit_cast(u32x4, tt ? xb[ks] : xa[ks]);
+        // (uint4 members: element access on a bit-cast u32x4 vector here made hipcc read the first
+        // dword four times)
+        const uint4 q = __builtin_bit_cast(uint4, tt ? xb[ks] : xa[ks]);
+        const uint32_t w[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const bf16x2 v2 = __builtin_bit_cast(bf16x2, w[e]);
@@ -799,5 +811,33 @@ void launch_gemm8(const GemmArgs& g, hipStream_t st) {
   if (g.ln) hipLaunchKernelGGL((gemm8_kernel<true>), dim3((unsigned)nblk), dim3(512), G8_BYTES, st, g);
   else hipLaunchKernelGGL((gemm8_kernel<false>), dim3((unsigned)nblk), dim3(512), G8_BYTES, st, g);
 }
+
+#ifdef TURTLE_G8_ABLATIONS
+// tools/g8bench ablation launcher (non-persistent kernel, one instantiation per DBG value)
+template <int DBG>
+static void g8_launch_dbg(const GemmArgs& g, hipStream_t st) {
+  const int64_t mt = (g.M + 255) / 256, nblk = mt * ((g.N + 255) / 256);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<false, DBG>), hipFuncAttributeMaxDynamicSharedMemorySize, G8_BYTES);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gemm8_kernel<true, DBG>), hipFuncAttributeMaxDynamicSharedMemorySize, G8_BYTES);
+  if (g.ln) hipLaunchKernelGGL((gemm8_kernel<true, DBG>), dim3((unsigned)nblk), dim3(512), G8_BYTES, st, g);
+  else hipLaunchKernelGGL((gemm8_kernel<false, DBG>), dim3((unsigned)nblk), dim3(512), G8_BYTES, st, g);
+}
+void launch_gemm8_dbg(const GemmArgs& g, int dbg, hipStream_t st) {
+  switch (dbg) {
+    case 1: g8_launch_dbg<1>(g, st); break;
+    case 2: g8_launch_dbg<2>(g, st); break;
+    case 4: g8_launch_dbg<4>(g, st); break;
+    case 8: g8_launch_dbg<8>(g, st); break;
+    case 16: g8_launch_dbg<16>(g, st); break;
+    case 5: g8_launch_dbg<5>(g, st); break;
+    case 6: g8_launch_dbg<6>(g, st); break;
+    case 14: g8_launch_dbg<14>(g, st); break;
+    case 7: g8_launch_dbg<7>(g, st); break;
+    case 15: g8_launch_dbg<15>(g, st); break;
+    case 22: g8_launch_dbg<22>(g, st); break;
+    default: g8_launch_dbg<0>(g, st);
+  }
+}
+#endif
 
 }  // namespace turtle
