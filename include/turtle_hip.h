@@ -135,10 +135,12 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
  *   "gemm_lds"     [1] LDS-pipelined GEMM (fallback where the kernels above do not apply)
  *   "panel_gemm"   [1] register-panel GEMM fallback; 0: K-loop GEMM
  *   "blaslt"       [1] hipBLASLt for the latent-level plain projections it wins (blas.cpp)
- *   "gemm8"        [0] 256 x 256 four-phase GEMM (gemm8.hip): 1 in place of hipBLASLt, 2 every eligible projection
+ *   "gemm8"        [3] 256 x 256 four-phase GEMM (gemm8.hip): 1 in place of hipBLASLt, 2 every eligible projection,
+ *                  3 the multi-source projections with K >= 1024 (where it measures fastest), 0 never
  *   "gemm8_ps"     [0] ... in its persistent form (one block per CU walks its tiles as one K-tile stream)
  *   "attn_fin"     [0] channel-attention row softmax inside the W_eff launch (attn.hip)
- *   "sab_waves"    [4] waves per SAB score block: 4 (64 queries) or 8 (128 queries per staged key tile)
+ *   "sab_waves"    [0] waves per SAB score block: 4 (64 queries) or 8 (128 queries per staged key tile); 0 = 8 at
+ *                  token widths d >= 256, 4 below
  *   "tilepd"       [1] level-3 LN -> pointwise -> depthwise with the hidden map on chip (tilepd.hip:
  *                  channel-attention qkv + qkv_dwconv)
  *   "tilepd_gate"  [0] ... also the GatedFeedForward's project_in + dwconv + gelu gate (slower than pn + dwgemm)

@@ -151,7 +151,7 @@ def test_kernel_variants_agree(dtype):
     variants += [dict(base, gemm_lds=1), dict(base, gemm_pn=1), dict(base, sab_mfma=1), dict(base, sab_mfma=1, sab_db=1), dict(base, stem_mfma=1),
                  dict(base, blaslt=1), dict(base, fuse=1, fused2=1),
                  dict(base, gemm_ar=1), dict(base, gemm_kt=1), dict(base, dwgemm=1), dict(base, dwgemm=1, dwgemm_attn=0), dict(base, dwgemm=1, dwgemm_cb=0), dict(base, ffn=1), dict(base, down_tile=1), dict(base, tilepd=1), dict(base, tilepd=1, tilepd_gate=1), dict(base, tilepd=1, tilepd_gate=1, gemm_kt=1),
-                 dict(base, tilepd=1, tilepd_gate=1, tilepd_cb=0), dict(base, gemm8=2), dict(base, gemm8=2, gemm8_ps=1), dict(base, gemm8=2, gemm_kt=1, tilepd=1), dict(base, attn_fin=1), dict(base, sab_waves=8),
+                 dict(base, tilepd=1, tilepd_gate=1, tilepd_cb=0), dict(base, gemm8=2), dict(base, gemm8=2, gemm8_ps=1), dict(base, gemm8=3, gemm_kt=1), dict(base, gemm8=2, gemm_kt=1, tilepd=1), dict(base, attn_fin=1), dict(base, sab_waves=8),
                  dict(base, gemm_kt=1, gemm_ar=1, gemm_pn=1, gemm_lds=1, fuse=1, fused2=1, dw_rows=1, panel_gemm=1, dwgemm=1, ffn=1),
                  dict(base, gemm_kt=1, gemm_ar=1, gemm_pn=1, fuse=1, fused2=1, dw_rows=1, dwgemm=1, ffn=1, tilepd=1),
                  dict(base, gemm_lds=1, gemm_pn=1, fuse=1, fused2=1, dw_rows=1, panel_gemm=1, sab_mfma=1, stem_mfma=1, blaslt=1)]

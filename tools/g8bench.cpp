@@ -137,7 +137,7 @@ int main(int argc, char** argv) {
     if (abl) {                     // 1 no MFMA, 2 no DMA, 4 no fragment reads, 8 no barriers, 16 no stores
       if (s.conv3 || s.hw || s.nsrc > 1 || s.M < 30000) continue;
       printf("%-26s", s.tag);
-      for (int dbg : {0, 1, 2, 4, 8, 16, 5, 6, 14, 7, 15, 22}) {
+      for (int dbg : {0, 1, 2, 4, 8, 16, 32, 64, 96, 33, 34, 38, 46, 39, 47, 6, 14, 7}) {
         launch_gemm8_dbg(g8, dbg, 0);
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(e0, 0));

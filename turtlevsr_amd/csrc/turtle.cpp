@@ -321,10 +321,11 @@ struct TurtleHandle {
   bool gemm_pn = true;                                // resident-panel bf16 GEMM, K <= 512 (gemm3.hip)
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
-  int sab_waves = 4;                                  // waves per SAB score block: 4 (64 queries) or 8 (128)
+  int sab_waves = 0;                                  // waves per SAB score block: 4 (64 queries), 8 (128), 0 = 8 at
+                                                      // d >= 256, else 4 (tools/sabbench, profiles/r04_sabbench_waves.log)
   bool attn_fin = false;                              // channel-attention softmax rows inside the W_eff kernel (attn.hip)
   bool gemm8_ps = false;                              // ... in its persistent form (one block per CU walks its tiles)
-  int gemm8 = 0;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 in place of
+  int gemm8 = 3;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 in place of
                                                       // hipBLASLt, 2 every eligible projection
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   bool sab_db = false;                                // SAB A.v: double-buffered 1-block/CU variant (else 2 blocks / CU)
@@ -774,8 +775,12 @@ struct Runner {
     }
     bool lt = ln_cand ? use_blas(gl) : use_blas(g);
     if (ES == 2 && h->gemm8) {
+      // 1: in place of hipBLASLt, 2: every eligible projection, 3: the K-concatenated multi-source
+      // projections with K >= 1024 (the FHR / CHM W_eff GEMMs, where it measures ~7-10 % faster than
+      // the 2-D tiled kernel: profiles/r04_g8bench.log; elsewhere hipBLASLt / pn / kt stay faster)
       g.allow_g8 = h->gemm8_ps ? 2 : 1;           // 2: the persistent form (gemm8.hip)
-      if (gemm8_ok(g) && (h->gemm8 == 2 || lt)) lt = false;
+      const bool pick = h->gemm8 == 2 || (h->gemm8 == 1 && lt) || (h->gemm8 == 3 && a.n >= 2 && a.Ktot >= 1024 && !conv3);
+      if (gemm8_ok(g) && pick) lt = false;
       else g.allow_g8 = 0;
     }
     tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s%s%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
@@ -1271,7 +1276,8 @@ struct Runner {
     T* q2f = buf(P * d2);
     T* k2f = buf(P * d2);
     T* qtok = buf((int64_t)B * N * d2);
-    const int nsplit = sab_score_nsplit(B, NT, N, d2, h->sab_waves);
+    const int sab_waves = h->sab_waves ? h->sab_waves : (d2 >= 256 ? 8 : 4);
+    const int nsplit = sab_score_nsplit(B, NT, N, d2, sab_waves);
     // partial lists sized for either block size, so the sab_waves switch never changes the workspace
     const int nsplit_ws = std::max(sab_score_nsplit(B, NT, N, d2, 4), sab_score_nsplit(B, NT, N, d2, 8));
     float* topv = fbuf((int64_t)B * NT * nsplit_ws * N * 5);
@@ -1328,7 +1334,7 @@ struct Runner {
       if (NT > TURTLE_MAX_T) TFAIL(TURTLE_EINVAL, "too many cached frames");
       SabScoreArgs sa{};
       sa.q = qtok; sa.q_bstride = (int64_t)N * d2; sa.B = B; sa.T = NT; sa.N = N; sa.d = d2;
-      sa.th = th; sa.tw = tw; sa.nsplit = nsplit; sa.waves = h->sab_waves;
+      sa.th = th; sa.tw = tw; sa.nsplit = nsplit; sa.waves = sab_waves;
       sa.tau = h->fptr(bw.sab_tau); sa.topv = topv; sa.topi = topi; sa.ballv = ballv;
       SabGatherArgs ga{};
       ga.B = B; ga.T = NT; ga.N = N; ga.th = th; ga.tw = tw; ga.ws = ws; ga.C = c;
