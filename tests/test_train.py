@@ -436,22 +436,29 @@ def test_fp16_autocast_matches_aten_same_autocast():
     within 10 % relative L2 (bf16's 7-bit mantissa against fp16's 10)."""
     g, meta = load("train_tiny")
     lq, gt = _data(meta, "cuda")
+    scale = 1024.0                                   # GradScaler's role: fp16 gradients must not underflow
     res = []
     for ops in (None, AtenOps):
         net = _net(meta, ops, "cuda")
         tr = Trainer(net, amp="fp16")
         loss = tr.loss(lq, gt)
-        (loss + 0 * sum(p.sum() for p in net.parameters())).backward()
+        ((loss + 0 * sum(p.sum() for p in net.parameters())) * scale).backward()
         torch.cuda.synchronize()
-        res.append((float(loss.detach()), {k: p.grad.detach().float().cpu() for k, p in net.named_parameters()}))
+        res.append((float(loss.detach()), {k: p.grad.detach().float().cpu() / scale for k, p in net.named_parameters()}))
     (lh, gh), (la, ga) = res
     assert np.isfinite(lh) and lh == pytest.approx(la, rel=2e-2), (lh, la)
+    # whole-gradient relative L2 <= 5 %, and per parameter <= 10 % wherever its gradient is above the
+    # fp16 noise floor (norm >= 1e-3 of the largest parameter gradient)
+    num = sum(float((gh[k] - r).norm()) ** 2 for k, r in ga.items())
+    den = sum(float(r.norm()) ** 2 for r in ga.values())
+    assert num ** 0.5 <= 0.05 * den ** 0.5, (num ** 0.5, den ** 0.5)
+    gmax = max(float(r.norm()) for r in ga.values())
     bad = []
     for k, r in ga.items():
-        den = float(r.norm())
-        if den == 0.0:
+        d = float(r.norm())
+        if d < 1e-3 * gmax:
             continue
-        err = float((gh[k] - r).norm()) / den
+        err = float((gh[k] - r).norm()) / d
         if err > 0.1:
             bad.append((k, err))
     assert not bad, bad[:10]
