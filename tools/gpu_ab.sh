@@ -7,8 +7,8 @@ OUT=gpurun_out/${1:-ab}
 mkdir -p $OUT
 export TMPDIR=/tmp
 if [ -n "$TESTS" ]; then
-  K=""; [ "$TESTS" != "all" ] && K="-k $TESTS"
-  timeout -k 10 1500 python -u -m pytest tests -m gpu -v -x --timeout 600 --timeout-method thread $K > $OUT/pytest_gpu.log 2>&1
+  K=(); [ "$TESTS" != "all" ] && K=(-k "$TESTS")
+  timeout -k 10 1500 python -u -m pytest tests -m gpu -v -x --timeout 600 --timeout-method thread "${K[@]}" > $OUT/pytest_gpu.log 2>&1
   rc=$?; echo "tests rc=$rc"; tail -4 $OUT/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
 fi
 IFS=';' read -ra SETS <<< "${OPTSETS:--}"
