@@ -15,7 +15,7 @@ IFS=';' read -ra SETS <<< "${OPTSETS:--}"
 i=0
 for set in "${SETS[@]}"; do
   args=""; [ "$set" != "-" ] && for o in $set; do args="$args --opt $o"; done
-  TURTLE_BENCH_DUMP=$OUT/launches_$i.tsv timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-psnr --no-scaling-point $args > $OUT/bench_$i.log 2>&1
+  TURTLE_BENCH_DUMP=$OUT/launches_$i.tsv timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-psnr --no-scaling-point ${RESARGS:-} $args > $OUT/bench_$i.log 2>&1
   rc=$?; echo "[$set] $(tail -1 $OUT/bench_$i.log | cut -c1-150)"; [ $rc -ne 0 ] && exit $rc
   python3 tools/launch_report.py $OUT/launches_$i.tsv --steps 3 --top 200 > $OUT/launch_report_$i.txt 2>&1
   i=$((i+1))

@@ -576,7 +576,7 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
     // small frames (fewer than 32768 pixels: < 256 pn panels, i.e. a partly idle chip) also go to
     // the 2-D tiled kernel, whose channel tiles multiply the grid
     const int K = g.a.Ktot;
-    if (((g.conv3 && g.N >= 256) || (!g.conv3 && K >= 640) || (!g.ln && K == 512 && g.N >= 512) || g.M < 32768) &&
+    if (((g.conv3 && g.N >= 256) || (!g.conv3 && K >= 640) || (!g.ln && K == 512 && g.N >= 512) || g.M < (g.kt_max_px ? g.kt_max_px : 32768)) &&
         gemm_kt_ok(g)) {
       launch_gemm_kt(g, st);
       return;

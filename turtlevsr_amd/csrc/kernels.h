@@ -41,6 +41,7 @@ struct GemmArgs {
   unsigned long long* stamps;      // tools/kbench s_memtime stamps of the pn kernel (null in the product path)
   int64_t cb_px;                   // STORE_CB16: pixels per 16-channel block (= M)
   int allow_g8;                    // 256 x 256 four-phase kernel permitted (turtle_set_option "gemm8")
+  int kt_max_px;                   // GEMMs over fewer pixels go to the 2-D tiled kernel (0: 32768)
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
 bool gemm_lds_ok(const GemmArgs& g);                              // gemm2.hip (bf16)

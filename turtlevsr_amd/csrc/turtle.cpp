@@ -321,6 +321,8 @@ struct TurtleHandle {
   bool gemm_pn = true;                                // resident-panel bf16 GEMM, K <= 512 (gemm3.hip)
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
+  int kt_max_px = 32768;                              // below this many pixels the 2-D tiled GEMM takes every shape it can
+  int blas_multi_img = 0;                             // 1: hipBLASLt also for multi-image W_eff (per-image calls)
   int sab_waves = 0;                                  // waves per SAB score block: 4 (64 queries), 8 (128), 0 = 8 at
                                                       // d >= 256, else 4 (tools/sabbench, profiles/r04_sabbench_waves.log)
   bool attn_fin = false;                              // channel-attention softmax rows inside the W_eff kernel (attn.hip)
@@ -759,7 +761,7 @@ struct Runner {
     g.res = res; g.ldr = ldr; g.offr = offr;
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store; g.cb_px = store == STORE_CB16 ? M : 0;
     g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel; g.allow_lds = h->gemm_lds; g.allow_pn = h->gemm_pn;
-    g.allow_ar = h->gemm_ar; g.allow_kt = h->gemm_kt;
+    g.allow_ar = h->gemm_ar; g.allow_kt = h->gemm_kt; g.kt_max_px = h->kt_max_px;
     if (store == STORE_CB16 && (ES != 2 || !gemm_pn_ok(g)) && !(ES == 2 && h->gemm8 == 2 && gemm8_ok((g.allow_g8 = 1, g))))
       TFAIL(TURTLE_EINVAL, "channel-blocked store needs the pn GEMM (M " + std::to_string(M) + " N " + std::to_string(g.N) +
                                " K " + std::to_string(a.Ktot) + " HW " + std::to_string(HW) + ")");
@@ -779,7 +781,10 @@ struct Runner {
       // projections with K >= 1024 (the FHR / CHM W_eff GEMMs, where it measures ~7-10 % faster than
       // the 2-D tiled kernel: profiles/r04_g8bench.log; elsewhere hipBLASLt / pn / kt stay faster)
       g.allow_g8 = h->gemm8_ps ? 2 : 1;           // 2: the persistent form (gemm8.hip)
-      const bool pick = h->gemm8 == 2 || (h->gemm8 == 1 && lt) || (h->gemm8 == 3 && a.n >= 2 && a.Ktot >= 1024 && !conv3);
+      // (mode 3 only where the 256 x 256 tiles still give every CU one: small frames go to kt)
+      const int64_t g8_tiles = ((M + 255) / 256) * ((g.N + 255) / 256);
+      const bool pick = h->gemm8 == 2 || (h->gemm8 == 1 && lt) ||
+                        (h->gemm8 == 3 && a.n >= 2 && a.Ktot >= 1024 && !conv3 && g8_tiles >= 256);
       if (gemm8_ok(g) && pick) lt = false;
       else g.allow_g8 = 0;
     }
@@ -806,6 +811,9 @@ struct Runner {
     const SrcDesc& s = g.a.s[0];
     if (s.img_mul != 1 || s.img_add != 0 || s.K != g.a.Ktot) return false;
     if (g.wstride && (g.HW <= 0 || g.M % g.HW || g.wstride % 8)) return false;
+    // per-image weight sets (W_eff) over several images: one hipBLASLt call per image (8 launches at
+    // 256x256 B = 8: 58 us per site) against one 2-D tiled launch over all of them
+    if (g.wstride && g.M / g.HW > 1 && h->blas_multi_img == 0) return false;
     const int64_t Mi = g.wstride ? g.HW : g.M;
     const int K = g.a.Ktot;
     if (!(K >= 512 || (Mi <= 140000 && g.N >= 256))) return false;
@@ -1610,6 +1618,8 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm8_ps") h->gemm8_ps = value != 0;
     else if (n == "attn_fin") h->attn_fin = value != 0;
     else if (n == "sab_waves") h->sab_waves = (int)value;
+    else if (n == "blas_multi_img") h->blas_multi_img = (int)value;
+    else if (n == "kt_max_px") h->kt_max_px = (int)value;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
     else if (n == "stem_mfma") h->stem_mfma = value != 0;
     else if (n == "fused2") h->fused2 = value != 0;
