@@ -225,7 +225,8 @@ def roofline(wprof, wgroups, nwarm, tgroups, steps, dtype):
     roof.update(traffic=round(tr["hbm_bytes_per_launch"]) if tr else None, kernel=tag,
                 hbm_frac=round(hbm_frac, 4), mfma_frac=round(mfma_frac, 4),
                 arithmetic_intensity=round(fpl / max(bpl, 1.0), 1), ridge_flop_per_byte=round(ridge, 1),
-                traffic_source=(pmc_src if tr else f"none measured on kernel sources {source_hash()}"),
+                traffic_source=(f"profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x 2 + WRITE_SIZE passes, run dir {pmc_src}, "
+                                f"kernel sources {source_hash()})" if tr else f"none measured on kernel sources {source_hash()}"),
                 launches_per_step=g["launches"] / steps, avg_launch_us=round(avg_s * 1e6, 2),
                 algorithmic_bytes_per_launch=round(bpl), algorithmic_flops_per_launch=round(fpl),
                 mfma_tflops=round(fpl / avg_s / 1e12, 2), hbm_gbs=round(bpl / avg_s / 1e9, 1),
