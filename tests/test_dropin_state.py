@@ -71,6 +71,29 @@ def test_sab_arena_zero_copy_and_immutable_history(dtype):
         assert torch.equal(o6, o6b)
 
 
+def test_sab_arena_refill_matches_roomy_arena():
+    """An exhausted arena is replaced by a fresh one that the library fills by copying the kept
+    frames (turtle.cpp sab_cache_shift): a 1-frame-headroom arena, refilled every other frame, gives
+    the same frames bit for bit as the default (byte-budgeted, never refilled here) arena."""
+    from turtlevsr_amd.synthetic import synthetic_frames
+    _, meta = load("clip_gopro_64")
+    clip = torch.from_numpy(synthetic_frames((1, 9, 3, 128, 128), 43)).cuda()
+    outs = []
+    for tight in (False, True):
+        m = _model(meta["opt"], meta["seed"], "bf16")
+        if tight:
+            m._ARENA_EXTRA, m._ARENA_BYTES = 1, 0
+        kc = vc = None
+        res = []
+        with torch.no_grad():
+            for j in range(9):
+                o, kc, vc = m(_pair(clip, j), kc, vc)
+                res.append(o.clone())
+        outs.append(res)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_minimum_input_size_is_refused():
     _, meta = load("clip_gopro_64")
     m = _model(meta["opt"], meta["seed"], "bf16")

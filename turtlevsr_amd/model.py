@@ -31,6 +31,7 @@ strides (P*heads*rows, rows, 1, heads*rows)); incoming caches of any layout are 
 from __future__ import annotations
 
 import ctypes as C
+import math
 import operator
 from typing import List, Optional
 
@@ -128,9 +129,15 @@ class TurtleHIP(TrainGraph, TurtleParams):
             self.__dict__["_arenas"] = {}
         h = self._handle.h
         with torch.cuda.device(dev):
-            for name, t in self.state_dict().items():
-                a = t.detach().float().cpu().contiguous()
-                _lib.check(L.turtle_set_weight(h, name.encode(), C.c_void_p(a.data_ptr()), a.numel()))
+            # one device->host transfer of all parameters (a per-tensor .cpu() is ~630 small copies)
+            sd = [(name, t.detach()) for name, t in self.state_dict().items()]
+            flat = torch.cat([t.reshape(-1).float() for _, t in sd]).cpu() if sd else torch.empty(0)
+            off = 0
+            for name, t in sd:
+                n = t.numel()
+                a = flat[off:off + n]
+                off += n
+                _lib.check(L.turtle_set_weight(h, name.encode(), C.c_void_p(a.data_ptr()), n))
             _lib.check(L.turtle_load_weights(h))
         self._sig = self._signature()
 
@@ -241,7 +248,9 @@ class TurtleHIP(TrainGraph, TurtleParams):
     # Every arena frame is written once and never again (the history stays immutable for callers
     # holding older caches); an incoming cache that is not the arena's latest (a branched or
     # moved history, B > 1) gets a fresh arena that the library fills by copying.
-    _ARENA_EXTRA = 6
+    _ARENA_EXTRA = 6                  # minimum frames of headroom
+    _ARENA_MAX_EXTRA = 64
+    _ARENA_BYTES = 6 << 30            # per slot
 
     def _sab_out(self, i, ks, vs, tin, kin, vin, cdt, dev):
         if ks[0] != 1:
@@ -258,7 +267,11 @@ class TurtleHIP(TrainGraph, TurtleParams):
                 b = s0 + first
                 a["next"] = b + tnew
                 return a["k"][b:b + tnew].unsqueeze(0), a["v"][b:b + tnew].unsqueeze(0)
-        cap = tnew + self._ARENA_EXTRA
+        # frames of headroom: a refill copies the kept frames once per `extra` frames, so size the
+        # arena by bytes (HBM is plentiful; a 1080p level-1 slot is ~0.27 GB per frame)
+        fbytes = (math.prod(ks[2:]) + math.prod(vs[2:])) * torch.empty(0, dtype=cdt).element_size()
+        extra = max(self._ARENA_EXTRA, min(self._ARENA_MAX_EXTRA, self._ARENA_BYTES // max(fbytes, 1)))
+        cap = tnew + extra
         a = arenas[i] = dict(k=torch.empty((cap,) + tuple(ks[2:]), dtype=cdt, device=dev),
                              v=torch.empty((cap,) + tuple(vs[2:]), dtype=cdt, device=dev), next=tnew)
         return a["k"][:tnew].unsqueeze(0), a["v"][:tnew].unsqueeze(0)
