@@ -39,7 +39,9 @@ __host__ __device__ inline int gram_nrm_off(int GP, int ch, int ncol, int ES, in
   return tiles > parts ? tiles : parts;
 }
 template <typename T, int GP, int MT>
-__global__ __launch_bounds__(256) void gram_kernel(GramArgs a) {
+// two blocks per CU (<= 256 VGPRs) wherever that costs no spills: up to 20 accumulator tiles per wave
+// at 32-pixel steps (the 5-segment CHM Grams: 1 -> 2 waves per SIMD, L2 311 -> 204 us at 1080p)
+__global__ __launch_bounds__(256, (MT <= 8 || (MT <= 16 && GP <= 64) || (MT <= 20 && GP <= 32)) ? 2 : 1) void gram_kernel(GramArgs a) {
   extern __shared__ __attribute__((aligned(16))) char gsm[];
   constexpr int VEC = Vec<T>::N, ES = sizeof(T);
   const int ch = a.ch, ncol = a.nseg * ch;
@@ -210,6 +212,7 @@ static void launch_gram_gp(const GramArgs& a, hipStream_t st) {
   if (mt <= 4) launch_gram_cfg<T, GP, 4>(a, st);
   else if (mt <= 8) launch_gram_cfg<T, GP, 8>(a, st);
   else if (mt <= 16) launch_gram_cfg<T, GP, 16>(a, st);
+  else if (mt <= 20) launch_gram_cfg<T, GP, 20>(a, st);
   else launch_gram_cfg<T, GP, GMAXT>(a, st);
 }
 
