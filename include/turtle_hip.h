@@ -127,6 +127,7 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
 /* Kernel-selection switches (performance A/B only; every setting computes the same function;
  * defaults in brackets). Names and semantics are those turtle_set_option (turtle.cpp) accepts:
  *   "fuse"         [1] block-level fused kernels (fused2.hip row walk / fused.hip) for input widths <= 128
+ *   "fuse_fp32"    [0] ... also in the fp32 build (the round-1 fused.hip kernel; 0: GEMM + depthwise + GEMM, faster)
  *   "fused2"       [1] the bf16 row-walk fused kernel (fused2.hip); 0: the round-1 fused.hip kernel
  *   "ffn"          [1] FeedForward in one kernel (ffn.hip) at widths 64 / 128 (bf16)
  *   "gemm_pn"      [1] persistent resident-panel GEMM for LN-folded 1x1 convolutions, K <= 512

@@ -314,6 +314,8 @@ struct TurtleHandle {
   size_t dev_bytes = 0;
   bool loaded = false;
   bool fuse = getenv("TURTLE_NO_FUSE") == nullptr;   // block-level fused kernels (fused.hip)
+  bool fuse_fp32 = false;                             // fp32 build: the round-1 fused block kernel (fused.hip) instead of GEMM + dw +
+                                                      // GEMM (540p fp32 16.6 -> 20.5 frames/s without it: profiles/r04o_*)
   bool fused2 = true;                                 // bf16 row-walk fused kernels (fused2.hip) where eligible
   bool panel = getenv("TURTLE_NO_PANEL") == nullptr; // panel GEMM (gemm.hip)
   bool dw_rows = true;                                // row-sweeping depthwise kernel (spatial.hip)
@@ -887,7 +889,7 @@ struct Runner {
   }
   // fused.hip handles input widths <= 128 in 16-channel slices and 32-deep GEMM2 K steps
   bool can_fuse(int c, int mode, int n1, int hidden) const {
-    if (!h->fuse || c > 128 || c % 16) return false;
+    if (!h->fuse || (ES == 4 && !h->fuse_fp32) || c > 128 || c % 16) return false;
     if (mode == F_DWONLY) return n1 % 16 == 0;
     return hidden % 32 == 0;
   }
@@ -1592,6 +1594,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     if (!h || !name) TFAIL(TURTLE_EINVAL, "null argument");
     const std::string n = name;
     if (n == "fuse") h->fuse = value != 0;
+    else if (n == "fuse_fp32") h->fuse_fp32 = value != 0;
     else if (n == "panel_gemm") h->panel = value != 0;
     else if (n == "dw_rows") h->dw_rows = value != 0;
     else if (n == "blaslt") h->blaslt = value != 0;
