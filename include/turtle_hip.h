@@ -157,7 +157,8 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
  *   "down_tile"    [1] LDS-tiled level-1 Downsample (spatial.hip)
  *   "stem_mfma"    [1] input_projection / ending 3x3 on the matrix cores (bf16, dim 64)
  *   "sab_mfma"     [1] SAB sparse A.v on the matrix cores (bf16)
- *   "sab_db"       [0] SAB A.v double-buffered at one block per CU; 0: two blocks per CU
+ *   "sab_db"       [0] SAB A.v: 0 two blocks per CU; 1 double-buffered at one block per CU; 2 two blocks per CU
+ *                  with the top-5 tail rows fetched a chunk ahead (slower)
  *   "split_out"    [1] output-adjacent weights (ending, reduce_chan_level1) as split bf16 pairs
  * Unknown names return TURTLE_EINVAL. */
 int turtle_set_option(TurtleHandle* h, const char* name, int value);

@@ -149,7 +149,7 @@ def test_kernel_variants_agree(dtype):
     ref = _run(_opts(_model(meta, "fp32"), base), clip)[0]
     variants = [dict(base, fuse=f, panel_gemm=p, dw_rows=d) for f in (0, 1) for p in (0, 1) for d in (0, 1)]
     variants += [dict(base, fuse=1, fuse_fp32=1), dict(base, fuse=1, fuse_fp32=1, panel_gemm=1)]   # fp32 fused block kernel
-    variants += [dict(base, gemm_lds=1), dict(base, gemm_pn=1), dict(base, sab_mfma=1), dict(base, sab_mfma=1, sab_db=1), dict(base, stem_mfma=1),
+    variants += [dict(base, gemm_lds=1), dict(base, gemm_pn=1), dict(base, sab_mfma=1), dict(base, sab_mfma=1, sab_db=1), dict(base, sab_mfma=1, sab_db=2), dict(base, stem_mfma=1),
                  dict(base, blaslt=1), dict(base, fuse=1, fused2=1),
                  dict(base, gemm_ar=1), dict(base, gemm_kt=1), dict(base, dwgemm=1), dict(base, dwgemm=1, dwgemm_attn=0), dict(base, dwgemm=1, dwgemm_cb=0), dict(base, ffn=1), dict(base, down_tile=1), dict(base, tilepd=1), dict(base, tilepd=1, tilepd_gate=1), dict(base, tilepd=1, tilepd_gate=1, gemm_kt=1),
                  dict(base, tilepd=1, tilepd_gate=1, tilepd_cb=0), dict(base, gemm8=2), dict(base, gemm8=2, gemm8_ps=1), dict(base, gemm8=3, gemm_kt=1), dict(base, gemm8=2, gemm_kt=1, tilepd=1), dict(base, attn_fin=1), dict(base, sab_waves=8),
@@ -169,6 +169,20 @@ def test_kernel_variants_agree(dtype):
             else:
                 assert psnr(a.numpy(), r.numpy()) >= BF16_DB, (key, j)
                 assert psnr(a.numpy(), outs[k0][j].numpy()) >= BF16_DB, (key, j)
+
+
+def test_sab_av_variants_bit_identical():
+    """The three SAB A.v pipelines (sab_db 0: tail rows in their own chunk, 1: double-buffered, 2:
+    tail rows a chunk ahead) run the same arithmetic per output (MFMA over the non-zero 32-key steps,
+    then the top-5 tail FMAs in list order): bf16 frames are identical, on a ragged token grid
+    (160x224: 10x14 level-1 tokens, partial 8x8 tiles)."""
+    from turtlevsr_amd.synthetic import synthetic_frames
+    _, meta = load("clip_gopro_64")
+    clip = synthetic_frames((1, 4, 3, 160, 224), 17)
+    outs = [_run(_opts(_model(meta, "bf16"), {"sab_db": v}), clip)[0] for v in (0, 1, 2)]
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
 
 
 def _opts(m, opts):

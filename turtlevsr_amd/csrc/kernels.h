@@ -124,7 +124,8 @@ struct SabGatherArgs {             // out = sum_c w_c v[key_c], dilated token ->
   const int* cnt; const int* ci; const float* cw;
   const float* ballw;              // [B*T][N][41] dense ball weights (matrix-core A.v)
   void* out;                       // [B*T][Hl][Wl][C] pixel-major
-  int db;                          // sab_av_mfma: 1 double-buffered (1 block / CU), 0 two blocks / CU
+  int db;                          // sab_av_mfma: 0 two blocks / CU; 1 double-buffered (1 block / CU); 2 two
+                                   // blocks / CU with the tail rows fetched one chunk ahead
 };
 bool sab_av_mfma_ok(const SabGatherArgs& a);
 void launch_sab_av_mfma(const SabGatherArgs& a, hipStream_t st);   // bf16

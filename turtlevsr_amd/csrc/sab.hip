@@ -531,7 +531,10 @@ constexpr int SM_RO = SM_E + 4;                    // output staging row (floats
 // fetched at the top of their own chunk, <= 256 registers: two blocks per CU
 template <bool DB> constexpr int sm_lds() { return (DB ? 2 : 1) * 256 * SM_RV + 64 * SM_RO * 4 + 64 * SAB_K * 8; }
 
-template <bool DB>
+// PF (with !DB): the tail rows of chunk c + 1 are fetched at the top of chunk c into a second
+// register set, so their L2 latency overlaps a whole chunk at two blocks per CU. Measured slower
+// than fetching them at the top of their own chunk (level 1 757 vs 724 us at 1080p); sab_db = 2.
+template <bool DB, bool PF>
 __global__ __launch_bounds__(256, DB ? 1 : 2) void sab_av_mfma_kernel(SabGatherArgs a, int nsplit) {
   extern __shared__ __attribute__((aligned(16))) char sm[];
   char* sV = sm;                                   // [1 or 2][256][SM_RV]
@@ -583,18 +586,22 @@ __global__ __launch_bounds__(256, DB ? 1 : 2) void sab_av_mfma_kernel(SabGatherA
     sB[e] = (ti < a.th && tj < a.tw) ? a.ballw[((int64_t)bt * a.N + ti * a.tw + tj) * BALL + s] : 0.f;
   }
   __syncthreads();
-  // ---- W' A fragments in registers: q-tile qt (16 queries), K-step ks (32 square keys) ----
+  // ---- W' A fragments in registers: wave wid owns q-tile qt = wid (16 queries) for all 64
+  // elements of a chunk; K-step ks = qt + s (32 square keys: query rows 2 qt, 2 qt + 1 reach
+  // key-square rows 2 qt .. 2 qt + 9 only, the other 3 steps are all zero and skipped) - 20
+  // registers per wave instead of 4 tiles x 8 steps ----
   // lane: query row qt*16 + (l & 15), keys 32 ks + 8 (l >> 4) + j
-  bf16x8 wf[4][8];
+  bf16x8 wf[5];
   {
     const int ql_lo = lane & 15, kg = lane >> 4;
-#pragma unroll
-    for (int qt = 0; qt < 4; ++qt) {
+    {
+      const int qt = wid;
       const int ql = qt * 16 + ql_lo;
       const int qy = ql / SM_T, qx = ql % SM_T;                 // query offset in the tile
       const float* bw = sB + ql * BALL;
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
+      for (int s = 0; s < 5; ++s) {
+        const int ks = qt + s;
         bf16x8 f;
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
@@ -605,7 +612,7 @@ __global__ __launch_bounds__(256, DB ? 1 : 2) void sab_av_mfma_kernel(SabGatherA
           if (ad <= 4) w = bw[ball_slot(di, dj)];
           f[j] = (bf16)w;
         }
-        wf[qt][ks] = f;
+        wf[s] = f;
       }
     }
   }
@@ -639,7 +646,7 @@ __global__ __launch_bounds__(256, DB ? 1 : 2) void sab_av_mfma_kernel(SabGatherA
   // tail rows of this thread's query / element group, fetched one chunk ahead (their L2 latency
   // was the critical path of a chunk)
   const int tq = tid >> 2, teg = (tid & 3) * 16;
-  uint4 tcur[2 * SAB_K], tnext[DB ? 2 * SAB_K : 1];
+  uint4 tcur[2 * SAB_K], tnext[(DB || PF) ? 2 * SAB_K : 1];
   auto load_tail = [&](int chn, uint4 (&r)[2 * SAB_K]) {
 #pragma unroll
     for (int x = 0; x < SAB_K; ++x) {
@@ -650,36 +657,39 @@ __global__ __launch_bounds__(256, DB ? 1 : 2) void sab_av_mfma_kernel(SabGatherA
   };
   if (ch_beg < ch_end) {
     load_v(ch_beg);
-    if constexpr (DB) load_tail(ch_beg, tcur);
+    if constexpr (DB || PF) load_tail(ch_beg, tcur);
     store_v(0);
   }
   __syncthreads();
   for (int chn = ch_beg; chn < ch_end; ++chn) {
     const int buf = DB ? (chn - ch_beg) & 1 : 0;
-    if constexpr (!DB) load_tail(chn, tcur);      // lands during this chunk's MFMAs
+    if constexpr (!DB && !PF) load_tail(chn, tcur);   // lands during this chunk's MFMAs
     if (chn + 1 < ch_end) {
       load_v(chn + 1);
-      if constexpr (DB) load_tail(chn + 1, tnext);
+      if constexpr (DB || PF) load_tail(chn + 1, tnext);
     }
-    // MFMA: wave w owns elements w*16 .. +15 of the chunk, all 64 queries
+    // MFMA: wave w owns queries w*16 .. +15 (q-tile w), all 64 elements of the chunk (4 groups of 16)
     f32x4 acc[4];
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt) acc[qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int eg = 0; eg < 4; ++eg) acc[eg] = f32x4{0.f, 0.f, 0.f, 0.f};
     const char* vb = sV + buf * 256 * SM_RV;
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const char* va = vb + (ks * 32 + 8 * g16 + qq) * SM_RV + (wid * 16 + 4 * pp) * 2;
-      const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)va);
-      const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(va + 4 * SM_RV));
-      const bf16x8 bfr = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+    for (int s = 0; s < 5; ++s) {
+      const int ks = wid + s;
 #pragma unroll
-      for (int qt = 0; qt < 4; ++qt) acc[qt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[qt][ks], bfr, acc[qt], 0, 0, 0);
+      for (int eg = 0; eg < 4; ++eg) {
+        const char* va = vb + (ks * 32 + 8 * g16 + qq) * SM_RV + (eg * 16 + 4 * pp) * 2;
+        const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)va);
+        const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(va + 4 * SM_RV));
+        const bf16x8 bfr = __builtin_bit_cast(bf16x8, (v8s)__builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc[eg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[s], bfr, acc[eg], 0, 0, 0);
+      }
     }
-    // C: column (l & 15) = element wid*16 + (l & 15), rows 4 (l >> 4) + i = query
+    // C: column (l & 15) = element eg*16 + (l & 15), rows 4 (l >> 4) + i = query wid*16 + ..
 #pragma unroll
-    for (int qt = 0; qt < 4; ++qt)
+    for (int eg = 0; eg < 4; ++eg)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sO[(qt * 16 + g16 * 4 + i) * SM_RO + wid * 16 + li] = acc[qt][i];
+      for (int i = 0; i < 4; ++i) sO[(wid * 16 + g16 * 4 + i) * SM_RO + eg * 16 + li] = acc[eg][i];
     __syncthreads();                               // (!DB: every wave's V reads of this chunk are done)
     if constexpr (!DB) {
       if (chn + 1 < ch_end) store_v(0);
@@ -718,6 +728,11 @@ __global__ __launch_bounds__(256, DB ? 1 : 2) void sab_av_mfma_kernel(SabGatherA
 #pragma unroll
         for (int x = 0; x < 2 * SAB_K; ++x) tcur[x] = tnext[x];
       }
+    } else if constexpr (PF) {
+      if (chn + 1 < ch_end) {
+#pragma unroll
+        for (int x = 0; x < 2 * SAB_K; ++x) tcur[x] = tnext[x];
+      }
     }
     __syncthreads();
   }
@@ -735,12 +750,16 @@ void launch_sab_av_mfma(const SabGatherArgs& a, hipStream_t st) {
   const int nsplit = std::max(1, std::min(nch, (1024 + tiles - 1) / tiles));
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_av_mfma_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize, sm_lds<true>());
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_av_mfma_kernel<false>), hipFuncAttributeMaxDynamicSharedMemorySize, sm_lds<false>());
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_av_mfma_kernel<true, false>), hipFuncAttributeMaxDynamicSharedMemorySize, sm_lds<true>());
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_av_mfma_kernel<false, false>), hipFuncAttributeMaxDynamicSharedMemorySize, sm_lds<false>());
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&sab_av_mfma_kernel<false, true>), hipFuncAttributeMaxDynamicSharedMemorySize, sm_lds<false>());
     attr = true;
   }
-  if (a.db) hipLaunchKernelGGL(sab_av_mfma_kernel<true>, dim3((unsigned)(tiles * nsplit)), dim3(256), sm_lds<true>(), st, a, nsplit);
-  else hipLaunchKernelGGL(sab_av_mfma_kernel<false>, dim3((unsigned)(tiles * nsplit)), dim3(256), sm_lds<false>(), st, a, nsplit);
+  const dim3 grid((unsigned)(tiles * nsplit));
+  constexpr int l1 = sm_lds<true>(), l2 = sm_lds<false>();
+  if (a.db == 1) hipLaunchKernelGGL((sab_av_mfma_kernel<true, false>), grid, dim3(256), l1, st, a, nsplit);
+  else if (a.db == 2) hipLaunchKernelGGL((sab_av_mfma_kernel<false, true>), grid, dim3(256), l2, st, a, nsplit);
+  else hipLaunchKernelGGL((sab_av_mfma_kernel<false, false>), grid, dim3(256), l2, st, a, nsplit);
 }
 
 template void launch_sab_score<float>(const SabScoreArgs&, hipStream_t);

@@ -332,7 +332,8 @@ struct TurtleHandle {
   int gemm8 = 3;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 in place of
                                                       // hipBLASLt, 2 every eligible projection
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
-  bool sab_db = false;                                // SAB A.v: double-buffered 1-block/CU variant (else 2 blocks / CU)
+  int sab_db = 0;                                     // SAB A.v: 0 two blocks / CU; 1 double-buffered, one block / CU;
+                                                      // 2 two blocks / CU with the tail rows fetched a chunk ahead
   bool sab_mfma = true;                               // matrix-core SAB A.v over query tiles (sab.hip)
   bool dwgemm = true;                                 // depthwise (+ gate) folded into the next GEMM's operand, c >= 256 (dwgemm.hip)
   int gram_blocks = getenv("TURTLE_GRAM_BLOCKS") ? atoi(getenv("TURTLE_GRAM_BLOCKS")) : 512;   // Gram pixel splits: blocks over all (b, head)
@@ -1348,7 +1349,7 @@ struct Runner {
       sa.tau = h->fptr(bw.sab_tau); sa.topv = topv; sa.topi = topi; sa.ballv = ballv;
       SabGatherArgs ga{};
       ga.B = B; ga.T = NT; ga.N = N; ga.th = th; ga.tw = tw; ga.ws = ws; ga.C = c;
-      ga.cnt = ccnt; ga.ci = cidx; ga.cw = cwt; ga.ballw = ballv; ga.out = xs; ga.db = h->sab_db ? 1 : 0;
+      ga.cnt = ccnt; ga.ci = cidx; ga.cw = cwt; ga.ballw = ballv; ga.out = xs; ga.db = h->sab_db;
       for (int t = 0; t < NT; ++t) {
         if (t < Tin) {
           sa.k[t] = kin + (int64_t)t * N * d2; sa.k_bstride[t] = (int64_t)Tin * N * d2;
@@ -1611,7 +1612,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "tilepd_gate") h->tilepd_gate = value != 0;
     else if (n == "tilepd_min_blocks") h->tilepd_min_blocks = (int)value;
     else if (n == "down_tile") h->down_tile = value != 0;
-    else if (n == "sab_db") h->sab_db = value != 0;
+    else if (n == "sab_db") h->sab_db = (int)value;
     else if (n == "dwgemm_min_blocks") h->dwgemm_min_blocks = (int)value;
     else if (n == "gemm_lds") h->gemm_lds = value != 0;
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
