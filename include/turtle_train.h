@@ -51,6 +51,12 @@ int turtle_train_colsum(const void* dy, int64_t ld, float* db, int64_t P, int N,
  * out[img][n] += sum over the img_px pixels of image img of x[p][n]^2; out fp32 [P / img_px][N], zeroed by the caller */
 int turtle_train_colsumsq(const void* x, int64_t ld, float* out, int64_t P, int N, int64_t img_px, int dtype, void* stream);
 
+/* the per-image weight of the normalised channel-attention Gram backward (turtle_t1_arch.py:690-697
+ * differentiated): wd[b] [2c][2c] = [[diag(aq[b]), D[b]], [D[b]^T, diag(ak[b])]], D [B][heads][ch][ch] fp32
+ * block-diagonal per head (ch = c / heads), aq / ak fp32 [B][c]; wd in the activation dtype, dense */
+int turtle_train_gram_wd(const float* D, const float* aq, const float* ak, void* wd, int64_t B, int c, int heads, int dtype,
+                         void* stream);
+
 /* pointwise GEMM (a 1x1 convolution, nn.Conv2d(K, N, 1) on NHWC rows; also its input gradient with
  * W transposed, and the channel-attention A.v with per-image weights):
  *   y[p][n] = sum_k x[p][k] w[img(p)][n][k] + bias[n]

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 GPU check (one gpurun call). Steps are chained: a failing / timed-out step ends the call.
-#   bash tools/gpu_r04.sh <tag> [steps...]   steps: tests testsall newtests bench launch prof smoke train
+#   bash tools/gpu_r04.sh <tag> [steps...]   steps: tests testsall newtests bench launch prof smoke train trainprof
 set -o pipefail
 TAG=${1:-r04}; shift
 STEPS=${@:-tests bench}
@@ -34,6 +34,9 @@ for s in $STEPS; do
     train)
       timeout -k 10 300 python -u bench.py --train --steps 3 --warmup 1 > $OUT/bench_train.log 2>&1
       rc=$?; tail -1 $OUT/bench_train.log | cut -c1-300; [ $rc -ne 0 ] && exit $rc ;;
+    trainprof)
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/tprof -o run -- python3 bench.py --train --steps 2 --warmup 1 > $OUT/tprof.log 2>&1
+      rc=$?; echo "trainprof rc=$rc"; tail -1 $OUT/tprof.log | cut -c1-300; [ $rc -ne 0 ] && exit $rc ;;
     kbench)
       timeout -k 10 300 $KBENCH_CMD > $OUT/kbench.log 2>&1
       rc=$?; echo "kbench rc=$rc"; tail -30 $OUT/kbench.log; [ $rc -ne 0 ] && exit $rc ;;

@@ -140,18 +140,27 @@ class CopyLog(TorchDispatchMode):
             t = out if torch.is_tensor(out) else (args[0] if args and torch.is_tensor(args[0]) else None)
             if t is not None:
                 site = "?"
-                for fr in reversed(traceback.extract_stack()[:-1]):
+                stack = list(reversed(traceback.extract_stack()[:-1]))
+                for i, fr in enumerate(stack):
                     if "turtlevsr_amd" in fr.filename or "train_copies" in fr.filename:
                         site = f"{os.path.basename(fr.filename)}:{fr.lineno} {fr.line.strip()[:70]}"
+                        if fr.filename.endswith("train_ops.py"):     # name the graph line that called the op
+                            up = next((g for g in stack[i + 1:] if g.filename.endswith("train.py")), None)
+                            if up is not None:
+                                site += f"  <- train.py:{up.lineno} {up.line.strip()[:50]}"
                         break
                 node = torch._C._current_autograd_node()
                 if node is not None:
                     site = f"[bwd {node.name()}] " + site
                 src = args[1] if name.startswith("copy_") and len(args) > 1 and torch.is_tensor(args[1]) else None
                 desc = f"{name} {tuple(t.shape)} {str(t.dtype)[6:]}"
+                if name.startswith("clone") and args and torch.is_tensor(args[0]):
+                    a0 = args[0]
+                    desc += f" <- {str(a0.dtype)[6:]} cl={a0.is_contiguous(memory_format=CL)} nchw={a0.is_contiguous()} stride={a0.stride()}"
                 if src is not None:
                     desc += f" <- {str(src.dtype)[6:]} cl={src.is_contiguous(memory_format=CL)} nchw={src.is_contiguous()}"
-                key = (self.phase, site, desc.split(" (")[0] + (" " + desc.split(" <- ")[1] if " <- " in desc else ""))
+                key = (self.phase, site, desc.split(" (")[0] + (" " + desc.split(" <- ")[1] if " <- " in desc else "")
+                       + (f" {tuple(t.shape)}" if "train.py:146" in site else ""))
                 self.tot[key] += t.numel() * t.element_size()
                 self.n[key] += 1
         return out

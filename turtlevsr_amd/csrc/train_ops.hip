@@ -473,6 +473,34 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, i
   for (int i = threadIdx.x; i < N; i += 256) atomicAdd(&db[i], sred[i]);
 }
 
+
+// The per-image weight of the normalised channel-attention Gram backward (train_ops._NormGram):
+// Wd[b] = [[diag(aq[b]), D[b]], [D[b]^T, diag(ak[b])]] with D block-diagonal per head
+// (D[b][h] = dL/dG of head h), written densely in the GEMM dtype in one pass (zeros included):
+// dqk = qk Wd^T is then one per-image GEMM over the [q | k] rows.
+template <typename T>
+__global__ __launch_bounds__(256) void gram_wd_kernel(const float* __restrict__ D, const float* __restrict__ aq,
+                                                      const float* __restrict__ ak, T* __restrict__ wd, int c, int heads,
+                                                      int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c2 = 2 * c, ch = c / heads;
+  const int64_t per = (int64_t)c2 * c2;
+  const int b = (int)(i / per);
+  const int r = (int)((i % per) / c2), col = (int)(i % c2);
+  const bool rq = r < c, cq = col < c;
+  const int rr = rq ? r : r - c, cc = cq ? col : col - c;
+  float v = 0.f;
+  if (r == col) {
+    v = rq ? aq[(int64_t)b * c + rr] : ak[(int64_t)b * c + rr];
+  } else if (rq != cq && rr / ch == cc / ch) {
+    const int h = rr / ch;
+    const float* Dh = D + ((int64_t)b * heads + h) * ch * ch;
+    v = rq ? Dh[(rr % ch) * ch + cc % ch] : Dh[(cc % ch) * ch + rr % ch];
+  }
+  wd[i] = T(v);
+}
+
 // ---------------------------------------------------------------------------------------------
 // reduction GEMM  C[img][n][k] = sum_{p in img} A[p][n] B[p][k]
 //   bf16: block = 64 (n) x 64 (k) output tile, 4 waves of 32 x 32 (2 x 2 MFMA 16x16x32 tiles);
@@ -480,8 +508,10 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, i
 //   read with ds_read_b64_tr_b16. A lane group g (16 lanes) of the transposed read h covers the
 //   pixel rows 4 g + 16 h + q (q = 0..3): the 8 rows a 32-lane half reads are consecutive, which
 //   with the 160-B row pitch (40 dwords) puts them on 8 distinct 8-bank sets (conflict-free); the
-//   same pixel order is used for A and B, so the contraction is exact. Pixel splits write fp32
-//   partials [split][img][N][K]; rgemm_reduce sums them in split order.
+//   same pixel order is used for A and B, so the contraction is exact. Two LDS stages: the next
+//   stage's global loads (unconditional, clamped addresses, masked rows) are in flight during this
+//   stage's MFMAs. Pixel splits write fp32 partials [split][img][N][K]; rgemm_reduce sums them in
+//   split order.
 //   fp32 (parity builds): the same tiling on the VALU.
 // ---------------------------------------------------------------------------------------------
 constexpr int RG_BN = 64, RG_BK = 64, RG_BP = 64, RG_PITCH = 160;
@@ -497,8 +527,10 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
                                                          int64_t ldb, float* __restrict__ part, int64_t img_px, int nimg_out,
                                                          int N, int K, int64_t P, int64_t ppb) {
   typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
-  __shared__ __attribute__((aligned(16))) char sA[RG_BP * RG_PITCH];
-  __shared__ __attribute__((aligned(16))) char sB[RG_BP * RG_PITCH];
+  // two stage buffers: the global loads of stage s + 1 are in flight (in registers) while the
+  // MFMAs of stage s read the other buffer; one barrier per stage
+  __shared__ __attribute__((aligned(16))) char sA[2][RG_BP * RG_PITCH];
+  __shared__ __attribute__((aligned(16))) char sB[2][RG_BP * RG_PITCH];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int ntn = (N + RG_BN - 1) / RG_BN, ntk = (K + RG_BK - 1) / RG_BK;
   const int tile = blockIdx.x % (ntn * ntk);
@@ -514,42 +546,83 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // staging: thread -> pixel row tid >> 2, 16-B chunks 2 (tid & 3) and + 1 of each operand
+  // staging: thread -> pixel row tid >> 2, 16-B chunks 2 (tid & 3) and + 1 of each operand.
+  // Loads are unconditional: a column chunk past N / K is clamped to the last one (it only feeds
+  // output rows / columns that are not stored), a pixel row past the split's end is clamped to its
+  // last row and zeroed by a mask when it is written to LDS (both operands: no inf * 0).
   const int srow = tid >> 2, sch = 2 * (tid & 3);
-  // transposed reads: lane group g = lane >> 4, row q = (lane >> 2) & 3, column quad pq = lane & 3
-  const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
-  for (int64_t pb = p0; pb < p1; pb += RG_BP) {
-    const int64_t p = pb + srow;
-    const bool live = p < p1;
+  const bf16* pa[2];
+  const bf16* pb_[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    pa[u] = A + pbase * lda + min(n0 + 8 * (sch + u), N - 8);
+    pb_[u] = B + pbase * ldb + min(k0 + 8 * (sch + u), K - 8);
+  }
+  uint4 ra[2], rb[2];
+  uint32_t live_mask = 0;
+  auto gload = [&](int64_t pbk) {
+    const int64_t p = pbk + srow;
+    live_mask = p < p1 ? 0xffffffffu : 0u;
+    const int64_t pc = p < p1 ? p : p1 - 1;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int cA = n0 + 8 * (sch + u), cB = k0 + 8 * (sch + u);
-      uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
-      if (live && cA < N) va = *reinterpret_cast<const uint4*>(A + (pbase + p) * lda + cA);
-      if (live && cB < K) vb = *reinterpret_cast<const uint4*>(B + (pbase + p) * ldb + cB);
-      *reinterpret_cast<uint4*>(sA + srow * RG_PITCH + 16 * (sch + u)) = va;
-      *reinterpret_cast<uint4*>(sB + srow * RG_PITCH + 16 * (sch + u)) = vb;
+      ra[u] = *reinterpret_cast<const uint4*>(pa[u] + pc * lda);
+      rb[u] = *reinterpret_cast<const uint4*>(pb_[u] + pc * ldb);
     }
-    __syncthreads();
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const uint4 va = make_uint4(ra[u].x & live_mask, ra[u].y & live_mask, ra[u].z & live_mask, ra[u].w & live_mask);
+      const uint4 vb = make_uint4(rb[u].x & live_mask, rb[u].y & live_mask, rb[u].z & live_mask, rb[u].w & live_mask);
+      *reinterpret_cast<uint4*>(sA[buf] + srow * RG_PITCH + 16 * (sch + u)) = va;
+      *reinterpret_cast<uint4*>(sB[buf] + srow * RG_PITCH + 16 * (sch + u)) = vb;
+    }
+  };
+  // transposed reads: lane group g = lane >> 4, row q = (lane >> 2) & 3, column quad pq = lane & 3
+  const int g = lane >> 4, q = (lane >> 2) & 3, pq = lane & 3;
+  if (p0 < p1) {
+    gload(p0);
+    lstore(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int64_t pbk = p0; pbk < p1; pbk += RG_BP) {
+    const bool more = pbk + RG_BP < p1;           // block-uniform
+    if (more) gload(pbk + RG_BP);
+    const char* cA = sA[buf];
+    const char* cB = sB[buf];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {               // 32 pixels per MFMA K step
-      bf16x8v af[2], bfr[2];
+      uint2 ra0[2], ra1[2], rb0[2], rb1[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const int cn = 32 * wn + 16 * t + 4 * pq, ck = 32 * wk + 16 * t + 4 * pq;
         const int r0 = 32 * ks + 4 * g + q;
-        const uint2 a0 = ds_read_tr16(sA + r0 * RG_PITCH + 2 * cn), a1 = ds_read_tr16(sA + (r0 + 16) * RG_PITCH + 2 * cn);
-        const uint2 b0 = ds_read_tr16(sB + r0 * RG_PITCH + 2 * ck), b1 = ds_read_tr16(sB + (r0 + 16) * RG_PITCH + 2 * ck);
-        af[t] = __builtin_bit_cast(bf16x8v, make_uint4(a0.x, a0.y, a1.x, a1.y));
-        bfr[t] = __builtin_bit_cast(bf16x8v, make_uint4(b0.x, b0.y, b1.x, b1.y));
+        ra0[t] = ds_read_tr16(cA + r0 * RG_PITCH + 2 * cn);
+        ra1[t] = ds_read_tr16(cA + (r0 + 16) * RG_PITCH + 2 * cn);
+        rb0[t] = ds_read_tr16(cB + r0 * RG_PITCH + 2 * ck);
+        rb1[t] = ds_read_tr16(cB + (r0 + 16) * RG_PITCH + 2 * ck);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      // the wait names the read results as operands: the compiler does not see the asm reads as
+      // LDS loads, so without the dependence it may schedule an MFMA before the wait
+      asm volatile("s_waitcnt lgkmcnt(0)"
+                   : "+v"(ra0[0]), "+v"(ra0[1]), "+v"(ra1[0]), "+v"(ra1[1]), "+v"(rb0[0]), "+v"(rb0[1]), "+v"(rb1[0]),
+                     "+v"(rb1[1])::"memory");
+      bf16x8v af[2], bfr[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        af[t] = __builtin_bit_cast(bf16x8v, make_uint4(ra0[t].x, ra0[t].y, ra1[t].x, ra1[t].y));
+        bfr[t] = __builtin_bit_cast(bf16x8v, make_uint4(rb0[t].x, rb0[t].y, rb1[t].x, rb1[t].y));
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+    if (more) lstore(buf ^ 1);
     __syncthreads();
+    buf ^= 1;
   }
   // lane holds C[n0 + 32 wn + 16 i + 4 g + e][k0 + 32 wk + 16 j + (lane & 15)]
   float* out = part + ((int64_t)split * nimg_out + img) * N * K;
@@ -743,6 +816,14 @@ int colsumsq(const void* x, int64_t ld, float* out, int64_t P, int N, int64_t im
   return 0;
 }
 
+// per-image Gram-backward weights (gram_wd_kernel)
+template <typename T>
+int gram_wd(const float* D, const float* aq, const float* ak, void* wd, int64_t B, int c, int heads, hipStream_t st) {
+  const int64_t total = B * 4 * (int64_t)c * c;
+  hipLaunchKernelGGL(gram_wd_kernel<T>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, D, aq, ak, (T*)wd, c, heads, total);
+  return 0;
+}
+
 // device constants of the GEMM family (zero / one vectors for branch-free operands), per device
 static const float* train_consts(int which) {
   static std::mutex mu;
@@ -867,6 +948,13 @@ int turtle_train_colsumsq(const void* x, int64_t ld, float* out, int64_t P, int 
   if (!rows_ok(x, ld, dtype) || !out || P <= 0 || N <= 0 || N % 8 || N > 2048 || img_px <= 0 || P % img_px || P / img_px > 65535)
     return -1;
   TT_DISPATCH(dtype, colsumsq, x, ld, out, P, N, img_px, (hipStream_t)stream);
+}
+
+int turtle_train_gram_wd(const float* D, const float* aq, const float* ak, void* wd, int64_t B, int c, int heads, int dtype,
+                         void* stream) {
+  if (!D || !aq || !ak || !wd || B <= 0 || c <= 0 || heads <= 0 || c % heads || B * 4 * (int64_t)c * c > ((int64_t)1 << 40))
+    return -1;
+  TT_DISPATCH(dtype, gram_wd, D, aq, ak, wd, B, c, heads, (hipStream_t)stream);
 }
 
 int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride, int64_t img_px, const float* bias, void* y,

@@ -53,8 +53,8 @@ class _ChanSplit(torch.autograd.Function):
     channels-last per qkv split on the HIP graph (the largest copy traffic of the training step)."""
 
     @staticmethod
-    def forward(ctx, x, *sizes):
-        ctx.sizes = sizes
+    def forward(ctx, x, sink, *sizes):
+        ctx.sizes, ctx.sink = sizes, sink
         ctx.cl = x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
         outs, a = [], 0
         for n in sizes:
@@ -64,6 +64,10 @@ class _ChanSplit(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
+        if ctx.sink is not None:        # the consumers wrote their gradients into one buffer
+            buf = ctx.sink.take(grads, ctx.sizes)
+            if buf is not None:
+                return (buf, None) + (None,) * len(ctx.sizes)
         parts = []
         for g, n in zip(grads, ctx.sizes):
             if g is None:
@@ -76,11 +80,11 @@ class _ChanSplit(torch.autograd.Function):
                 g = g.contiguous(memory_format=torch.channels_last)
             parts.append(g)
         out = torch.cat(parts, dim=1)
-        return (out,) + (None,) * len(ctx.sizes)
+        return (out, None) + (None,) * len(ctx.sizes)
 
 
-def _split(x, *sizes):
-    return _ChanSplit.apply(x, *sizes)
+def _split(x, *sizes, sink=None):
+    return _ChanSplit.apply(x, sink, *sizes)
 
 
 class _ToNCHW(torch.autograd.Function):
@@ -194,12 +198,17 @@ class TrainGraph:
             # on the op set's kernels: the Gram of the L2-normalised q, k (690-697) in one op over
             # the channel-adjacent [q | k] rows, softmax, then project_out . blockdiag(A) as one
             # per-image weight set applied to v (A v followed by project_out, 697-702)
-            qk, v = _split(qkv, 2 * c, c)
+            # the [q | k] and v slices' input gradients land in one buffer (GradSink): no concatenation
+            # in the split's backward
+            sink = ops.grad_sink(qkv) if getattr(ops, "grad_sink", None) and qkv.is_contiguous(
+                memory_format=torch.channels_last) and not qkv.is_contiguous() else None
+            qk, v = _split(qkv, 2 * c, c, sink=sink)
             ch = c // heads
-            a = torch.softmax(ops.norm_gram(qk, heads) * m.temperature, dim=-1)
+            kw = lambda off: {} if sink is None else {"sink": (sink, off)}
+            a = torch.softmax(ops.norm_gram(qk, heads, **kw(0)) * m.temperature, dim=-1)
             wp = m.project_out.weight.reshape(c, heads, ch)
             weff = torch.einsum("ohi,bhij->bohj", wp, a).reshape(b, c, c)
-            return ops.conv1x1(v, weff, m.project_out.bias), None, None
+            return ops.conv1x1(v, weff, m.project_out.bias, **kw(2 * c)), None, None
         if ntc is None and kc is None and vc is None and hasattr(ops, "gram"):
             # on the op set's kernels: Gram of the raw q, k over HW (per head) divided by the L2
             # norms (== normalising first, 690-693), softmax, then project_out . blockdiag(A) as
@@ -242,8 +251,12 @@ class TrainGraph:
         return t.reshape(b, c, ws, hh, ws, ww).permute(0, 3, 5, 2, 4, 1).reshape(b, 1, 1, hh * ww, ws * ws * c)
 
     @staticmethod
-    def _undilated(o, bt, c, hl, wl, ws):
+    def _undilated(o, bt, c, hl, wl, ws, cl=False):
+        """Inverse of _dilated; ``cl``: the same values as a channels-last [bt, c, hl, wl] tensor (one
+        NHWC copy instead of an NCHW one the next GEMM would re-lay out)."""
         hh, ww = hl // ws, wl // ws
+        if cl:
+            return o.reshape(bt, hh, ww, ws, ws, c).permute(0, 3, 1, 4, 2, 5).reshape(bt, hl, wl, c).permute(0, 3, 1, 2)
         return o.reshape(bt, hh, ww, ws, ws, c).permute(0, 5, 3, 1, 4, 2).reshape(bt, c, hl, wl)
 
     def _sab(self, m, x, ws, ntc, kc, vc):
@@ -269,11 +282,13 @@ class TrainGraph:
         t = k.shape[1]
         s = (q @ k.transpose(-2, -1)) * m.temperature                   # [b, t, 1, n, n]
         top = torch.zeros_like(s).scatter_(-1, torch.topk(s, SAB_TOPK, dim=-1).indices, 1.0)
-        s = s * top + s * self._ball_mask(th, tw, s.device, s.dtype)
+        # s * top + s * ball as s * (top + ball): the same values bit for bit (factors 0 / 1 / 2 are
+        # exact), one full-size pass fewer forward and backward
+        s = s * top.add_(self._ball_mask(th, tw, s.device, s.dtype))
         zero = s == 0
         p = torch.softmax(s.masked_fill(zero, float("-inf")), dim=-1).masked_fill(zero, 0.0)
         a = p / p.sum(dim=-1, keepdim=True)
-        o = self._undilated(a @ vt, b * t, c, hl, wl, ws)
+        o = self._undilated(a @ vt, b * t, c, hl, wl, ws, getattr(self._ops(), "channels_last", False))
         o = self._c1(m.project_out, o).reshape(b, t, c, hl, wl)
         return o, k[:, -ntc:], vt[:, -ntc:]
 
@@ -367,8 +382,13 @@ class TrainGraph:
         e1 = self._dense(img.float(), ip.weight, ip.bias)
         ks, vs = [], []
         e1, k, v = self._level("encoder_level1", e1, k_cached[0], v_cached[0]); ks.append(k); vs.append(v)
-        down = lambda m, t: F.pixel_unshuffle(self._dense(t, m.body[0].weight), 2)     # Downsample 136-144
-        up = lambda m, t: F.pixel_shuffle(self._dense(t, m.body[0].weight), 2)         # Upsample 146-154
+        # Downsample 136-144 / Upsample 146-154. On the channels-last op set the shuffled map is made
+        # channels-last once here (pixel_(un)shuffle returns NCHW on ROCm): otherwise the next level's
+        # residual stream stays NCHW and every LayerNorm / GEMM of the level re-lays its input out
+        cl = (lambda t: t.contiguous(memory_format=torch.channels_last)) if getattr(self._ops(), "channels_last", False) \
+            else (lambda t: t)
+        down = lambda m, t: cl(F.pixel_unshuffle(self._dense(t, m.body[0].weight), 2))
+        up = lambda m, t: cl(F.pixel_shuffle(self._dense(t, m.body[0].weight), 2))
         e2, k, v = self._level("encoder_level2", down(self.down1_2, e1), k_cached[1], v_cached[1]); ks.append(k); vs.append(v)
         e3, k, v = self._level("encoder_level3", down(self.down2_3, e2), k_cached[2], v_cached[2]); ks.append(k); vs.append(v)
         lat, k1, v1, k2, v2 = self._latent(down(self.down3_4, e3), k_cached[3], v_cached[3], k_cached[4], v_cached[4])

@@ -49,6 +49,7 @@ def lib():
     L.turtle_train_rgemm_workspace.restype = sz
     L.turtle_train_rgemm.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, i64, ci, ci, vp, sz, vp]
     L.turtle_train_colsumsq.argtypes = [vp, i64, vp, i64, ci, i64, ci, vp]
+    L.turtle_train_gram_wd.argtypes = [vp, vp, vp, vp, i64, ci, ci, ci, vp]
     _train = L
     return L
 
@@ -131,8 +132,8 @@ class _LayerNorm(torch.autograd.Function):
         B, Cc, H, W = x.shape
         P = B * H * W
         dx = _empty(B, Cc, H, W, x)
-        dw = torch.zeros(Cc, dtype=torch.float32, device=x.device)
-        db = torch.zeros(Cc, dtype=torch.float32, device=x.device) if ctx.has_b else None
+        z = torch.zeros(2 * Cc if ctx.has_b else Cc, dtype=torch.float32, device=x.device)    # one fill for both
+        dw, db = z[:Cc], (z[Cc:] if ctx.has_b else None)
         dt = _dt(x) | ((_dt(dy) + 1) << 4 if dy.dtype != x.dtype else 0)
         _check(lib().turtle_train_ln_bwd(_p(x), ctx.ldx, _p(w32), _p(mu), _p(rs), _p(dy), lddy, _p(dx), Cc, _p(dw), _p(db), P, Cc,
                                          int(ctx.biasfree), dt, _stream(x)), "ln_bwd")
@@ -163,8 +164,8 @@ class _DWConv(torch.autograd.Function):
         # passed as a plain forward so the row-sweeping kernel takes it
         w9f = w9.flip(0).contiguous()
         _check(lib().turtle_train_dw3x3_fwd(_p(dy), lddy, _p(w9f), None, _p(dx), Cc, B, Cc, H, W, 0, _dt(x), st), "dw_dgrad")
-        dw9 = torch.zeros(9, Cc, dtype=torch.float32, device=x.device)
-        db = torch.zeros(Cc, dtype=torch.float32, device=x.device) if ctx.has_b else None
+        z = torch.zeros(10 * Cc if ctx.has_b else 9 * Cc, dtype=torch.float32, device=x.device)  # one fill for both
+        dw9, db = z[:9 * Cc].view(9, Cc), (z[9 * Cc:] if ctx.has_b else None)
         _check(lib().turtle_train_dw3x3_wgrad(_p(x), ctx.ldx, _p(dy), lddy, _p(dw9), _p(db), B, Cc, H, W, _dt(x), st), "dw_wgrad")
         return dx, dw9.t().reshape(Cc, 1, 3, 3), db
 
@@ -205,15 +206,60 @@ def _rgemm(a, lda, b, ldb, P, N, K, img_px):
     return c
 
 
-def _gemm_into(x, ldx, w, img_px, bias, P, K, N):
+def _gemm_into(x, ldx, w, img_px, bias, P, K, N, out=None):
     """y = x w^T (+ bias): x rows [P][ldx] of a [B, K, H, W] tensor; w [N, K] or [nimg, N, K] in x's
-    dtype; returns a channels_last [B, N, H, W] tensor."""
+    dtype; returns a channels_last [B, N, H, W] tensor, or writes ``out`` (NHWC rows with their own
+    pixel stride: a channel slice of a wider tensor) and returns it."""
     B, _, H, W = x.shape
-    y = _empty(B, N, H, W, x)
+    if out is None:
+        y, ldy = _empty(B, N, H, W, x), N
+    else:
+        y, ldy = rows(out)
+        if y is not out:
+            raise ValueError("gemm output slice is not NHWC rows")
     wstride = (N * K) if w.dim() == 3 else 0
-    _check(lib().turtle_train_gemm(_p(x), ldx, _p(w), wstride, img_px if wstride else 0, _p(bias), _p(y), N, P, K, N, _dt(x),
+    _check(lib().turtle_train_gemm(_p(x), ldx, _p(w), wstride, img_px if wstride else 0, _p(bias), _p(y), ldy, P, K, N, _dt(x),
                                    _stream(x)), "gemm")
     return y
+
+
+class GradSink:
+    """One input-gradient buffer for the channel slices of a channels-last tensor (the qkv map of a
+    channel attention, split into [q | k] and v: turtle_t1_arch.py:688-689). The HIP ops consuming
+    the slices write their input gradients straight into their channel range of the buffer (the
+    GEMM's output pixel stride is the full width), and the split's backward returns the buffer when
+    every slice gradient is that range, untouched - no concatenation pass. A slice claimed twice in
+    one backward (two consumers), or a gradient autograd had to accumulate, falls back to the
+    split's concatenation."""
+
+    def __init__(self, x):
+        self.shape, self.dtype, self.device = tuple(x.shape), x.dtype, x.device
+        self.buf, self.claimed = None, set()
+
+    def claim(self, off: int, n: int, dtype):
+        if dtype != self.dtype or off in self.claimed:
+            return None
+        if self.buf is None:
+            self.buf = torch.empty(self.shape, dtype=self.dtype, device=self.device, memory_format=CL)
+        self.claimed.add(off)
+        return self.buf.narrow(1, off, n)
+
+    def take(self, grads, sizes):
+        """The buffer if ``grads`` are exactly its claimed slices (then the sink resets), else None."""
+        buf, off = self.buf, 0
+        self.buf, self.claimed = None, set()
+        if buf is None:
+            return None
+        for g, n in zip(grads, sizes):
+            ref = buf.narrow(1, off, n)
+            if g is None or g.data_ptr() != ref.data_ptr() or g.shape != ref.shape or g.stride() != ref.stride():
+                return None
+            off += n
+        return buf
+
+
+def _sink_out(sink, n, dtype):
+    return None if sink is None else sink[0].claim(sink[1], n, dtype)
 
 
 class _WCast:
@@ -267,9 +313,10 @@ class _Conv1x1(torch.autograd.Function):
     """y = x W^T + b on NHWC rows; W [N, K] (shared) or [B, N, K] (one set per image)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, sink=None):
         gdt = _gemm_dt(x)
         out_dt = x.dtype
+        ctx.sink = sink
         xg, ldx = rows(x.to(gdt))
         B, K, H, W = xg.shape
         N = w.shape[-2]
@@ -290,7 +337,8 @@ class _Conv1x1(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             wt = ctx.wcache.transposed() if ctx.wcache is not None else wg.transpose(-1, -2).contiguous()   # [.., K, N]
-            dx = _gemm_into(dy, lddy, wt, HW, None, P, N, K).to(ctx.in_dt)
+            dst = _sink_out(ctx.sink, K, ctx.in_dt) if xg.dtype == ctx.in_dt else None
+            dx = _gemm_into(dy, lddy, wt, HW, None, P, N, K, out=dst).to(ctx.in_dt)
         if ctx.needs_input_grad[1]:
             if wg.dim() == 3:
                 dw = _rgemm(dy, lddy, xg, ctx.ldx, P, N, K, HW)  # [B, N, K]
@@ -300,7 +348,7 @@ class _Conv1x1(torch.autograd.Function):
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = torch.zeros(N, dtype=torch.float32, device=dy.device)
             _check(lib().turtle_train_colsum(_p(dy), lddy, _p(db), P, N, _dt(dy), _stream(dy)), "colsum")
-        return dx, dw, db
+        return dx, dw, db, None
 
 
 class _Gram(torch.autograd.Function):
@@ -346,9 +394,10 @@ class _NormGram(torch.autograd.Function):
     copies of q and k nor the norm ops' elementwise passes of the ATen formulation exist."""
 
     @staticmethod
-    def forward(ctx, qk, heads: int):
+    def forward(ctx, qk, heads: int, sink=None):
         gdt = _gemm_dt(qk)
         in_dt = qk.dtype
+        ctx.sink = sink
         qk, ld = rows(qk.to(gdt))
         B, C2, H, W = qk.shape
         c = C2 // 2
@@ -380,16 +429,14 @@ class _NormGram(torch.autograd.Function):
         live = (n > 1e-12).float()
         aq = (-t.sum(-1) / (nq * nq)).reshape(B, c) * live[:, :c]          # dL/d|q_i| / |q_i|
         ak = (-t.sum(-2) / (nk * nk)).reshape(B, c) * live[:, c:]
-        Wd = torch.zeros(B, C2, C2, dtype=torch.float32, device=qk.device)
-        idx = torch.arange(c, device=qk.device)
-        Wd[:, idx, idx] = aq
-        Wd[:, c + idx, c + idx] = ak
-        for h in range(heads):
-            s0, s1 = h * ch, (h + 1) * ch
-            Wd[:, s0:s1, c + s0:c + s1] = D[:, h]
-            Wd[:, c + s0:c + s1, s0:s1] = D[:, h].transpose(1, 2)
-        dqk = _gemm_into(qk, ctx.ld, Wd.to(qk.dtype).contiguous(), HW, None, P, C2, C2)
-        return dqk.to(ctx.in_dt), None
+        # Wd [B, 2c, 2c] = [[diag(aq), D], [D^T, diag(ak)]] built densely in the GEMM dtype by one
+        # kernel (no fp32 zero-fill, block scatter and cast passes)
+        Wd = torch.empty(B, C2, C2, dtype=qk.dtype, device=qk.device)
+        D, aq, ak = D.contiguous(), aq.contiguous(), ak.contiguous()
+        _check(lib().turtle_train_gram_wd(_p(D), _p(aq), _p(ak), _p(Wd), B, c, heads, _dt(qk), _stream(qk)), "gram_wd")
+        dst = _sink_out(ctx.sink, C2, ctx.in_dt) if qk.dtype == ctx.in_dt else None
+        dqk = _gemm_into(qk, ctx.ld, Wd, HW, None, P, C2, C2, out=dst)
+        return dqk.to(ctx.in_dt), None, None
 
 
 def _act_dtype(x: torch.Tensor) -> torch.dtype:
@@ -423,17 +470,20 @@ class HipOps:
     def gelu_gate(x):
         return _Gate.apply(_act(x))
 
+    grad_sink = GradSink
+
     @staticmethod
-    def conv1x1(x, w, b):
-        """nn.Conv2d(K, N, 1)(x): w [N, K, 1, 1] (or [B, N, K]: one weight set per image)."""
-        return _Conv1x1.apply(_act(x), w.reshape(w.shape[0], w.shape[1]) if w.dim() == 4 else w, b)
+    def conv1x1(x, w, b, sink=None):
+        """nn.Conv2d(K, N, 1)(x): w [N, K, 1, 1] (or [B, N, K]: one weight set per image). ``sink``
+        (GradSink, channel offset): write the input gradient into that slice of the sink's buffer."""
+        return _Conv1x1.apply(_act(x), w.reshape(w.shape[0], w.shape[1]) if w.dim() == 4 else w, b, sink)
 
     @staticmethod
     def gram(q, k, heads: int):
         return _Gram.apply(_act(q), _act(k), heads)
 
     @staticmethod
-    def norm_gram(qk, heads: int):
+    def norm_gram(qk, heads: int, sink=None):
         """[b, heads, ch, ch] Gram of the L2-normalised (over HW) q and k, the first / second half of
-        qk's channels."""
-        return _NormGram.apply(_act(qk), heads)
+        qk's channels (``sink`` as in conv1x1)."""
+        return _NormGram.apply(_act(qk), heads, sink)
