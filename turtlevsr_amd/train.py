@@ -47,7 +47,7 @@ def _conv1(m, x):
 
 
 class _ChanSplit(torch.autograd.Function):
-    """x[:, a:b] channel slices whose backward concatenates the slice gradients in x's memory
+    """x[:, a:b] channel slices whose backward assembles the slice gradients in x's memory
     format. Plain slicing's backward (slice_backward) builds each slice gradient into a zero-filled
     NCHW tensor and sums them: three fills, three transposing copies and a re-layout back to
     channels-last per qkv split on the HIP graph (the largest copy traffic of the training step)."""
@@ -68,16 +68,27 @@ class _ChanSplit(torch.autograd.Function):
             buf = ctx.sink.take(grads, ctx.sizes)
             if buf is not None:
                 return (buf, None) + (None,) * len(ctx.sizes)
+        ref = next(t for t in grads if t is not None)
+        if ctx.cl:
+            # each slice gradient copied once, in whatever layout it arrives, straight into its
+            # channel range of the channels-last result (not re-laid out first, then concatenated)
+            shape = list(ref.shape)
+            shape[1] = sum(ctx.sizes)
+            out = torch.empty(shape, dtype=ref.dtype, device=ref.device, memory_format=torch.channels_last)
+            a = 0
+            for g, n in zip(grads, ctx.sizes):
+                if g is None:
+                    out.narrow(1, a, n).zero_()
+                else:
+                    out.narrow(1, a, n).copy_(g)
+                a += n
+            return (out, None) + (None,) * len(ctx.sizes)
         parts = []
         for g, n in zip(grads, ctx.sizes):
             if g is None:
-                ref = next(t for t in grads if t is not None)
                 shape = list(ref.shape)
                 shape[1] = n
-                g = torch.zeros(shape, dtype=ref.dtype, device=ref.device,
-                                memory_format=torch.channels_last if ctx.cl else torch.contiguous_format)
-            elif ctx.cl:
-                g = g.contiguous(memory_format=torch.channels_last)
+                g = torch.zeros(shape, dtype=ref.dtype, device=ref.device)
             parts.append(g)
         out = torch.cat(parts, dim=1)
         return (out, None) + (None,) * len(ctx.sizes)
