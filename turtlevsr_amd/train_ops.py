@@ -403,9 +403,14 @@ class _NormGram(torch.autograd.Function):
         c = C2 // 2
         ch = c // heads
         P, HW = B * H * W, H * W
-        G = torch.empty(B, heads, ch, ch, dtype=torch.float32, device=qk.device)
-        for h in range(heads):
-            G[:, h] = _rgemm(qk[:, h * ch:(h + 1) * ch], ld, qk[:, c + h * ch:c + (h + 1) * ch], ld, P, ch, ch, HW)
+        if heads == 1:
+            G = _rgemm(qk[:, :c], ld, qk[:, c:], ld, P, c, c, HW).view(B, 1, c, c)
+        else:
+            # one reduction GEMM over all c x c channel pairs, then the heads' diagonal blocks: the
+            # GEMM is bound by reading q and k (read once either way), and one launch pair replaces
+            # `heads` GEMM + reduce + block-copy triples
+            Gf = _rgemm(qk[:, :c], ld, qk[:, c:], ld, P, c, c, HW)                  # [B, c, c]
+            G = Gf.view(B, heads, ch, heads, ch).diagonal(dim1=1, dim2=3).permute(0, 3, 1, 2).contiguous()
         ss = torch.zeros(B, C2, dtype=torch.float32, device=qk.device)
         _check(lib().turtle_train_colsumsq(_p(qk), ld, _p(ss), P, C2, HW, _dt(qk), _stream(qk)), "colsumsq")
         n = ss.sqrt()
