@@ -140,12 +140,29 @@ class _LayerNorm(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
+_DWCACHE = WeakIdKeyDictionary()
+
+
+def _dw_taps(w):
+    """(w9, w9 flipped): the depthwise weight [C, 1, 3, 3] as fp32 tap-major [9, C] tables for the
+    forward and the data gradient, built once per parameter version (5 frames x forward + backward
+    reuse them) - the same validity rule as the GEMM weight casts (_WCast)."""
+    if not isinstance(w, torch.nn.Parameter):
+        w9 = w.detach().float().reshape(w.shape[0], 9).t().contiguous()
+        return w9, w9.flip(0).contiguous()
+    e = _DWCACHE.get(w)
+    if e is None or e[0] != w._version or e[1] != w.data_ptr() or e[2].device != w.device:
+        w9 = w.detach().float().reshape(w.shape[0], 9).t().contiguous()
+        e = _DWCACHE[w] = (w._version, w.data_ptr(), w9, w9.flip(0).contiguous())
+    return e[2], e[3]
+
+
 class _DWConv(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x, ldx = rows(x)
         B, Cc, H, W = x.shape
-        w9 = w.float().reshape(Cc, 9).t().contiguous()
+        w9, ctx.w9f = _dw_taps(w)
         b32 = None if b is None else b.float().contiguous()
         y = _empty(B, Cc, H, W, x)
         _check(lib().turtle_train_dw3x3_fwd(_p(x), ldx, _p(w9), _p(b32), _p(y), Cc, B, Cc, H, W, 0, _dt(x), _stream(x)), "dw_fwd")
@@ -162,7 +179,7 @@ class _DWConv(torch.autograd.Function):
         st = _stream(x)
         # dx = depthwise of dy with the taps flipped (correlation transposed); the flipped table is
         # passed as a plain forward so the row-sweeping kernel takes it
-        w9f = w9.flip(0).contiguous()
+        w9f = ctx.w9f
         _check(lib().turtle_train_dw3x3_fwd(_p(dy), lddy, _p(w9f), None, _p(dx), Cc, B, Cc, H, W, 0, _dt(x), st), "dw_dgrad")
         z = torch.zeros(10 * Cc if ctx.has_b else 9 * Cc, dtype=torch.float32, device=x.device)  # one fill for both
         dw9, db = z[:9 * Cc].view(9, Cc), (z[9 * Cc:] if ctx.has_b else None)
@@ -291,6 +308,7 @@ _WCACHE = WeakIdKeyDictionary()
 def clear_weight_cache():
     """Drop every cached weight cast (after parameter writes that bypass the version counter)."""
     _WCACHE.clear()
+    _DWCACHE.clear()
 
 
 def _weight_cast(w, gdt):
