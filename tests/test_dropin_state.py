@@ -132,3 +132,37 @@ def test_assign_load_then_train_step_then_eval_uses_new_weights():
     with torch.no_grad():
         want, _, _ = ref(x)
     assert torch.equal(got, want), float((got - want).abs().max())
+
+
+def test_tiled_harness_keeps_one_small_arena_per_tile():
+    """the tiled protocol (harness.run_inference_patched, inference.py:172-246)
+    runs one B = 1 stream per tile position, interleaved frame by frame. Each stream keeps its own
+    SAB arena (a hit every frame: no roll copy), sized small (tnew + 6 frames within 6 frames), and
+    device memory stays flat from frame to frame instead of a full-budget arena per tile and call."""
+    from turtlevsr_amd.harness import run_video
+    from turtlevsr_amd.synthetic import synthetic_frames
+    _, meta = load("clip_gopro_64")
+    m = _model(meta["opt"], meta["seed"], "bf16")
+    clip = torch.from_numpy(synthetic_frames((1, 6, 3, 128, 192), 47))[0].cuda()
+    frames = [clip[j] for j in range(6)]
+    mem = []
+
+    class Probe:
+        def __call__(self, x, k, v):
+            return m(x, k, v)
+
+    with torch.no_grad():
+        for n in (3, 6):
+            torch.cuda.synchronize()
+            run_video(frames[:n], frames[:n], Probe(), tile=64, tile_overlap=16)
+            torch.cuda.synchronize()
+            mem.append(torch.cuda.memory_allocated())
+    ntile = 3 * 4                                   # tile starts: h [0, 48, 64], w [0, 48, 96, 128]
+    for slot, streams in m._arenas.items():
+        assert len(streams) <= 2 * ntile            # two videos ran; at most one arena per tile each
+        for a in streams:
+            assert a["extra"] == m._ARENA_EXTRA     # no stream outgrew its first arena in 6 frames
+    m.release_history()
+    torch.cuda.synchronize()
+    assert torch.cuda.memory_allocated() <= mem[-1]
+    assert mem[1] < mem[0] + (256 << 20)

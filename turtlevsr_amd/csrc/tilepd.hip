@@ -74,6 +74,15 @@ TURTLE_DEV void tp_vmwait(bf16x8& a, bf16x8& b) {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
 }
+// the same for the two ring slots that are live across the pass loop's back-edge (and its entry):
+// those fragments must have landed before the edge, because the register allocator may copy a
+// loop-carried value there - an asm load's destination still in flight would be copied half-written
+// (tools/check_asm_vmem.py finds such copies; round 4's sab_avt fault was one)
+template <int N>
+TURTLE_DEV void tp_vmwait_ring(bf16x8 (&w)[3][2]) {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[1][0]), "+v"(w[1][1]) : "n"(N) : "memory");
+}
 
 template <int MODE, int CM, int RH, int N1M, int DBG>
 __global__ __launch_bounds__(TP_NT, 1) void tilepd_kernel(TilePdArgs a) {
@@ -91,6 +100,21 @@ __global__ __launch_bounds__(TP_NT, 1) void tilepd_kernel(TilePdArgs a) {
   // waves 4..7 (each sharing a SIMD with one of 0..3) win issue arbitration: the two waves of a SIMD
   // drift out of phase, so one's MFMA phase runs beside the other's depthwise (VALU) phase
   if (wid >= TP_NW / 2) __builtin_amdgcn_s_setprio(1);
+
+  // W1 fragments: a 3-deep ring of K steps (see the pass loop); the first pass's first two steps are
+  // issued here, so they land during the prologue
+  const bf16* W1 = reinterpret_cast<const bf16*>(a.w1);
+  const int hid = MODE == TP_GATE ? N1 / 2 : N1;
+  const int npass = MODE == TP_GATE ? hid / 16 : N1 / 32;
+  auto row0 = [&](int u, int t) __attribute__((always_inline)) { return MODE == TP_GATE ? (t ? hid : 0) + 16 * u : 32 * u + 16 * t; };
+  bf16x8 wf[3][2];
+  auto load_w = [&](int uu, int k) __attribute__((always_inline)) {
+    const int uc = uu < npass ? uu : 0;                     // past the last pass: a harmless in-range reload
+#pragma unroll
+    for (int t = 0; t < 2; ++t) tp_gload(wf[k % 3][t], W1 + (int64_t)(row0(uc, t) + (lane & 15)) * CM + (lane >> 4) * 8 + k * 32);
+  };
+  load_w(wid, 0);
+  load_w(wid, 1);
 
   // ---- per-channel tables -> LDS once per block (bf16 taps [9][N1], GEMM1 epilogue and depthwise
   // bias fp32) ----
@@ -192,11 +216,7 @@ __global__ __launch_bounds__(TP_NT, 1) void tilepd_kernel(TilePdArgs a) {
   const float colok = (xg >= 0 && xg < a.W) ? 1.f : 0.f;
   const bool out_col = px >= 1 && px <= TP_TX && xg < a.W;
   const char* xb = sX + px * L::XP + grp * 16;
-  const bf16* W1 = reinterpret_cast<const bf16*>(a.w1);
-  const int hid = MODE == TP_GATE ? N1 / 2 : N1;
-  const int npass = MODE == TP_GATE ? hid / 16 : N1 / 32;
   bf16* out = reinterpret_cast<bf16*>(a.out);
-  auto row0 = [&](int u, int t) __attribute__((always_inline)) { return MODE == TP_GATE ? (t ? hid : 0) + 16 * u : 32 * u + 16 * t; };
   const int64_t pix0 = ((int64_t)img * a.H + y0) * a.W + (out_col ? xg : 0);   // output row 1 of this lane
 
   // W1 fragments: a 3-deep ring of K steps (two L2 loads in flight behind the step in use); the
@@ -205,19 +225,12 @@ __global__ __launch_bounds__(TP_NT, 1) void tilepd_kernel(TilePdArgs a) {
   // a fixed program order, and each wait counts exactly the ops issued after the awaited load (the
   // hardware retires vmcnt in issue order). hipcc's own counting sees no stores and would wait for
   // a pass's stores at the next pass's first K step
-  bf16x8 wf[3][2];
-  auto load_w = [&](int uu, int k) __attribute__((always_inline)) {
-    const int uc = uu < npass ? uu : 0;                     // past the last pass: a harmless in-range reload
-#pragma unroll
-    for (int t = 0; t < 2; ++t) tp_gload(wf[k % 3][t], W1 + (int64_t)(row0(uc, t) + px) * CM + grp * 8 + k * 32);
-  };
   // stores per pass (unconditional: sink lanes); none in the no-store ablation, whose waits must
   // not count them (an under-waited load lands in a register hipcc has since reused)
   constexpr int NS = (DBG & 16) ? 0 : (MODE == TP_GATE ? R : 2 * R);
   bf16* sinkp = reinterpret_cast<bf16*>(g_sink_tp) + ((blockIdx.x % TP_SINK_BLOCKS) * TP_NT + tid) * 4;
   float chk = 0.f;                                          // DBG 16 only
-  load_w(wid, 0);
-  load_w(wid, 1);
+  tp_vmwait_ring<0>(wf);                                    // loop entry: landed (see tp_vmwait_ring)
   for (int u = wid; u < npass; u += TP_NW) {
     const bool first = u == wid;
     f32x4 acc[2][RH];
@@ -351,6 +364,9 @@ __global__ __launch_bounds__(TP_NT, 1) void tilepd_kernel(TilePdArgs a) {
       dw_tile(1);
       store_rows(row0(u, 1) + grp * 4, 1, false);
     }
+    // back-edge: the next pass's first two K steps (issued before the depthwise, NS stores ago)
+    // have landed before the loop-carried ring slots can be copied
+    tp_vmwait_ring<NS>(wf);
   }
   if constexpr ((DBG & 16) != 0) {
     if (chk == -1.2345f) out[tid] = (bf16)chk;             // never true in practice: keeps the work alive

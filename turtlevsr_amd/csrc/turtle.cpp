@@ -765,7 +765,12 @@ struct Runner {
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store; g.cb_px = store == STORE_CB16 ? M : 0;
     g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel; g.allow_lds = h->gemm_lds; g.allow_pn = h->gemm_pn;
     g.allow_ar = h->gemm_ar; g.allow_kt = h->gemm_kt; g.kt_max_px = h->kt_max_px;
-    if (store == STORE_CB16 && (ES != 2 || !gemm_pn_ok(g)) && !(ES == 2 && h->gemm8 == 2 && gemm8_ok((g.allow_g8 = 1, g))))
+    // channel-blocked stores: the pn GEMM, or gemm8 when every projection may take it (eligibility
+    // tested on a copy; g.allow_g8 is set in one place, below)
+    GemmArgs g8t = g;
+    g8t.allow_g8 = 1;
+    const bool cb_g8 = ES == 2 && h->gemm8 == 2 && gemm8_ok(g8t);
+    if (store == STORE_CB16 && (ES != 2 || !gemm_pn_ok(g)) && !cb_g8)
       TFAIL(TURTLE_EINVAL, "channel-blocked store needs the pn GEMM (M " + std::to_string(M) + " N " + std::to_string(g.N) +
                                " K " + std::to_string(a.Ktot) + " HW " + std::to_string(HW) + ")");
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
@@ -1287,7 +1292,15 @@ struct Runner {
     T* q2f = buf(P * d2);
     T* k2f = buf(P * d2);
     T* qtok = buf((int64_t)B * N * d2);
-    const int sab_waves = h->sab_waves ? h->sab_waves : (d2 >= 256 ? 8 : 4);
+    // score blocks stage KT keys x d2 channels as 16-byte vectors split evenly over the block's
+    // threads (sab.hip load_tile): 8 waves only where that split is whole (d2 = 320 / 448 at bf16
+    // are not), else 4; a width neither divides is refused instead of reading stale LDS
+    const int sab_kt = d2 <= 256 ? 64 : 32, sab_vec = 16 / (int)ES;
+    auto sab_fits = [&](int w) { return d2 <= 512 && d2 % sab_vec == 0 && (sab_kt * (d2 / sab_vec)) % (w * 64) == 0; };
+    int sab_waves = h->sab_waves ? h->sab_waves : (d2 >= 256 ? 8 : 4);
+    if (!sab_fits(sab_waves)) sab_waves = 4;
+    if (!sab_fits(sab_waves))
+      TFAIL(TURTLE_EINVAL, "SAB token width " + std::to_string(d2) + " is not supported by the score kernel (d <= 512, whole 16-byte staging split)");
     const int nsplit = sab_score_nsplit(B, NT, N, d2, sab_waves);
     // partial lists sized for either block size, so the sab_waves switch never changes the workspace
     const int nsplit_ws = std::max(sab_score_nsplit(B, NT, N, d2, 4), sab_score_nsplit(B, NT, N, d2, 8));

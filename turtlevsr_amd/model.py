@@ -37,6 +37,7 @@ from typing import List, Optional
 
 import torch
 import torch.nn as nn
+from torch.nn.modules import module as _mod
 
 from . import _lib
 from .arch import resolve
@@ -44,6 +45,18 @@ from .params import TurtleParams
 from .train import TrainGraph
 
 _VERSION = operator.attrgetter("_version")
+
+# bumped by every parameter / submodule registration on any nn.Module (global torch hooks): the
+# drop-in module's cached parameter list is stale after one
+_REG_EPOCH = [0]
+
+
+def _bump_epoch(*_):
+    _REG_EPOCH[0] += 1
+
+
+_mod.register_module_parameter_registration_hook(_bump_epoch)
+_mod.register_module_module_registration_hook(_bump_epoch)
 
 _DT = {"fp32": (_lib.DTYPE_F32, torch.float32), "bf16": (_lib.DTYPE_BF16, torch.bfloat16)}
 
@@ -95,21 +108,19 @@ class TurtleHIP(TrainGraph, TurtleParams):
     def compute_dtype(self) -> torch.dtype:
         return _DT[self._dtype_name][1]
 
-    def __setattr__(self, name, value):
-        # a parameter / submodule (re)assigned on this module invalidates the cached parameter list
-        if isinstance(value, (nn.Parameter, nn.Module)):
-            self.__dict__.pop("_plist", None)
-        super().__setattr__(name, value)
-
     def _signature(self):
-        # parameter list cached (Parameter objects survive .to() and in-place loads; it is dropped
-        # by load_state_dict - assign=True swaps the objects -, refresh_weights and attribute
-        # assignment); the version sum catches in-place updates, the leading data pointers catch
-        # device moves and `.data` rebinding
+        # parameter list cached (Parameter objects survive .to() and in-place loads); rebuilt after
+        # load_state_dict (assign=True swaps the objects), refresh_weights, and whenever any module
+        # anywhere registered a parameter or submodule since (_REG_EPOCH: a Parameter or module
+        # assigned on a SUBmodule, e.g. blk.attn.temperature = nn.Parameter(...), counts too); the
+        # version sum catches in-place updates, the leading data pointers catch device moves and
+        # `.data` rebinding
         ps = self.__dict__.get("_plist")
-        if ps is None:
+        if ps is None or self.__dict__.get("_plist_epoch") != _REG_EPOCH[0]:
+            self.__dict__["_plist_epoch"] = _REG_EPOCH[0]
             ps = self.__dict__["_plist"] = list(self.parameters())
-        return (ps[0].device, self._dtype_name, sum(map(_VERSION, ps)), tuple(p.data_ptr() for p in ps[:4]))
+        return (ps[0].device, self._dtype_name, self.__dict__["_plist_epoch"], sum(map(_VERSION, ps)),
+                tuple(p.data_ptr() for p in ps[:4]))
 
     def refresh_weights(self):
         """Pack the current parameters into the device layout (done automatically on change)."""
@@ -242,38 +253,58 @@ class TurtleHIP(TrainGraph, TurtleParams):
         self._keepalive = (inp, k_in, v_in)
         return out, k_out, v_out
 
-    # SAB history slots (B = 1): the returned k / v are views of a per-slot frame arena, laid out
-    # so that the new cache's kept frames ARE the incoming cache's last frames - the library then
-    # skips the roll copy (turtle.cpp chm: source == destination) and only writes the current frame.
-    # Every arena frame is written once and never again (the history stays immutable for callers
-    # holding older caches); an incoming cache that is not the arena's latest (a branched or
-    # moved history, B > 1) gets a fresh arena that the library fills by copying.
-    _ARENA_EXTRA = 6                  # minimum frames of headroom
+    # SAB history slots (B = 1): the returned k / v are views of a frame arena, laid out so that
+    # the new cache's kept frames ARE the incoming cache's last frames - the library then skips the
+    # roll copy (turtle.cpp chm: source == destination) and only writes the current frame. Every
+    # arena frame is written once and never again (the history stays immutable for callers holding
+    # older caches). Arenas are kept per STREAM: each slot holds a short LRU list, and a call's
+    # arena is the one whose latest frames its incoming cache is (interleaved B = 1 streams - the
+    # tiled harness runs one per tile position - each keep their own). A stream starts with a small
+    # arena (tnew + _ARENA_EXTRA frames) and doubles its headroom at each refill, up to the byte
+    # budget, so only a long single stream ends up with a large one; an incoming cache that is no
+    # arena's latest (a branched or moved history, B > 1) gets a fresh small arena filled by copying.
+    _ARENA_EXTRA = 6                  # initial frames of headroom
     _ARENA_MAX_EXTRA = 64
-    _ARENA_BYTES = 6 << 30            # per slot
+    _ARENA_BYTES = 6 << 30            # per stream and slot, reached only by doubling
+    _ARENA_STREAMS = 64               # arenas remembered per slot (least recently used dropped)
+
+    def release_history(self):
+        """Drop the SAB history arenas this module keeps for fast cache hand-over (caches the caller
+        still holds stay valid: they own their storage)."""
+        self.__dict__["_arenas"] = {}
 
     def _sab_out(self, i, ks, vs, tin, kin, vin, cdt, dev):
         if ks[0] != 1:
             return torch.empty(ks, dtype=cdt, device=dev), torch.empty(vs, dtype=cdt, device=dev)
-        arenas = self.__dict__.setdefault("_arenas", {})
+        streams = self.__dict__.setdefault("_arenas", {}).setdefault(i, [])
         tnew = ks[1]
         first = tin - (tnew - 1)                  # first incoming frame kept in the new cache
-        a = arenas.get(i)
-        if a is not None and tin > 0 and a["k"].dtype == cdt and a["k"].device == dev and \
-                tuple(a["k"].shape[1:]) == tuple(ks[2:]) and tuple(a["v"].shape[1:]) == tuple(vs[2:]):
-            s0 = a["next"] - tin                  # arena index of the incoming cache's frame 0
-            if s0 >= 0 and s0 + first + tnew <= a["k"].shape[0] and \
-                    kin.data_ptr() == a["k"][s0].data_ptr() and vin.data_ptr() == a["v"][s0].data_ptr():
-                b = s0 + first
-                a["next"] = b + tnew
-                return a["k"][b:b + tnew].unsqueeze(0), a["v"][b:b + tnew].unsqueeze(0)
-        # frames of headroom: a refill copies the kept frames once per `extra` frames, so size the
-        # arena by bytes (HBM is plentiful; a 1080p level-1 slot is ~0.27 GB per frame)
         fbytes = (math.prod(ks[2:]) + math.prod(vs[2:])) * torch.empty(0, dtype=cdt).element_size()
-        extra = max(self._ARENA_EXTRA, min(self._ARENA_MAX_EXTRA, self._ARENA_BYTES // max(fbytes, 1)))
+        extra = self._ARENA_EXTRA
+        if tin > 0:
+            for j, a in enumerate(streams):
+                if a["k"].dtype != cdt or a["k"].device != dev or tuple(a["k"].shape[1:]) != tuple(ks[2:]) or \
+                        tuple(a["v"].shape[1:]) != tuple(vs[2:]):
+                    continue
+                s0 = a["next"] - tin              # arena index of the incoming cache's frame 0
+                if s0 < 0 or kin.data_ptr() != a["k"][s0].data_ptr() or vin.data_ptr() != a["v"][s0].data_ptr():
+                    continue
+                del streams[j]
+                b = s0 + first
+                if b + tnew <= a["k"].shape[0]:
+                    a["next"] = b + tnew
+                    streams.append(a)             # most recently used last
+                    return a["k"][b:b + tnew].unsqueeze(0), a["v"][b:b + tnew].unsqueeze(0)
+                # this stream outgrew its arena: refill into one with twice the headroom (a refill
+                # copies the kept frames; HBM is plentiful, a 1080p level-1 slot is ~0.27 GB a frame)
+                cap_bytes = max(self._ARENA_EXTRA, min(self._ARENA_MAX_EXTRA, self._ARENA_BYTES // max(fbytes, 1)))
+                extra = min(cap_bytes, 2 * a["extra"])
+                break
         cap = tnew + extra
-        a = arenas[i] = dict(k=torch.empty((cap,) + tuple(ks[2:]), dtype=cdt, device=dev),
-                             v=torch.empty((cap,) + tuple(vs[2:]), dtype=cdt, device=dev), next=tnew)
+        a = dict(k=torch.empty((cap,) + tuple(ks[2:]), dtype=cdt, device=dev),
+                 v=torch.empty((cap,) + tuple(vs[2:]), dtype=cdt, device=dev), next=tnew, extra=extra)
+        streams.append(a)
+        del streams[:-self._ARENA_STREAMS]
         return a["k"][:tnew].unsqueeze(0), a["v"][:tnew].unsqueeze(0)
 
     @staticmethod
