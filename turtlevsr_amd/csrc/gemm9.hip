@@ -1,0 +1,378 @@
+// bf16 projection GEMM with 256 x 256 output tiles on FOUR waves ("g9" kernel): each wave owns a
+// 128-pixel x 128-channel quadrant, i.e. 64 accumulator tiles of 16 x 16 (256 of the SIMD's 512
+// registers, in the accumulation file), so every fragment read from LDS feeds 8 MFMAs and one
+// barrier covers 64 MFMAs (1,024 matrix-pipe cycles) of every SIMD.
+//
+//   out[m][n] = epilogue( sum_k A[m][k] * W[n][k] )        m = pixel, n = output channel
+//
+// Where it is used: the large plain / LayerNorm-folded 1x1 projections that ran on hipBLASLt
+// (latent level: LN project_in 512 -> 2560, LN qkv 512 -> 1536, project_out 1280 -> 512, W_eff
+// 512 -> 512 per image; level 3: W_eff 256 -> 256 per image) - turtle_t1_arch.py:159-178, 666-702.
+//
+// Structure (MI355X, one 256-thread block per CU at 1 wave per SIMD):
+//   * K steps of 32. The block stages a step's A (256 pixel rows x 64 B) and W (256 channel rows x
+//     64 B) tiles through registers: each thread issues 8 global_load_dwordx4 four steps before the
+//     step's MFMAs and writes them to one of two 32 KB LDS slots two steps later (ds_write_b128), so
+//     the global loads have two steps of MFMAs (~2,000 cycles) to land; nothing is asm: hipcc counts
+//     every vmcnt / lgkmcnt itself (no hand-counted waits);
+//   * per step: one barrier, then the next step's 16 fragments are read from the other slot while
+//     the 64 MFMAs of this step run (fragment registers double-buffered);
+//   * LDS rows of 64 B (32 k): 16-byte chunk c of row r sits at position c ^ ((r >> 2) & 2), which
+//     makes the 16-row fragment reads (ds_read_b128) and the staging writes (ds_write_b128)
+//     conflict-free on gfx950's lane groups (exhaustive check over the lane groups of both);
+//   * weight rows are placed in pn's permuted order (MFMA row 4g+e of sub-tile s <- channel 8g+4s+e
+//     of a 32-channel group), so a lane's accumulators of two sub-tiles are 8 CONSECUTIVE channels of
+//     one pixel: 16-byte residual loads and stores;
+//   * LayerNorm (turtle_t1_arch.py:83-112) folded into the epilogue: W' = W diag(g), s = rowsum(W'),
+//     t = W b, and out = rs (acc - mu s) + t + bias with the per-pixel (mu, rs) of a small statistics
+//     pass (ln_stats_kernel below, two-pass variance like the reference) - no normalised copy of the
+//     activations (the hipBLASLt path wrote one);
+//   * XCD-aware tile order: the channel tiles of one pixel panel run on one XCD (shared A panel in L2).
+#include <algorithm>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace turtle {
+
+namespace {
+
+constexpr int G9_BK = 32;
+constexpr int G9_SLOT = 32768;                 // A 16 KB + W 16 KB
+constexpr int G9_LDS = 2 * G9_SLOT;
+
+// MFMA row -> channel inside a 32-channel group (see header)
+TURTLE_DEV int g9_perm(int r) { return (r & ~31) | (8 * ((r >> 2) & 3) + 4 * ((r >> 4) & 1) + (r & 3)); }
+// byte offset of 16-byte chunk c of LDS row r (64-byte rows, swizzled)
+TURTLE_DEV int g9_off(int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 2)) << 4); }
+
+}  // namespace
+
+// DBG (tools/g8bench ablations only; 0 in the library): 1 no MFMA, 2 no global loads in the loop,
+// 4 no LDS traffic in the loop, 16 no epilogue stores
+template <bool LN, int DBG = 0>
+__global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs g, const float2* __restrict__ stats) {
+  __shared__ __attribute__((aligned(16))) char smem[G9_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wid >> 1, wn = wid & 1;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // ---- tile: the channel tiles of one pixel panel are consecutive ids on one XCD ----
+  const int ntn = (g.N + 255) / 256;
+  int lin = blockIdx.x;
+  {
+    const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
+    lin = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + y;
+  }
+  const int nt = lin % ntn, mt = lin / ntn;
+  int64_t m0, mlim;
+  if (g.wstride) {                                  // per-image weight sets: tiles never straddle images
+    const int tpi = (g.HW + 255) / 256;
+    const int64_t im = mt / tpi;
+    m0 = im * g.HW + (int64_t)(mt % tpi) * 256;
+    mlim = min(g.M, (im + 1) * (int64_t)g.HW);
+  } else {
+    m0 = (int64_t)mt * 256;
+    mlim = g.M;
+  }
+  const int n0 = nt * 256;
+  const int K = g.a.Ktot, nk = K / G9_BK;
+  const bf16* Wp = reinterpret_cast<const bf16*>(g.w) + (g.wstride ? (int64_t)(m0 / g.HW / g.wdiv) * g.wstride : 0);
+
+  // ---- staging geometry: thread loads chunk c = tid & 3 of rows tid / 4 + 64 i (i = 0..3) of both tiles ----
+  const int sc = tid & 3, sr0 = tid >> 2;
+  int64_t xrow[4];                                  // clamped pixel rows
+  const bf16* wrow[4];                              // weight rows (permuted, clamped)
+  int soff[4];                                      // swizzled LDS offsets (same for A and W rows)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = sr0 + 64 * i;
+    const int64_t m = m0 + r;
+    xrow[i] = m < mlim ? m : m0;
+    wrow[i] = Wp + (int64_t)min(n0 + g9_perm(r), g.N - 1) * g.ldw + sc * 8;
+    soff[i] = g9_off(r, sc);
+  }
+  uint4 ga[4], gw[4];                               // one staged K step
+  // single-source operand (every LN GEMM and most plain ones): row byte offsets computed once
+  const bool one_src = g.a.n == 1;
+  const bf16* xbase0 = reinterpret_cast<const bf16*>(g.a.s[0].base) + g.a.s[0].off + sc * 8;
+  int64_t xoff0[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) xoff0[i] = xrow[i] * g.a.s[0].ld;
+  auto gload = [&](int t) __attribute__((always_inline)) {
+    if constexpr ((DBG & 2) != 0) return;
+    const int k0 = t * G9_BK;
+    if (one_src) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ga[i] = ld16(xbase0 + xoff0[i] + k0);
+    } else {
+      // the K step's source (steps never straddle two: every source is a multiple of 32 wide)
+      const bf16* base = reinterpret_cast<const bf16*>(g.a.s[0].base);
+      int64_t sld = g.a.s[0].ld;
+      int soffs = g.a.s[0].off, kb = 0, kbj = g.a.s[0].K;
+#pragma unroll
+      for (int j = 1; j < TURTLE_MAX_SRC; ++j) {
+        const bool hit = j < g.a.n && k0 >= kbj;
+        base = hit ? reinterpret_cast<const bf16*>(g.a.s[j].base) : base;
+        sld = hit ? g.a.s[j].ld : sld;
+        soffs = hit ? g.a.s[j].off : soffs;
+        kb = hit ? kbj : kb;
+        kbj += j < g.a.n ? g.a.s[j].K : 0;
+      }
+      const bf16* b2 = base + soffs + (k0 - kb) + sc * 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ga[i] = ld16(b2 + xrow[i] * sld);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gw[i] = ld16(wrow[i] + k0);
+  };
+  auto swrite = [&](int slot) __attribute__((always_inline)) {
+    if constexpr ((DBG & 4) != 0) return;
+    char* sb = smem + slot * G9_SLOT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(sb + soff[i]) = ga[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(sb + 16384 + soff[i]) = gw[i];
+  };
+  // fragment reads: rows wm*128 + 16 i + fr of A, wn*128 + 16 j + fr of W; chunk fq
+  const int foff = g9_off(fr, fq);                  // (rows of a fragment start at multiples of 16)
+  const char* fa_base = smem + (wm * 128) * 64 + foff;
+  const char* fw_base = smem + 16384 + (wn * 128) * 64 + foff;
+  auto rd = [&](const char* p) __attribute__((always_inline)) {
+    if constexpr ((DBG & 4) != 0) {
+      bf16x8 z;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) z[e] = (bf16)(float)(lane + e);
+      return z;
+    }
+    return *reinterpret_cast<const bf16x8*>(p);
+  };
+  bf16x8 fa[8], fw[2][8];                           // A: one set, refilled row by row; W: two sets
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- pipeline. At step t (register set b = t & 1 of W):
+  //   barrier: slot (t+1)&1 holds step t+1 (written at step t-1), every read of slot t&1 is done
+  //   W fragments of step t+1 -> set b^1 (all 8, from slot (t+1)&1)
+  //   MFMA row i of step t (8 MFMAs on A_i), then A_i <- step t+1's (its last use is behind it)
+  //   slot t&1 <- staged step t+2; staged <- global loads of step t+3 (a step of MFMAs to land)
+  // K % 64 == 0 (gemm9_ok): nk is even, the loop is unrolled by two and every set index static.
+  auto step = [&](int t, auto B, auto WRITE, auto LOAD) __attribute__((always_inline)) {
+    constexpr int b = decltype(B)::value;
+    const int nslot = ((t + 1) & 1) * G9_SLOT;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 8; ++j) fw[b ^ 1][j] = rd(fw_base + nslot + 16 * j * 64);
+    if constexpr (decltype(WRITE)::value) swrite(t & 1);
+    if constexpr (decltype(LOAD)::value) gload(t + 3);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr ((DBG & 1) == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[b][j], fa[i], acc[i][j], 0, 0, 0);
+      }
+      fa[i] = rd(fa_base + nslot + 16 * i * 64);
+    }
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  // prologue: steps 0, 1 -> slots 0, 1; step 2 staged; fragments of step 0
+  gload(0);
+  swrite(0);
+  gload(1);
+  swrite(1);
+  gload(2);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fw[0][j] = rd(fw_base + 16 * j * 64);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) fa[i] = rd(fa_base + 16 * i * 64);
+  int t = 0;
+  for (; t + 4 < nk; t += 2) {                      // every step that stages t+2 and loads t+3
+    step(t, I0{}, T_{}, T_{});
+    step(t + 1, I1{}, T_{}, T_{});
+  }
+  // last four steps (nk even, >= 4): t = nk-4 stages nk-2 and loads nk-1; nk-3 stages nk-1
+  step(t, I0{}, T_{}, T_{});
+  step(t + 1, I1{}, T_{}, F_{});
+  step(t + 2, I0{}, F_{}, F_{});
+  step(t + 3, I1{}, F_{}, F_{});
+
+  // ---- epilogue: lane holds channels c .. c+7 (c = n0 + 128 wn + 32 s + 8 fq) of pixel rows
+  // m0 + 128 wm + 16 i + fr (sub-tiles 2s, 2s+1 of the permuted weight rows) ----
+  bf16* o = reinterpret_cast<bf16*>(g.out);
+  const bf16* res = reinterpret_cast<const bf16*>(g.res);
+  const float* vs = g.ln_s ? g.ln_s : g.zeros;
+  const float* vt = g.ln_t ? g.ln_t : g.zeros;
+  const float* vb = g.bias ? g.bias : g.zeros;
+  const float* vc = g.scale ? g.scale : g.ones;
+  float mu[8], rs[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int64_t m = m0 + wm * 128 + 16 * i + fr;
+    if constexpr (LN) {
+      const uint2 q = ld8(stats + (m < mlim ? m : m0));
+      const float2 st = float2{__uint_as_float(q.x), __uint_as_float(q.y)};
+      mu[i] = st.x; rs[i] = st.y;
+    } else {
+      mu[i] = 0.f; rs[i] = 1.f;
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const int c = n0 + wn * 128 + 32 * s + 8 * fq;
+    if (c >= g.N) continue;                         // N % 8 == 0: a group of 8 is all in or all out
+    float fs[8], ft[8], fb[8], fc[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(vs + c + 4 * h), bb = *reinterpret_cast<const f32x4*>(vt + c + 4 * h);
+      const f32x4 d = *reinterpret_cast<const f32x4*>(vb + c + 4 * h), e = *reinterpret_cast<const f32x4*>(vc + c + 4 * h);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { fs[4 * h + q] = a[q]; ft[4 * h + q] = bb[q] + d[q]; fc[4 * h + q] = e[q]; }
+    }
+    (void)fb;
+    uint4 rv[8];
+    if (res) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int64_t m = m0 + wm * 128 + 16 * i + fr;
+        rv[i] = ld16(res + (m < mlim ? m : m0) * g.ldr + g.offr + c);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int64_t m = m0 + wm * 128 + 16 * i + fr;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = acc[i][2 * s + (e >> 2)][e & 3];
+        if constexpr (LN) x = rs[i] * (x - mu[i] * fs[e]);
+        x += ft[e];
+        if (g.gelu) x = gelu_bf16(x);
+        v[e] = x * fc[e];
+      }
+      if (res) {
+        const uint32_t rw[4] = {rv[i].x, rv[i].y, rv[i].z, rv[i].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += __uint_as_float(rw[e] << 16);
+          v[2 * e + 1] += __uint_as_float(rw[e] & 0xffff0000u);
+        }
+      }
+      bf16x8 ov;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ov[e] = (bf16)v[e];
+      if (m >= mlim) continue;
+      const int64_t dst = g.store_mode == STORE_CB16 ? ((((int64_t)(c >> 4) * g.cb_px + m) << 4) + (c & 15)) : m * g.ldo + g.offo + c;
+      if constexpr (!(DBG & 16)) *reinterpret_cast<bf16x8*>(o + dst) = ov;
+      else if (v[0] == 1.2345f) o[tid] = ov[0];
+    }
+  }
+}
+
+// Per-pixel LayerNorm statistics (mu, 1 / sqrt(var + 1e-5)) of a [M][ld] bf16 map's K channels at
+// offset `off` (turtle_t1_arch.py:94-99: biased variance about the mean, two passes in registers):
+// 8 lanes per pixel, K / 64 16-byte chunks each, an 8-lane DPP reduction.
+template <int K>
+__global__ __launch_bounds__(256) void ln_stats_kernel(const bf16* __restrict__ x, int64_t ld, int off, int64_t M, float2* __restrict__ out) {
+  constexpr int CPL = K / 64;
+  const int tid = threadIdx.x, cc = tid & 7;
+  const int64_t p = (int64_t)blockIdx.x * 32 + (tid >> 3);
+  const int64_t pc = p < M ? p : M - 1;
+  const bf16* src = x + pc * ld + off + cc * 8;
+  uint4 v[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) v[q] = ld16(src + q * 64);
+  auto sum8 = [](float s) __attribute__((always_inline)) {
+    s += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s), 0xB1, 0xf, 0xf, false));   // xor 1
+    s += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s), 0x4E, 0xf, 0xf, false));   // xor 2
+    s += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, s), 0x141, 0xf, 0xf, false));  // half mirror
+    return s;
+  };
+  float sm = 0.f;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    Vec<bf16> vv; vv.from_raw(v[q]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sm += vv.v[e];
+  }
+  const float mu = sum8(sm) * (1.f / K);
+  float sq = 0.f;
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    Vec<bf16> vv; vv.from_raw(v[q]);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = vv.v[e] - mu; sq = fmaf(d, d, sq); }
+  }
+  const float rstd = rsqrtf(sum8(sq) * (1.f / K) + 1e-5f);
+  if (cc == 0 && p < M) out[p] = float2{mu, rstd};
+}
+
+// Eligible: bf16, one LN source or K-concatenated plain sources (each a multiple of 32 wide, img_mul
+// 1 / img_add 0), K % 64 == 0 and 128 <= K <= 4096, NHWC or channel-blocked store, N % 8 == 0, 16-byte
+// aligned rows, no 3x3 / shuffle stores. LN needs K in {256, 512, 1024} (the statistics kernel).
+bool gemm9_ok(const GemmArgs& g) {
+  if (!g.allow_g9 || g.conv3 || g.a.cb_px || (g.store_mode != STORE_NHWC && g.store_mode != STORE_CB16)) return false;
+  if (g.store_mode == STORE_CB16 && (g.cb_px < g.M || g.N % 16 || g.wstride)) return false;
+  const int K = g.a.Ktot;
+  if (K % 64 || K < 128 || K > 4096 || g.N % 8 || g.ldo % 8 || g.offo % 8 || g.ldw % 8 || g.a.n < 1) return false;
+  if (g.ln && (g.a.n != 1 || (K != 256 && K != 512 && K != 1024))) return false;
+  if (g.res && (g.ldr % 8 || g.offr % 8 || reinterpret_cast<uintptr_t>(g.res) % 16)) return false;
+  if (reinterpret_cast<uintptr_t>(g.out) % 16 || reinterpret_cast<uintptr_t>(g.w) % 16) return false;
+  if (g.wstride && (g.HW <= 0 || g.M % g.HW || g.wstride % 8)) return false;
+  if (g.M > INT32_MAX) return false;
+  for (int j = 0; j < g.a.n; ++j) {
+    const SrcDesc& s = g.a.s[j];
+    if (s.img_mul != 1 || s.img_add != 0 || s.K % 32 || s.ld % 8 || s.off % 8 || reinterpret_cast<uintptr_t>(s.base) % 16) return false;
+  }
+  return true;
+}
+
+size_t gemm9_stats_bytes(const GemmArgs& g) { return g.ln ? (size_t)g.M * sizeof(float2) : 0; }
+
+// `stats`: workspace of gemm9_stats_bytes(g) (LN GEMMs), filled here before the GEMM
+void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st) {
+  const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + 255) / 256) : (g.M + 255) / 256;
+  const int64_t nblk = mt * ((g.N + 255) / 256);
+  float2* sp = reinterpret_cast<float2*>(stats);
+  if (g.ln) {
+    const SrcDesc& s = g.a.s[0];
+    const bf16* x = reinterpret_cast<const bf16*>(s.base);
+    const dim3 gs((unsigned)((g.M + 31) / 32));
+    if (g.a.Ktot == 256) hipLaunchKernelGGL((ln_stats_kernel<256>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
+    else if (g.a.Ktot == 512) hipLaunchKernelGGL((ln_stats_kernel<512>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
+    else hipLaunchKernelGGL((ln_stats_kernel<1024>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
+    hipLaunchKernelGGL((gemm9_kernel<true>), dim3((unsigned)nblk), dim3(256), 0, st, g, sp);
+  } else {
+    hipLaunchKernelGGL((gemm9_kernel<false>), dim3((unsigned)nblk), dim3(256), 0, st, g, sp);
+  }
+}
+
+#ifdef TURTLE_G9_ABLATIONS
+template <int DBG>
+static void g9_launch_dbg(const GemmArgs& g, void* stats, hipStream_t st) {
+  const int64_t nblk = ((g.M + 255) / 256) * ((g.N + 255) / 256);
+  if (g.ln) hipLaunchKernelGGL((gemm9_kernel<true, DBG>), dim3((unsigned)nblk), dim3(256), 0, st, g, reinterpret_cast<float2*>(stats));
+  else hipLaunchKernelGGL((gemm9_kernel<false, DBG>), dim3((unsigned)nblk), dim3(256), 0, st, g, reinterpret_cast<float2*>(stats));
+}
+void launch_gemm9_dbg(const GemmArgs& g, void* stats, int dbg, hipStream_t st) {
+  switch (dbg) {
+    case 1: g9_launch_dbg<1>(g, stats, st); break;
+    case 2: g9_launch_dbg<2>(g, stats, st); break;
+    case 4: g9_launch_dbg<4>(g, stats, st); break;
+    case 6: g9_launch_dbg<6>(g, stats, st); break;
+    case 16: g9_launch_dbg<16>(g, stats, st); break;
+    case 22: g9_launch_dbg<22>(g, stats, st); break;
+    default: g9_launch_dbg<0>(g, stats, st);
+  }
+}
+#endif
+
+}  // namespace turtle

@@ -42,6 +42,7 @@ struct GemmArgs {
   int64_t cb_px;                   // STORE_CB16: pixels per 16-channel block (= M)
   int allow_g8;                    // 256 x 256 four-phase kernel permitted (turtle_set_option "gemm8")
   int kt_max_px;                   // GEMMs over fewer pixels go to the 2-D tiled kernel (0: 32768)
+  int allow_g9;                    // 256 x 256 four-wave kernel permitted (turtle_set_option "gemm9")
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
 bool gemm_lds_ok(const GemmArgs& g);                              // gemm2.hip (bf16)
@@ -54,6 +55,9 @@ bool gemm_kt_ok(const GemmArgs& g);                               // gemm5.hip (
 void launch_gemm_kt(const GemmArgs& g, hipStream_t st);
 bool gemm8_ok(const GemmArgs& g);                                 // gemm8.hip (bf16)
 void launch_gemm8(const GemmArgs& g, hipStream_t st);
+bool gemm9_ok(const GemmArgs& g);                                 // gemm9.hip (bf16)
+size_t gemm9_stats_bytes(const GemmArgs& g);                      // LN statistics workspace
+void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st);
 
 enum DwMode { DW_PLAIN = 0, DW_GELU = 1, DW_GATE = 2 };
 struct DwArgs {

@@ -331,6 +331,8 @@ struct TurtleHandle {
   bool gemm8_ps = false;                              // ... in its persistent form (one block per CU walks its tiles)
   int gemm8 = 3;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 in place of
                                                       // hipBLASLt, 2 every eligible projection
+  int gemm9 = 0;                                      // four-wave 256 x 256 bf16 GEMM (gemm9.hip): 1 in place of
+                                                      // hipBLASLt, 2 on every eligible projection
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   int sab_db = 0;                                     // SAB A.v: 0 two blocks / CU; 1 double-buffered, one block / CU;
                                                       // 2 two blocks / CU with the tail rows fetched a chunk ahead
@@ -752,6 +754,9 @@ struct Runner {
     const bool ln_ws = ES == 2 && a.n == 1 && !conv3 && !gelu && store == STORE_NHWC && a.Ktot >= 512 &&
                        a.Ktot <= 64 * 8 * 4 && a.Ktot % 8 == 0 && M * a.Ktot <= ((int64_t)32 << 20);
     T* xn = ln_ws ? buf(M * a.Ktot) : nullptr;
+    // per-pixel LayerNorm statistics of the four-wave GEMM (gemm9.hip; shape-only, as above)
+    const bool g9_ws = ES == 2 && w.ln && a.n == 1 && !conv3 && (a.Ktot == 256 || a.Ktot == 512 || a.Ktot == 1024);
+    float* st9 = g9_ws ? fbuf(2 * M) : nullptr;
     const bool ln_cand = ln_ws && h->blaslt && w.ln && w.scale == NONE && a.s[0].img_mul == 1 &&
                          a.s[0].img_add == 0 && !wptr && !bias && w.tb != NONE;
     if (dry()) return;
@@ -796,10 +801,24 @@ struct Runner {
       if (gemm8_ok(g) && pick) lt = false;
       else g.allow_g8 = 0;
     }
-    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s%s%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
-        res != nullptr, store, a.n, a.cb_px ? " cb" : "", lt ? " lt" : "", g.allow_g8 ? " g8" : "");
+    // four-wave 256 x 256 GEMM: 1 in place of hipBLASLt, 2 every eligible bf16 projection
+    bool use9 = false;
+    if (ES == 2 && h->gemm9) {
+      GemmArgs t9 = g;
+      t9.allow_g9 = 1;
+      if ((h->gemm9 == 2 || lt) && gemm9_ok(t9) && (!g.ln || st9)) {
+        use9 = true;
+        lt = false;
+        g.allow_g8 = 0;
+        g.allow_g9 = 1;
+      }
+    }
+    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s%s%s%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
+        res != nullptr, store, a.n, a.cb_px ? " cb" : "", lt ? " lt" : "", g.allow_g8 ? " g8" : "", use9 ? " g9" : "");
     launch(TURTLE_K_GEMM, bytes + (ln_cand && lt ? 2.0 * ES * M * a.Ktot : 0.0), 2.0 * M * g.N * a.Ktot, [&] {
-      if (lt && ln_cand) {
+      if (use9) {
+        launch_gemm9(g, st9, st);
+      } else if (lt && ln_cand) {
         LnRowsArgs la{a.s[0].base, a.s[0].ld, a.s[0].off, xn, a.Ktot, M, a.Ktot, h->arch.cfg.layernorm_biasfree ? 0 : 1};
         launch_ln_rows<T>(la, st);
         run_blas(gl);
@@ -1633,6 +1652,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm_kt") h->gemm_kt = value != 0;
     else if (n == "gemm8") h->gemm8 = (int)value;
     else if (n == "gemm8_ps") h->gemm8_ps = value != 0;
+    else if (n == "gemm9") h->gemm9 = (int)value;
     else if (n == "attn_fin") h->attn_fin = value != 0;
     else if (n == "sab_waves") h->sab_waves = (int)value;
     else if (n == "blas_multi_img") h->blas_multi_img = (int)value;
