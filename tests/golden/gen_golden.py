@@ -257,7 +257,8 @@ def gen_train(t1):
     only = [a for a in sys.argv[1:] if a.startswith("train_")]
     for name, opt, shape, seed in [("train_tiny", tiny_opt(), (2, 4, 3, 64, 64), 21),
                                    ("train_tiny_hetero", tiny_opt(**HETERO), (1, 4, 3, 64, 64), 22),
-                                   ("train_gopro", gopro_opt(), (1, 2, 3, 64, 64), 23)]:
+                                   ("train_gopro", gopro_opt(), (1, 2, 3, 64, 64), 23),
+                                   ("train_gopro_amp", gopro_opt(), (1, 2, 3, 64, 64), 23)]:
         if only and name not in only:
             continue
         torch.manual_seed(0)
@@ -267,10 +268,16 @@ def gen_train(t1):
         gt = torch.from_numpy(synthetic_frames(shape, seed, name="gt"))
         kc = vc = None
         loss = 0
-        for j in range(shape[1]):
-            inp = torch.cat([lq[:, j if j == 0 else j - 1].unsqueeze(1), lq[:, j].unsqueeze(1)], dim=1)
-            out, kc, vc = model(inp, kc, vc)
-            loss = loss + torch.nn.functional.l1_loss(out, gt[:, j])
+        # train_gopro_amp: the reference's mixed precision (feed_data :73-76 lq.half(); optimize_parameters
+        # :80 autocast) - CPU autocast with float16, the reference's CUDA autocast being absent here
+        amp = name.endswith("_amp")
+        if amp:
+            lq = lq.half()
+        with torch.autocast("cpu", dtype=torch.float16, enabled=amp):
+            for j in range(shape[1]):
+                inp = torch.cat([lq[:, j if j == 0 else j - 1].unsqueeze(1), lq[:, j].unsqueeze(1)], dim=1)
+                out, kc, vc = model(inp, kc, vc)
+                loss = loss + torch.nn.functional.l1_loss(out, gt[:, j])
         loss = loss / shape[1]
         total = loss + 0 * sum(p.sum() for p in model.parameters())
         total.backward()
@@ -282,7 +289,8 @@ def gen_train(t1):
                 rec[f"g_{k}__{sk}"] = sv
             if k in full:
                 rec[f"g_{k}"] = g.numpy().astype(np.float32)
-        save(name, rec, dict(opt=arch_opt(opt), seed=seed, shape=list(shape), n_params=len(list(model.parameters()))))
+        save(name, rec, dict(opt=arch_opt(opt), seed=seed, shape=list(shape), n_params=len(list(model.parameters())),
+                             amp="fp16 (cpu autocast)" if amp else None))
 
 
 def gen_keys(t1, sr):

@@ -402,8 +402,9 @@ def test_dropin_module_reference_loop_gpu_fp32_and_fp16():
 def test_config5_bf16_step_8x5x256_through_trainer():
     """SURVEY §8 config 5 as specified: the GoPro network, B = 8 clips x 5 frames of 256x256 per GPU,
     one bf16-autocast step through Trainer (video_restoration_model.py:78-108). Loss and every
-    gradient finite; the first-step loss equals the same graph on the ATen op set (torch ops, same
-    device, same bf16 autocast) to bf16 tolerance; AdamW moves the weights."""
+    gradient finite; the first-step loss and the gradient norms (whole and per parameter) equal the
+    same graph on the ATen op set (torch ops, same device, same bf16 autocast) to bf16 tolerance;
+    AdamW moves the weights."""
     import yaml
     with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "options",
                            "Turtle_Deblur_Gopro.yml")) as f:
@@ -411,9 +412,11 @@ def test_config5_bf16_step_8x5x256_through_trainer():
     lq = torch.from_numpy(synthetic_frames((8, 5, 3, 256, 256), 51, name="lq")).cuda()
     gt = (lq + 0.05 * torch.from_numpy(synthetic_frames((8, 5, 3, 256, 256), 52, name="gt")).cuda()).clamp(0, 1)
     ref_net = _net(dict(opt=opt, seed=5), AtenOps, "cuda")
-    with torch.no_grad():
-        l_aten = float(Trainer(ref_net, amp="bf16").loss(lq, gt))
-    del ref_net
+    l_ref = Trainer(ref_net, amp="bf16").loss(lq, gt)
+    (l_ref + 0 * sum(p.sum() for p in ref_net.parameters())).backward()
+    l_aten = float(l_ref.detach())
+    ref_norms = {k: float(p.grad.float().norm()) for k, p in ref_net.named_parameters()}
+    del ref_net, l_ref
     net = _net(dict(opt=opt, seed=5), None, "cuda")
     tr = Trainer(net, amp="bf16", lr=1e-4)
     before = {k: p.detach().clone() for k, p in net.named_parameters()}
@@ -423,6 +426,13 @@ def test_config5_bf16_step_8x5x256_through_trainer():
     l_hip = float(loss.detach())
     assert np.isfinite(l_hip) and l_hip == pytest.approx(l_aten, rel=2e-2), (l_hip, l_aten)
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in net.parameters())
+    # the gradients, not only the loss - the whole-gradient norm within 5 % of the ATen
+    # graph's and the per-parameter norms within 10 % relative L2 (bf16 over 5 frames of BPTT)
+    hn = np.array([float(p.grad.float().norm()) for _, p in net.named_parameters()])
+    rn = np.array([ref_norms[k] for k, _ in net.named_parameters()])
+    ratio = float(np.linalg.norm(hn) / np.linalg.norm(rn))
+    nrel = float(np.linalg.norm(hn - rn) / np.linalg.norm(rn))
+    assert abs(ratio - 1) <= 0.05 and nrel <= 0.10, (ratio, nrel)
     tr.opt.step()
     moved = sum(int(not torch.equal(before[k], p.detach())) for k, p in net.named_parameters())
     assert moved > 0.9 * len(before)
@@ -462,6 +472,59 @@ def test_fp16_autocast_matches_aten_same_autocast():
         if err > 0.1:
             bad.append((k, err))
     assert not bad, bad[:10]
+
+
+def _sampled_grad_stats(net, g):
+    """(relative L2 over the fixture's sampled gradient entries, relative L2 of the vector of
+    per-parameter gradient norms) of `net`'s gradients against a golden training record."""
+    num = den = 0.0
+    norms, rnorms = [], []
+    for k, p in net.named_parameters():
+        grad = (p.grad if p.grad is not None else torch.zeros_like(p)).detach().double().reshape(-1).cpu()
+        samp = grad[torch.from_numpy(g[f"g_{k}__idx"])].numpy()
+        ref = g[f"g_{k}__samp"].astype(np.float64)
+        num += float(((samp - ref) ** 2).sum())
+        den += float((ref ** 2).sum())
+        norms.append(float(grad.norm()))
+        rnorms.append(float(np.sqrt(g[f"g_{k}__sqsum"])))
+    norms, rnorms = np.array(norms), np.array(rnorms)
+    return (num / den) ** 0.5, float(np.linalg.norm(norms - rnorms) / np.linalg.norm(rnorms))
+
+
+@pytest.mark.gpu
+def test_fp16_autocast_gradients_match_reference_amp():
+    """config-5 numerics pinned to the REFERENCE under its own mixed precision, not to
+    our restatement. tests/golden/train_gopro_amp: the reference Turtle_t1 (GoPro widths, 2 x 64x64
+    frames, BPTT through the caches) run by gen_golden.py under fp16 autocast on lq.half()
+    (video_restoration_model.py:73-80; CPU autocast - the reference's CUDA autocast is absent in the
+    build container). The HIP training graph under the reference's fp16 autocast (Trainer amp
+    "fp16": the 1x1 GEMMs / Gram in bf16) gives:
+      * the loss within 0.2 % relative;
+      * gradients within 6 % relative L2 over the fixture's 40,512 sampled entries (64 per
+        parameter) and the per-parameter gradient norms within 8 % relative L2 - the reference's
+        own fp16-vs-fp32 gap on the same clip is 1.0 % / 2.9 % (train_gopro_amp vs train_gopro);
+      * the same statistics against the fp32 fixture within the same bounds."""
+    g, meta = load("train_gopro_amp")
+    gf, _ = load("train_gopro")
+    net = _net(meta, None, "cuda")
+    tr = Trainer(net, amp="fp16")
+    lq, gt = _data(meta, "cuda")
+    scale = 1024.0                                   # GradScaler's role: fp16 gradients must not underflow
+    loss = tr.loss(lq.half(), gt)
+    ((loss + 0 * sum(p.sum() for p in net.parameters())) * scale).backward()
+    torch.cuda.synchronize()
+    for p in net.parameters():
+        if p.grad is not None:
+            p.grad.div_(scale)
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in net.parameters())
+    l = float(loss.detach())
+    assert l == pytest.approx(float(g["loss"]), rel=2e-3), (l, float(g["loss"]))
+    rel, nrel = _sampled_grad_stats(net, g)
+    assert rel <= 0.06 and nrel <= 0.08, (rel, nrel)
+    rel32, nrel32 = _sampled_grad_stats(net, gf)
+    assert rel32 <= 0.06 and nrel32 <= 0.08, (rel32, nrel32)
+    print(f"amp fixture: loss {l:.6f} vs {float(g['loss']):.6f}, sampled rel-L2 {rel:.4f}, norm rel-L2 {nrel:.4f}; "
+          f"vs fp32 fixture {rel32:.4f} / {nrel32:.4f}")
 
 
 def _ddp_worker_gpu(rank, world, port, meta, q):

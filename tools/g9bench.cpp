@@ -1,4 +1,4 @@
-// Microbenchmark of the four-wave 256 x 256 GEMM (gemm9.hip) against the 2-D tiled kernel
+// Microbenchmark of the 256-pixel-row GEMM (gemm9.hip, BN = 128 and 256 channel tilings) against the 2-D tiled kernel
 // (gemm5.hip, the parity reference here) and hipBLASLt on the Turtle projection shapes (GPU box).
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTURTLE_G9_ABLATIONS -I turtlevsr_amd/csrc \
 //         tools/g9bench.cpp turtlevsr_amd/csrc/gemm9.hip -L turtlevsr_amd/lib -lturtle_hip \
@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
   int bad = 0;
   if (abl) printf("ablations (us): d0 full, d1 no MFMA, d2 no global loads, d4 no LDS, d6 no loads+LDS, d16 no stores, d22\n");
   else
-    printf("%-26s %8s %5s %5s | %8s %7s %6s | %8s %7s | %8s %7s | %9s %s\n", "shape", "M", "N", "K", "g9 us", "TF/s", "GB/s", "kt us",
+    printf("%-26s %8s %5s %5s | %8s %7s %6s | %8s | %8s %7s | %8s %7s | %9s %s\n", "shape", "M", "N", "K", "g9 us", "TF/s", "GB/s", "g9w us", "kt us",
            "TF/s", "blas us", "TF/s", "max|d|", "race");
   for (auto& s : shapes) {
     GemmArgs g{};
@@ -119,15 +119,17 @@ int main(int argc, char** argv) {
     const size_t n = (size_t)s.M * s.N;
     GemmArgs gk = g; gk.allow_kt = 1; gk.dbg = 0x10; gk.out = Okt;
     GemmArgs g9 = g; g9.allow_g9 = 1; g9.out = Og9;
+    GemmArgs g9w = g9; g9w.allow_g9 = 2; g9w.out = Og9b;   // the BN = 256 tiling
     if (!gemm9_ok(g9)) { printf("%-26s not eligible\n", s.tag); continue; }
     if (abl) {
       if (s.hw || s.M < 30000) continue;
       printf("%-26s", s.tag);
-      for (int dbg : {0, 1, 2, 4, 6, 16, 22}) {
-        launch_gemm9_dbg(g9, ST, dbg, 0);
+      for (int dbg : {0, 1, 2, 4, 6, 16, 22, 100, 116}) {   // 100+: the BN = 256 tiling
+        const GemmArgs& ga = dbg >= 100 ? g9w : g9;
+        launch_gemm9_dbg(ga, ST, dbg % 100, 0);
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(e0, 0));
-        for (int i = 0; i < reps; ++i) launch_gemm9_dbg(g9, ST, dbg, 0);
+        for (int i = 0; i < reps; ++i) launch_gemm9_dbg(ga, ST, dbg % 100, 0);
         CK(hipEventRecord(e1, 0));
         CK(hipEventSynchronize(e1));
         float ms;
@@ -142,11 +144,12 @@ int main(int argc, char** argv) {
     const bool bl_ok = blas && s.nsrc == 1 && !s.gelu && !s.hw &&
                        blas_ready(blas, s.M, s.N, s.K, s.K, s.K, s.res ? s.N : 0, s.N, s.res != 0, true);
     LnRowsArgs la{A, s.K, 0, XN, s.K, s.M, s.K, 1};
-    double us[3] = {0, 0, 0};
-    for (int v = 0; v < 3; ++v) {
+    double us[4] = {0, 0, 0, 0};
+    for (int v = 0; v < 4; ++v) {
       if ((v == 1 && !kt_ok) || (v == 2 && !bl_ok)) continue;
       auto run = [&] {
         if (v == 0) launch_gemm9(g9, ST, 0);
+        else if (v == 3) launch_gemm9(g9w, ST, 0);
         else if (v == 1) launch_gemm_kt(gk, 0);
         else {
           if (s.ln) launch_ln_rows<bf16>(la, 0);
@@ -168,7 +171,7 @@ int main(int argc, char** argv) {
     GemmArgs g9b = g9; g9b.out = Og9b;
     for (int it = 0; it < 8; ++it) {
       CK(hipMemset(Og9b, 0xff, n * 2));
-      launch_gemm9(g9b, ST, 0);
+      launch_gemm9(it & 1 ? g9w : g9b, ST, 0);       // both tilings: same arithmetic per output
       CK(hipMemcpy(r2.data(), Og9b, n * 2, hipMemcpyDeviceToHost));
       if (memcmp(r1.data(), r2.data(), n * 2)) ++races;
     }
@@ -182,8 +185,8 @@ int main(int argc, char** argv) {
       }
     }
     const double fl = 2.0 * s.M * s.N * s.K, by = 2.0 * ((double)s.M * s.K + (double)s.N * s.K + (double)s.M * s.N * (s.res ? 2 : 1));
-    printf("%-26s %8lld %5d %5d | %8.1f %7.0f %6.0f | %8.1f %7.0f | %8.1f %7.0f | %9.4g %d/8\n", s.tag, (long long)s.M, s.N, s.K, us[0],
-           fl / us[0] / 1e6, by / us[0] / 1e3, us[1], us[1] > 0 ? fl / us[1] / 1e6 : 0.0, us[2], us[2] > 0 ? fl / us[2] / 1e6 : 0.0, md, races);
+    printf("%-26s %8lld %5d %5d | %8.1f %7.0f %6.0f | %8.1f | %8.1f %7.0f | %8.1f %7.0f | %9.4g %d/8\n", s.tag, (long long)s.M, s.N, s.K, us[0],
+           fl / us[0] / 1e6, by / us[0] / 1e3, us[3], us[1], us[1] > 0 ? fl / us[1] / 1e6 : 0.0, us[2], us[2] > 0 ? fl / us[2] / 1e6 : 0.0, md, races);
     fflush(stdout);
     if (races || md > 0.07 || md < 0) ++bad;
   }

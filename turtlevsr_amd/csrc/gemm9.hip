@@ -1,7 +1,9 @@
-// bf16 projection GEMM with 256 x 256 output tiles on FOUR waves ("g9" kernel): each wave owns a
-// 128-pixel x 128-channel quadrant, i.e. 64 accumulator tiles of 16 x 16 (256 of the SIMD's 512
-// registers, in the accumulation file), so every fragment read from LDS feeds 8 MFMAs and one
-// barrier covers 64 MFMAs (1,024 matrix-pipe cycles) of every SIMD.
+// bf16 projection GEMM with 256 x 256 output tiles, eight waves at two per SIMD ("g9" kernel):
+// each wave owns 128 pixels x 64 channels (32 accumulator tiles of 16 x 16, 128 registers in the
+// accumulation file), so the two waves of a SIMD fill each other's memory-issue gaps in the matrix
+// pipe, and one barrier covers 64 MFMAs (1,024 matrix-pipe cycles) of every SIMD.
+// (A four-wave 128 x 128-per-wave form - hipBLASLt's tiling - needs all 512 registers of the SIMD;
+// hipcc's allocation of it spilled and shuffled the accumulators.)
 //
 //   out[m][n] = epilogue( sum_k A[m][k] * W[n][k] )        m = pixel, n = output channel
 //
@@ -9,11 +11,11 @@
 // (latent level: LN project_in 512 -> 2560, LN qkv 512 -> 1536, project_out 1280 -> 512, W_eff
 // 512 -> 512 per image; level 3: W_eff 256 -> 256 per image) - turtle_t1_arch.py:159-178, 666-702.
 //
-// Structure (MI355X, one 256-thread block per CU at 1 wave per SIMD):
+// Structure (MI355X, one 512-thread block per CU):
 //   * K steps of 32. The block stages a step's A (256 pixel rows x 64 B) and W (256 channel rows x
-//     64 B) tiles through registers: each thread issues 8 global_load_dwordx4 four steps before the
-//     step's MFMAs and writes them to one of two 32 KB LDS slots two steps later (ds_write_b128), so
-//     the global loads have two steps of MFMAs (~2,000 cycles) to land; nothing is asm: hipcc counts
+//     64 B) tiles through registers: each thread issues 4 global_load_dwordx4 three steps before the
+//     step's MFMAs and writes them to one of two 32 KB LDS slots a step later (ds_write_b128), so
+//     the global loads have a step of MFMAs (~1,000 cycles) to land; nothing is asm: hipcc counts
 //     every vmcnt / lgkmcnt itself (no hand-counted waits);
 //   * per step: one barrier, then the next step's 16 fragments are read from the other slot while
 //     the 64 MFMAs of this step run (fragment registers double-buffered);
@@ -38,8 +40,9 @@ namespace turtle {
 namespace {
 
 constexpr int G9_BK = 32;
-constexpr int G9_SLOT = 32768;                 // A 16 KB + W 16 KB
-constexpr int G9_LDS = 2 * G9_SLOT;
+#ifndef G9_SCHED
+#define G9_SCHED 1              // interleave the step's memory operations with its MFMAs (sched groups)
+#endif
 
 // MFMA row -> channel inside a 32-channel group (see header)
 TURTLE_DEV int g9_perm(int r) { return (r & ~31) | (8 * ((r >> 2) & 3) + 4 * ((r >> 4) & 1) + (r & 3)); }
@@ -48,18 +51,25 @@ TURTLE_DEV int g9_off(int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 2)) << 4
 
 }  // namespace
 
-// DBG (tools/g8bench ablations only; 0 in the library): 1 no MFMA, 2 no global loads in the loop,
+// DBG (tools/g9bench ablations only; 0 in the library): 1 no MFMA, 2 no global loads in the loop,
 // 4 no LDS traffic in the loop, 16 no epilogue stores
-template <bool LN, int DBG = 0>
-__global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs g, const float2* __restrict__ stats) {
-  __shared__ __attribute__((aligned(16))) char smem[G9_LDS];
+// MS: K-concatenated multi-source operand (per-step source selection); single source otherwise
+// BN: channels per block tile (256: 8 waves, one block per CU; 128: 4 waves, two blocks per CU, so
+// one block's epilogue stores overlap the other's main loop)
+template <bool LN, bool MS, int BN, int DBG = 0>
+__global__ __launch_bounds__(BN * 2, 2) void gemm9_kernel(GemmArgs g, const float2* __restrict__ stats) {
+  constexpr int NT = BN * 2;                        // threads: 2 pixel halves x BN / 64 channel groups of waves
+  constexpr int WOFF = 16384;                       // W tile offset in a slot (A: 256 rows x 64 B)
+  constexpr int SLOT = WOFF + BN * 64;
+  constexpr int NA = 1024 / NT, NW = BN * 4 / NT;   // staged 16-byte chunks per thread and step
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wid >> 1, wn = wid & 1;
+  const int wm = wid & 1, wn = wid >> 1;            // pixel half (128 rows), channel group (64)
   const int fr = lane & 15, fq = lane >> 4;
 
   // ---- tile: the channel tiles of one pixel panel are consecutive ids on one XCD ----
-  const int ntn = (g.N + 255) / 256;
+  const int ntn = (g.N + BN - 1) / BN;
   int lin = blockIdx.x;
   {
     const int nblk = gridDim.x, q = nblk / 8, r = nblk % 8, x = lin % 8, y = lin / 8;
@@ -76,36 +86,34 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs g, const float2*
     m0 = (int64_t)mt * 256;
     mlim = g.M;
   }
-  const int n0 = nt * 256;
+  const int n0 = nt * BN;
   const int K = g.a.Ktot, nk = K / G9_BK;
   const bf16* Wp = reinterpret_cast<const bf16*>(g.w) + (g.wstride ? (int64_t)(m0 / g.HW / g.wdiv) * g.wstride : 0);
 
-  // ---- staging geometry: thread loads chunk c = tid & 3 of rows tid / 4 + 64 i (i = 0..3) of both tiles ----
+  // ---- staging geometry: thread loads chunk c = tid & 3 of A rows tid / 4 + (NT / 4) i (i < NA)
+  // and W rows tid / 4 + (NT / 4) i (i < NW) ----
   const int sc = tid & 3, sr0 = tid >> 2;
-  int64_t xrow[4];                                  // clamped pixel rows
-  const bf16* wrow[4];                              // weight rows (permuted, clamped)
-  int soff[4];                                      // swizzled LDS offsets (same for A and W rows)
+  int64_t xrow[NA];                                 // clamped pixel rows
+  const bf16* xp0[NA];                              // single source: row pointers
+  int soff[NA];                                     // swizzled LDS offsets
+  const bf16* wrow[NW];                             // weight rows (permuted, clamped)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = sr0 + 64 * i;
+  for (int i = 0; i < NA; ++i) {
+    const int r = sr0 + (NT / 4) * i;
     const int64_t m = m0 + r;
     xrow[i] = m < mlim ? m : m0;
-    wrow[i] = Wp + (int64_t)min(n0 + g9_perm(r), g.N - 1) * g.ldw + sc * 8;
+    xp0[i] = reinterpret_cast<const bf16*>(g.a.s[0].base) + g.a.s[0].off + sc * 8 + (MS ? 0 : xrow[i] * g.a.s[0].ld);
     soff[i] = g9_off(r, sc);
   }
-  uint4 ga[4], gw[4];                               // one staged K step
-  // single-source operand (every LN GEMM and most plain ones): row byte offsets computed once
-  const bool one_src = g.a.n == 1;
-  const bf16* xbase0 = reinterpret_cast<const bf16*>(g.a.s[0].base) + g.a.s[0].off + sc * 8;
-  int64_t xoff0[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) xoff0[i] = xrow[i] * g.a.s[0].ld;
+  for (int i = 0; i < NW; ++i) wrow[i] = Wp + (int64_t)min(n0 + g9_perm(sr0 + (NT / 4) * i), g.N - 1) * g.ldw + sc * 8;
+  uint4 ga[NA], gw[NW];                             // one staged K step
   auto gload = [&](int t) __attribute__((always_inline)) {
     if constexpr ((DBG & 2) != 0) return;
     const int k0 = t * G9_BK;
-    if (one_src) {
+    if constexpr (!MS) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ga[i] = ld16(xbase0 + xoff0[i] + k0);
+      for (int i = 0; i < NA; ++i) ga[i] = ld16(xp0[i] + k0);
     } else {
       // the K step's source (steps never straddle two: every source is a multiple of 32 wide)
       const bf16* base = reinterpret_cast<const bf16*>(g.a.s[0].base);
@@ -122,23 +130,23 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs g, const float2*
       }
       const bf16* b2 = base + soffs + (k0 - kb) + sc * 8;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ga[i] = ld16(b2 + xrow[i] * sld);
+      for (int i = 0; i < NA; ++i) ga[i] = ld16(b2 + xrow[i] * sld);
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) gw[i] = ld16(wrow[i] + k0);
+    for (int i = 0; i < NW; ++i) gw[i] = ld16(wrow[i] + k0);
   };
   auto swrite = [&](int slot) __attribute__((always_inline)) {
     if constexpr ((DBG & 4) != 0) return;
-    char* sb = smem + slot * G9_SLOT;
+    char* sb = smem + slot * SLOT;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(sb + soff[i]) = ga[i];
+    for (int i = 0; i < NA; ++i) *reinterpret_cast<uint4*>(sb + soff[i]) = ga[i];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(sb + 16384 + soff[i]) = gw[i];
+    for (int i = 0; i < NW; ++i) *reinterpret_cast<uint4*>(sb + WOFF + soff[i]) = gw[i];
   };
-  // fragment reads: rows wm*128 + 16 i + fr of A, wn*128 + 16 j + fr of W; chunk fq
+  // fragment reads: rows wm*128 + 16 i + fr of A, wn*64 + 16 j + fr of W; chunk fq
   const int foff = g9_off(fr, fq);                  // (rows of a fragment start at multiples of 16)
   const char* fa_base = smem + (wm * 128) * 64 + foff;
-  const char* fw_base = smem + 16384 + (wn * 128) * 64 + foff;
+  const char* fw_base = smem + WOFF + (wn * 64) * 64 + foff;
   auto rd = [&](const char* p) __attribute__((always_inline)) {
     if constexpr ((DBG & 4) != 0) {
       bf16x8 z;
@@ -148,35 +156,51 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs g, const float2*
     }
     return *reinterpret_cast<const bf16x8*>(p);
   };
-  bf16x8 fa[8], fw[2][8];                           // A: one set, refilled row by row; W: two sets
+  bf16x8 fa[8], fw[2][4];                           // A: one set, refilled row by row; W: two sets
 
-  f32x4 acc[8][8];
+  f32x4 acc[8][4];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // ---- pipeline. At step t (register set b = t & 1 of W):
+  // ---- pipeline. At step t (W register set b = t & 1):
   //   barrier: slot (t+1)&1 holds step t+1 (written at step t-1), every read of slot t&1 is done
-  //   W fragments of step t+1 -> set b^1 (all 8, from slot (t+1)&1)
-  //   MFMA row i of step t (8 MFMAs on A_i), then A_i <- step t+1's (its last use is behind it)
+  //   W fragments of step t+1 -> set b^1 (from slot (t+1)&1)
+  //   MFMA row i of step t (4 MFMAs on A_i), then A_i <- step t+1's (its last use is behind it)
   //   slot t&1 <- staged step t+2; staged <- global loads of step t+3 (a step of MFMAs to land)
   // K % 64 == 0 (gemm9_ok): nk is even, the loop is unrolled by two and every set index static.
   auto step = [&](int t, auto B, auto WRITE, auto LOAD) __attribute__((always_inline)) {
     constexpr int b = decltype(B)::value;
-    const int nslot = ((t + 1) & 1) * G9_SLOT;
+    const int nslot = ((t + 1) & 1) * SLOT;
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 8; ++j) fw[b ^ 1][j] = rd(fw_base + nslot + 16 * j * 64);
+    for (int j = 0; j < 4; ++j) fw[b ^ 1][j] = rd(fw_base + nslot + 16 * j * 64);
     if constexpr (decltype(WRITE)::value) swrite(t & 1);
     if constexpr (decltype(LOAD)::value) gload(t + 3);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       if constexpr ((DBG & 1) == 0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[b][j], fa[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[b][j], fa[i], acc[i][j], 0, 0, 0);
       }
       fa[i] = rd(fa_base + nslot + 16 * i * 64);
+    }
+    // issue order: the memory operations one per MFMA gap - the next W fragments, the LDS writes,
+    // the global loads - then the next A fragments each behind the last MFMA of its row
+    if constexpr (G9_SCHED && (DBG & 7) == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); }
+      if constexpr (decltype(WRITE)::value) {
+#pragma unroll
+        for (int k = 0; k < NA + NW; ++k) { __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); __builtin_amdgcn_sched_group_barrier(0x200, 1, 0); }
+      }
+      if constexpr (decltype(LOAD)::value) {
+#pragma unroll
+        for (int k = 0; k < NA + NW; ++k) { __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); __builtin_amdgcn_sched_group_barrier(0x020, 1, 0); }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { __builtin_amdgcn_sched_group_barrier(0x008, 2, 0); __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); }
     }
   };
   using I0 = std::integral_constant<int, 0>;
@@ -191,7 +215,7 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs g, const float2*
   gload(2);
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < 8; ++j) fw[0][j] = rd(fw_base + 16 * j * 64);
+  for (int j = 0; j < 4; ++j) fw[0][j] = rd(fw_base + 16 * j * 64);
 #pragma unroll
   for (int i = 0; i < 8; ++i) fa[i] = rd(fa_base + 16 * i * 64);
   int t = 0;
@@ -205,7 +229,7 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs g, const float2*
   step(t + 2, I0{}, F_{}, F_{});
   step(t + 3, I1{}, F_{}, F_{});
 
-  // ---- epilogue: lane holds channels c .. c+7 (c = n0 + 128 wn + 32 s + 8 fq) of pixel rows
+  // ---- epilogue: lane holds channels c .. c+7 (c = n0 + 64 wn + 32 s + 8 fq) of pixel rows
   // m0 + 128 wm + 16 i + fr (sub-tiles 2s, 2s+1 of the permuted weight rows) ----
   bf16* o = reinterpret_cast<bf16*>(g.out);
   const bf16* res = reinterpret_cast<const bf16*>(g.res);
@@ -219,17 +243,16 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs g, const float2*
     const int64_t m = m0 + wm * 128 + 16 * i + fr;
     if constexpr (LN) {
       const uint2 q = ld8(stats + (m < mlim ? m : m0));
-      const float2 st = float2{__uint_as_float(q.x), __uint_as_float(q.y)};
-      mu[i] = st.x; rs[i] = st.y;
+      mu[i] = __uint_as_float(q.x); rs[i] = __uint_as_float(q.y);
     } else {
       mu[i] = 0.f; rs[i] = 1.f;
     }
   }
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int c = n0 + wn * 128 + 32 * s + 8 * fq;
+  for (int s = 0; s < 2; ++s) {
+    const int c = n0 + wn * 64 + 32 * s + 8 * fq;   // (N % 8 == 0)
     if (c >= g.N) continue;                         // N % 8 == 0: a group of 8 is all in or all out
-    float fs[8], ft[8], fb[8], fc[8];
+    float fs[8], ft[8], fc[8];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const f32x4 a = *reinterpret_cast<const f32x4*>(vs + c + 4 * h), bb = *reinterpret_cast<const f32x4*>(vt + c + 4 * h);
@@ -237,7 +260,6 @@ __global__ __launch_bounds__(256, 1) void gemm9_kernel(GemmArgs g, const float2*
 #pragma unroll
       for (int q = 0; q < 4; ++q) { fs[4 * h + q] = a[q]; ft[4 * h + q] = bb[q] + d[q]; fc[4 * h + q] = e[q]; }
     }
-    (void)fb;
     uint4 rv[8];
     if (res) {
 #pragma unroll
@@ -338,9 +360,15 @@ bool gemm9_ok(const GemmArgs& g) {
 size_t gemm9_stats_bytes(const GemmArgs& g) { return g.ln ? (size_t)g.M * sizeof(float2) : 0; }
 
 // `stats`: workspace of gemm9_stats_bytes(g) (LN GEMMs), filled here before the GEMM
-void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st) {
+template <int BN>
+static void g9_launch(const GemmArgs& g, float2* sp, hipStream_t st) {
   const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + 255) / 256) : (g.M + 255) / 256;
-  const int64_t nblk = mt * ((g.N + 255) / 256);
+  const dim3 grid((unsigned)(mt * ((g.N + BN - 1) / BN))), blk(2 * BN);
+  if (g.ln) hipLaunchKernelGGL((gemm9_kernel<true, false, BN>), grid, blk, 0, st, g, sp);
+  else if (g.a.n > 1) hipLaunchKernelGGL((gemm9_kernel<false, true, BN>), grid, blk, 0, st, g, sp);
+  else hipLaunchKernelGGL((gemm9_kernel<false, false, BN>), grid, blk, 0, st, g, sp);
+}
+void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st) {
   float2* sp = reinterpret_cast<float2*>(stats);
   if (g.ln) {
     const SrcDesc& s = g.a.s[0];
@@ -349,28 +377,34 @@ void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st) {
     if (g.a.Ktot == 256) hipLaunchKernelGGL((ln_stats_kernel<256>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
     else if (g.a.Ktot == 512) hipLaunchKernelGGL((ln_stats_kernel<512>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
     else hipLaunchKernelGGL((ln_stats_kernel<1024>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
-    hipLaunchKernelGGL((gemm9_kernel<true>), dim3((unsigned)nblk), dim3(256), 0, st, g, sp);
-  } else {
-    hipLaunchKernelGGL((gemm9_kernel<false>), dim3((unsigned)nblk), dim3(256), 0, st, g, sp);
   }
+  if (g.allow_g9 == 2) g9_launch<256>(g, sp, st);
+  else g9_launch<128>(g, sp, st);
 }
 
 #ifdef TURTLE_G9_ABLATIONS
-template <int DBG>
+template <int DBG, int BN>
 static void g9_launch_dbg(const GemmArgs& g, void* stats, hipStream_t st) {
-  const int64_t nblk = ((g.M + 255) / 256) * ((g.N + 255) / 256);
-  if (g.ln) hipLaunchKernelGGL((gemm9_kernel<true, DBG>), dim3((unsigned)nblk), dim3(256), 0, st, g, reinterpret_cast<float2*>(stats));
-  else hipLaunchKernelGGL((gemm9_kernel<false, DBG>), dim3((unsigned)nblk), dim3(256), 0, st, g, reinterpret_cast<float2*>(stats));
+  const dim3 grid((unsigned)(((g.M + 255) / 256) * ((g.N + BN - 1) / BN))), blk(2 * BN);
+  float2* sp = reinterpret_cast<float2*>(stats);
+  if (g.ln) hipLaunchKernelGGL((gemm9_kernel<true, false, BN, DBG>), grid, blk, 0, st, g, sp);
+  else if (g.a.n > 1) hipLaunchKernelGGL((gemm9_kernel<false, true, BN, DBG>), grid, blk, 0, st, g, sp);
+  else hipLaunchKernelGGL((gemm9_kernel<false, false, BN, DBG>), grid, blk, 0, st, g, sp);
+}
+template <int DBG>
+static void g9_dbg2(const GemmArgs& g, void* stats, hipStream_t st) {
+  if (g.allow_g9 == 2) g9_launch_dbg<DBG, 256>(g, stats, st);
+  else g9_launch_dbg<DBG, 128>(g, stats, st);
 }
 void launch_gemm9_dbg(const GemmArgs& g, void* stats, int dbg, hipStream_t st) {
   switch (dbg) {
-    case 1: g9_launch_dbg<1>(g, stats, st); break;
-    case 2: g9_launch_dbg<2>(g, stats, st); break;
-    case 4: g9_launch_dbg<4>(g, stats, st); break;
-    case 6: g9_launch_dbg<6>(g, stats, st); break;
-    case 16: g9_launch_dbg<16>(g, stats, st); break;
-    case 22: g9_launch_dbg<22>(g, stats, st); break;
-    default: g9_launch_dbg<0>(g, stats, st);
+    case 1: g9_dbg2<1>(g, stats, st); break;
+    case 2: g9_dbg2<2>(g, stats, st); break;
+    case 4: g9_dbg2<4>(g, stats, st); break;
+    case 6: g9_dbg2<6>(g, stats, st); break;
+    case 16: g9_dbg2<16>(g, stats, st); break;
+    case 22: g9_dbg2<22>(g, stats, st); break;
+    default: g9_dbg2<0>(g, stats, st);
   }
 }
 #endif
