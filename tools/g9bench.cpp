@@ -118,12 +118,29 @@ int main(int argc, char** argv) {
     g.zeros = zeros; g.ones = ones;
     const size_t n = (size_t)s.M * s.N;
     GemmArgs gk = g; gk.allow_kt = 1; gk.dbg = 0x10; gk.out = Okt;
-    GemmArgs g9 = g; g9.allow_g9 = 1; g9.out = Og9;
+    GemmArgs g9 = g; g9.allow_g9 = 3; g9.out = Og9;    // BN = 128
     GemmArgs g9w = g9; g9w.allow_g9 = 2; g9w.out = Og9b;   // the BN = 256 tiling
+    const int delays[3] = {0, 1, 3};                        // staggered second residents (g.dbg)
     if (!gemm9_ok(g9)) { printf("%-26s not eligible\n", s.tag); continue; }
     if (abl) {
       if (s.hw || s.M < 30000) continue;
       printf("%-26s", s.tag);
+      for (int dz : delays) {                               // BN = 128 with a staggered start
+        GemmArgs gz = g9; gz.dbg = dz;
+        launch_gemm9(gz, ST, 0);
+        CK(hipDeviceSynchronize());
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; ++rep) {
+          CK(hipEventRecord(e0, 0));
+          for (int i = 0; i < reps; ++i) launch_gemm9(gz, ST, 0);
+          CK(hipEventRecord(e1, 0));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          best = std::min(best, ms);
+        }
+        printf(" z%d=%.1f", dz, best * 1e3 / reps);
+      }
       for (int dbg : {0, 1, 2, 4, 6, 16, 22, 100, 116}) {   // 100+: the BN = 256 tiling
         const GemmArgs& ga = dbg >= 100 ? g9w : g9;
         launch_gemm9_dbg(ga, ST, dbg % 100, 0);

@@ -67,6 +67,10 @@ __global__ __launch_bounds__(BN * 2, 2) void gemm9_kernel(GemmArgs g, const floa
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid & 1, wn = wid >> 1;            // pixel half (128 rows), channel group (64)
   const int fr = lane & 15, fq = lane >> 4;
+  // experiment (g9bench): the second resident block of each CU starts g.dbg x 8k cycles late, so the
+  // two blocks' epilogues (stores) fall in each other's main loops from then on
+  if (BN == 128 && g.dbg > 0 && blockIdx.x >= 256 && blockIdx.x < 512)
+    for (int i = 0; i < g.dbg; ++i) __builtin_amdgcn_s_sleep(127);
 
   // ---- tile: the channel tiles of one pixel panel are consecutive ids on one XCD ----
   const int ntn = (g.N + BN - 1) / BN;
@@ -378,7 +382,11 @@ void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st) {
     else if (g.a.Ktot == 512) hipLaunchKernelGGL((ln_stats_kernel<512>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
     else hipLaunchKernelGGL((ln_stats_kernel<1024>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
   }
-  if (g.allow_g9 == 2) g9_launch<256>(g, sp, st);
+  // tiling: 256 channels where that still gives every CU two tiles (the A panel is read half as
+  // often), else 128 (two blocks per CU); allow_g9 2 / 3 force 256 / 128 (tools/g9bench)
+  const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + 255) / 256) : (g.M + 255) / 256;
+  const bool wide = g.allow_g9 == 2 || (g.allow_g9 == 1 && g.N % 256 == 0 && mt * (g.N / 256) >= 512);
+  if (wide) g9_launch<256>(g, sp, st);
   else g9_launch<128>(g, sp, st);
 }
 
@@ -393,7 +401,7 @@ static void g9_launch_dbg(const GemmArgs& g, void* stats, hipStream_t st) {
 }
 template <int DBG>
 static void g9_dbg2(const GemmArgs& g, void* stats, hipStream_t st) {
-  if (g.allow_g9 == 2) g9_launch_dbg<DBG, 256>(g, stats, st);
+  if (g.allow_g9 == 2) g9_launch_dbg<DBG, 256>(g, stats, st);   // (g9bench: 1 and 3 both BN = 128 here)
   else g9_launch_dbg<DBG, 128>(g, stats, st);
 }
 void launch_gemm9_dbg(const GemmArgs& g, void* stats, int dbg, hipStream_t st) {
