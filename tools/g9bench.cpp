@@ -93,10 +93,10 @@ int main(int argc, char** argv) {
   BlasCtx* blas = blas_create();
   std::vector<uint16_t> r1(maxO), r2(maxO);
   int bad = 0;
-  if (abl) printf("ablations (us): d0 full, d1 no MFMA, d2 no global loads, d4 no LDS, d6 no loads+LDS, d16 no stores, d22\n");
+  if (abl) printf("ablations (us), d<variant><DBG>: DBG 0 full, 1 no MFMA, 2 no global loads, 4 no LDS, 16 no stores, 22\n");
   else
-    printf("%-26s %8s %5s %5s | %8s %7s %6s | %8s | %8s %7s | %8s %7s | %9s %s\n", "shape", "M", "N", "K", "g9 us", "TF/s", "GB/s", "g9w us", "kt us",
-           "TF/s", "blas us", "TF/s", "max|d|", "race");
+    printf("%-26s %7s %5s %5s | %7s %7s %7s %7s %7s %7s %7s | best g9 | %9s %s\n", "shape (us)", "M", "N", "K", "128r", "256r", "256d4", "128d3",
+           "256d3", "kt", "blas", "max|d|", "races");
   for (auto& s : shapes) {
     GemmArgs g{};
     g.a.n = s.nsrc; g.a.Ktot = s.K;
@@ -119,30 +119,12 @@ int main(int argc, char** argv) {
     const size_t n = (size_t)s.M * s.N;
     GemmArgs gk = g; gk.allow_kt = 1; gk.dbg = 0x10; gk.out = Okt;
     GemmArgs g9 = g; g9.allow_g9 = 3; g9.out = Og9;    // BN = 128
-    GemmArgs g9w = g9; g9w.allow_g9 = 2; g9w.out = Og9b;   // the BN = 256 tiling
-    const int delays[3] = {0, 1, 3};                        // staggered second residents (g.dbg)
     if (!gemm9_ok(g9)) { printf("%-26s not eligible\n", s.tag); continue; }
     if (abl) {
       if (s.hw || s.M < 30000) continue;
       printf("%-26s", s.tag);
-      for (int dz : delays) {                               // BN = 128 with a staggered start
-        GemmArgs gz = g9; gz.dbg = dz;
-        launch_gemm9(gz, ST, 0);
-        CK(hipDeviceSynchronize());
-        float best = 1e30f;
-        for (int rep = 0; rep < 3; ++rep) {
-          CK(hipEventRecord(e0, 0));
-          for (int i = 0; i < reps; ++i) launch_gemm9(gz, ST, 0);
-          CK(hipEventRecord(e1, 0));
-          CK(hipEventSynchronize(e1));
-          float ms;
-          CK(hipEventElapsedTime(&ms, e0, e1));
-          best = std::min(best, ms);
-        }
-        printf(" z%d=%.1f", dz, best * 1e3 / reps);
-      }
-      for (int dbg : {0, 1, 2, 4, 6, 16, 22, 100, 116}) {   // 100+: the BN = 256 tiling
-        const GemmArgs& ga = dbg >= 100 ? g9w : g9;
+      for (int dbg : {400, 401, 402, 404, 416, 422, 500, 501, 502, 516}) {   // variant * 100 + DBG
+        GemmArgs ga = g9; ga.allow_g9 = dbg / 100;
         launch_gemm9_dbg(ga, ST, dbg % 100, 0);
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(e0, 0));
@@ -161,13 +143,16 @@ int main(int argc, char** argv) {
     const bool bl_ok = blas && s.nsrc == 1 && !s.gelu && !s.hw &&
                        blas_ready(blas, s.M, s.N, s.K, s.K, s.K, s.res ? s.N : 0, s.N, s.res != 0, true);
     LnRowsArgs la{A, s.K, 0, XN, s.K, s.M, s.K, 1};
-    double us[4] = {0, 0, 0, 0};
-    for (int v = 0; v < 4; ++v) {
-      if ((v == 1 && !kt_ok) || (v == 2 && !bl_ok)) continue;
+    // variants: g9 allow_g9 = 3 (BN 128 regs), 2 (BN 256 regs), 4 (BN 256 DMA4), 5 (BN 128 DMA3),
+    // 6 (BN 256 DMA3); then kt, hipBLASLt. Best of 3 timed batches each.
+    const int gv[5] = {3, 2, 4, 5, 6};
+    double us[7] = {0, 0, 0, 0, 0, 0, 0};
+    for (int v = 0; v < 7; ++v) {
+      if ((v == 5 && !kt_ok) || (v == 6 && !bl_ok)) continue;
+      GemmArgs gx = g9; if (v < 5) gx.allow_g9 = gv[v];
       auto run = [&] {
-        if (v == 0) launch_gemm9(g9, ST, 0);
-        else if (v == 3) launch_gemm9(g9w, ST, 0);
-        else if (v == 1) launch_gemm_kt(gk, 0);
+        if (v < 5) launch_gemm9(gx, ST, 0);
+        else if (v == 5) launch_gemm_kt(gk, 0);
         else {
           if (s.ln) launch_ln_rows<bf16>(la, 0);
           blas_gemm_bf16(blas, s.M, s.N, s.K, s.ln ? XN : A, s.K, Wt, s.K, vec + 8192, s.res ? R : nullptr, s.N, Obl, s.N, 0);
@@ -175,20 +160,26 @@ int main(int argc, char** argv) {
       };
       run();
       CK(hipDeviceSynchronize());
-      CK(hipEventRecord(e0, 0));
-      for (int i = 0; i < reps; ++i) run();
-      CK(hipEventRecord(e1, 0));
-      CK(hipEventSynchronize(e1));
-      float ms;
-      CK(hipEventElapsedTime(&ms, e0, e1));
-      us[v] = ms * 1e3 / reps;
+      float best = 1e30f;
+      for (int rep = 0; rep < 3; ++rep) {
+        CK(hipEventRecord(e0, 0));
+        for (int i = 0; i < reps; ++i) run();
+        CK(hipEventRecord(e1, 0));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        best = std::min(best, ms);
+      }
+      us[v] = best * 1e3 / reps;
     }
+    // race / variant screen: every variant's output equals the first launch's bit for bit
+    launch_gemm9(g9, ST, 0);
     CK(hipMemcpy(r1.data(), Og9, n * 2, hipMemcpyDeviceToHost));
     int races = 0;
-    GemmArgs g9b = g9; g9b.out = Og9b;
-    for (int it = 0; it < 8; ++it) {
+    for (int it = 0; it < 10; ++it) {
+      GemmArgs gx = g9; gx.out = Og9b; gx.allow_g9 = gv[it % 5];
       CK(hipMemset(Og9b, 0xff, n * 2));
-      launch_gemm9(it & 1 ? g9w : g9b, ST, 0);       // both tilings: same arithmetic per output
+      launch_gemm9(gx, ST, 0);
       CK(hipMemcpy(r2.data(), Og9b, n * 2, hipMemcpyDeviceToHost));
       if (memcmp(r1.data(), r2.data(), n * 2)) ++races;
     }
@@ -201,9 +192,11 @@ int main(int argc, char** argv) {
         md = std::max(md, std::isnan(d) ? 1e30 : d);
       }
     }
-    const double fl = 2.0 * s.M * s.N * s.K, by = 2.0 * ((double)s.M * s.K + (double)s.N * s.K + (double)s.M * s.N * (s.res ? 2 : 1));
-    printf("%-26s %8lld %5d %5d | %8.1f %7.0f %6.0f | %8.1f | %8.1f %7.0f | %8.1f %7.0f | %9.4g %d/8\n", s.tag, (long long)s.M, s.N, s.K, us[0],
-           fl / us[0] / 1e6, by / us[0] / 1e3, us[3], us[1], us[1] > 0 ? fl / us[1] / 1e6 : 0.0, us[2], us[2] > 0 ? fl / us[2] / 1e6 : 0.0, md, races);
+    const double fl = 2.0 * s.M * s.N * s.K;
+    printf("%-26s %7lld %5d %5d |", s.tag, (long long)s.M, s.N, s.K);
+    for (int v = 0; v < 7; ++v) printf(" %7.1f", us[v]);
+    double bestg = 1e30; for (int v = 0; v < 5; ++v) bestg = std::min(bestg, us[v]);
+    printf(" | %6.0f TF/s | %9.4g %d/10\n", fl / bestg / 1e6, md, races);
     fflush(stdout);
     if (races || md > 0.07 || md < 0) ++bad;
   }

@@ -49,6 +49,21 @@ TURTLE_DEV int g9_perm(int r) { return (r & ~31) | (8 * ((r >> 2) & 3) + 4 * ((r
 // byte offset of 16-byte chunk c of LDS row r (64-byte rows, swizzled)
 TURTLE_DEV int g9_off(int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 2)) << 4); }
 
+__device__ __attribute__((aligned(64))) uint4 g_zero_g9[4];
+
+// 64 lanes x 16 B -> LDS at M0 (inline asm: hipcc would treat the builtin as an LDS write it must
+// drain before every ds_read); M0 is compiler-reserved, so it is restored
+TURTLE_DEV void g9_dma16(const void* gp, uint32_t lds_wave_base) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gp), "s"(lds_wave_base) : "memory");
+}
+template <int N>
+TURTLE_DEV void g9_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
 }  // namespace
 
 // DBG (tools/g9bench ablations only; 0 in the library): 1 no MFMA, 2 no global loads in the loop,
@@ -56,21 +71,24 @@ TURTLE_DEV int g9_off(int r, int c) { return r * 64 + ((c ^ ((r >> 2) & 2)) << 4
 // MS: K-concatenated multi-source operand (per-step source selection); single source otherwise
 // BN: channels per block tile (256: 8 waves, one block per CU; 128: 4 waves, two blocks per CU, so
 // one block's epilogue stores overlap the other's main loop)
-template <bool LN, bool MS, int BN, int DBG = 0>
+// NSL: 0 - K steps staged through registers (global_load + ds_write), two LDS slots; 3 / 4 - staged
+// by LDS-DMA (global_load_lds_dwordx4: no VGPR round trip, no ds_write) into a ring of NSL slots,
+// NSL - 2 steps in flight, waits counted by hand (the loop issues no other vector-memory operation)
+template <bool LN, bool MS, int BN, int NSL = 0, int DBG = 0>
 __global__ __launch_bounds__(BN * 2, 2) void gemm9_kernel(GemmArgs g, const float2* __restrict__ stats) {
   constexpr int NT = BN * 2;                        // threads: 2 pixel halves x BN / 64 channel groups of waves
+  constexpr int NWV = NT / 64;                      // waves
   constexpr int WOFF = 16384;                       // W tile offset in a slot (A: 256 rows x 64 B)
   constexpr int SLOT = WOFF + BN * 64;
   constexpr int NA = 1024 / NT, NW = BN * 4 / NT;   // staged 16-byte chunks per thread and step
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  constexpr int NPW = (16 + BN / 16) / NWV;         // LDS-DMA: 1-KB pieces per wave and step
+  constexpr int NSLOT = NSL ? NSL : 2;
+  static_assert(NSL == 0 || NSL == 3 || NSL == 4, "ring depth");
+  __shared__ __attribute__((aligned(16))) char smem[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wid & 1, wn = wid >> 1;            // pixel half (128 rows), channel group (64)
   const int fr = lane & 15, fq = lane >> 4;
-  // experiment (g9bench): the second resident block of each CU starts g.dbg x 8k cycles late, so the
-  // two blocks' epilogues (stores) fall in each other's main loops from then on
-  if (BN == 128 && g.dbg > 0 && blockIdx.x >= 256 && blockIdx.x < 512)
-    for (int i = 0; i < g.dbg; ++i) __builtin_amdgcn_s_sleep(127);
 
   // ---- tile: the channel tiles of one pixel panel are consecutive ids on one XCD ----
   const int ntn = (g.N + BN - 1) / BN;
@@ -147,6 +165,63 @@ __global__ __launch_bounds__(BN * 2, 2) void gemm9_kernel(GemmArgs g, const floa
 #pragma unroll
     for (int i = 0; i < NW; ++i) *reinterpret_cast<uint4*>(sb + WOFF + soff[i]) = gw[i];
   };
+  // LDS-DMA geometry: piece q = wid + NWV i of a slot is 1 KB = 16 LDS rows of 64 B (A rows for
+  // q < 16, then W rows); lane l fills row 16 q + l / 4, position l % 4, which holds source chunk
+  // (l % 4) ^ swz(row) - the swizzle goes on the source address (the LDS side is lane-linear)
+  const bf16* dsrc[NPW];                            // step-0 source of each piece (A single source / W)
+  int64_t drow[NPW];                                // A pixel row (multi-source A)
+  int dck[NPW];                                     // source chunk (elements)
+  bool disa[NPW];
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+#pragma unroll
+  for (int i = 0; i < NPW; ++i) {
+    const int q = wid + NWV * i;
+    const int r = 16 * (q < 16 ? q : q - 16) + (lane >> 2);
+    const int c = ((lane & 3) ^ ((r >> 2) & 2)) * 8;
+    disa[i] = q < 16;
+    dck[i] = c;
+    if (q < 16) {
+      const int64_t m = m0 + r;
+      drow[i] = m < mlim ? m : m0;
+      dsrc[i] = reinterpret_cast<const bf16*>(g.a.s[0].base) + g.a.s[0].off + c + (MS ? 0 : drow[i] * g.a.s[0].ld);
+    } else {
+      drow[i] = 0;
+      dsrc[i] = Wp + (int64_t)min(n0 + g9_perm(r), g.N - 1) * g.ldw + c;
+    }
+  }
+  // K step t -> slot `slot` (past the last step: the zero line, so every step issues NPW pieces)
+  auto dma = [&](int t, int slot) __attribute__((always_inline)) {
+    if constexpr ((DBG & 2) != 0) return;
+    const int k0 = t * G9_BK;
+    const bool live = t < nk;
+    const bf16* base = nullptr;
+    int64_t sld = 0;
+    int kb = 0;
+    if constexpr (MS) {
+      base = reinterpret_cast<const bf16*>(g.a.s[0].base) + g.a.s[0].off;
+      sld = g.a.s[0].ld;
+      int kbj = g.a.s[0].K;
+#pragma unroll
+      for (int j = 1; j < TURTLE_MAX_SRC; ++j) {
+        const bool hit = j < g.a.n && k0 >= kbj;
+        base = hit ? reinterpret_cast<const bf16*>(g.a.s[j].base) + g.a.s[j].off : base;
+        sld = hit ? g.a.s[j].ld : sld;
+        kb = hit ? kbj : kb;
+        kbj += j < g.a.n ? g.a.s[j].K : 0;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NPW; ++i) {
+      const bf16* src;
+      if (MS && disa[i]) src = base + drow[i] * sld + (k0 - kb) + dck[i];
+      else src = dsrc[i] + k0;
+      uint64_t pa = reinterpret_cast<uint64_t>(src);
+      asm volatile("" : "+v"(pa));                   // computed for every lane, then selected (no branch)
+      g9_dma16(live ? reinterpret_cast<const void*>(pa) : reinterpret_cast<const void*>(g_zero_g9),
+               lds_base + slot * SLOT + (wid + NWV * i) * 1024);
+    }
+  };
+
   // fragment reads: rows wm*128 + 16 i + fr of A, wn*64 + 16 j + fr of W; chunk fq
   const int foff = g9_off(fr, fq);                  // (rows of a fragment start at multiples of 16)
   const char* fa_base = smem + (wm * 128) * 64 + foff;
@@ -207,10 +282,52 @@ __global__ __launch_bounds__(BN * 2, 2) void gemm9_kernel(GemmArgs g, const floa
       for (int k = 0; k < 8; ++k) { __builtin_amdgcn_sched_group_barrier(0x008, 2, 0); __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); }
     }
   };
+  // LDS-DMA ring: at step t - wait for own pieces of step t+1 (NSL-3 steps stay in flight),
+  // barrier (everyone's step t+1 landed; every read of step t-1's slot retired at step t-1's MFMAs),
+  // step t+NSL-1 -> that slot, fragments of step t+1, 64 MFMAs of step t
+  auto step_dma = [&](int t, auto B) __attribute__((always_inline)) {
+    constexpr int b = decltype(B)::value;
+    g9_vm<(NSLOT - 3) * NPW>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    dma(t + NSLOT - 1, (t + NSLOT - 1) % NSLOT);
+    const int nslot = ((t + 1) % NSLOT) * SLOT;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fw[b ^ 1][j] = rd(fw_base + nslot + 16 * j * 64);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if constexpr ((DBG & 1) == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fw[b][j], fa[i], acc[i][j], 0, 0, 0);
+      }
+      fa[i] = rd(fa_base + nslot + 16 * i * 64);
+    }
+    if constexpr (G9_SCHED && (DBG & 7) == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) { __builtin_amdgcn_sched_group_barrier(0x008, 3, 0); __builtin_amdgcn_sched_group_barrier(0x100, 1, 0); }
+    }
+  };
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
   using T_ = std::true_type;
   using F_ = std::false_type;
+  if constexpr (NSL > 0) {
+    for (int s0 = 0; s0 < NSLOT - 1; ++s0) dma(s0, s0);
+    g9_vm<(NSLOT - 2) * NPW>();                     // step 0 landed
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fw[0][j] = rd(fw_base + 16 * j * 64);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[i] = rd(fa_base + 16 * i * 64);
+    for (int t = 0; t < nk; t += 2) {
+      step_dma(t, I0{});
+      step_dma(t + 1, I1{});
+    }
+    g9_vm<0>();                                     // the zero-line pieces past the end have landed
+  } else {
   // prologue: steps 0, 1 -> slots 0, 1; step 2 staged; fragments of step 0
   gload(0);
   swrite(0);
@@ -232,6 +349,7 @@ __global__ __launch_bounds__(BN * 2, 2) void gemm9_kernel(GemmArgs g, const floa
   step(t + 1, I1{}, T_{}, F_{});
   step(t + 2, I0{}, F_{}, F_{});
   step(t + 3, I1{}, F_{}, F_{});
+  }
 
   // ---- epilogue: lane holds channels c .. c+7 (c = n0 + 64 wn + 32 s + 8 fq) of pixel rows
   // m0 + 128 wm + 16 i + fr (sub-tiles 2s, 2s+1 of the permuted weight rows) ----
@@ -364,14 +482,17 @@ bool gemm9_ok(const GemmArgs& g) {
 size_t gemm9_stats_bytes(const GemmArgs& g) { return g.ln ? (size_t)g.M * sizeof(float2) : 0; }
 
 // `stats`: workspace of gemm9_stats_bytes(g) (LN GEMMs), filled here before the GEMM
-template <int BN>
+template <int BN, int NSL>
 static void g9_launch(const GemmArgs& g, float2* sp, hipStream_t st) {
   const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + 255) / 256) : (g.M + 255) / 256;
   const dim3 grid((unsigned)(mt * ((g.N + BN - 1) / BN))), blk(2 * BN);
-  if (g.ln) hipLaunchKernelGGL((gemm9_kernel<true, false, BN>), grid, blk, 0, st, g, sp);
-  else if (g.a.n > 1) hipLaunchKernelGGL((gemm9_kernel<false, true, BN>), grid, blk, 0, st, g, sp);
-  else hipLaunchKernelGGL((gemm9_kernel<false, false, BN>), grid, blk, 0, st, g, sp);
+  if (g.ln) hipLaunchKernelGGL((gemm9_kernel<true, false, BN, NSL>), grid, blk, 0, st, g, sp);
+  else if (g.a.n > 1) hipLaunchKernelGGL((gemm9_kernel<false, true, BN, NSL>), grid, blk, 0, st, g, sp);
+  else hipLaunchKernelGGL((gemm9_kernel<false, false, BN, NSL>), grid, blk, 0, st, g, sp);
 }
+// g.allow_g9: 1 the measured choice per shape; 2..6 a fixed variant (tools/g9bench):
+// 2 BN 256 register-staged, 3 BN 128 register-staged, 4 BN 256 DMA ring 4, 5 BN 128 DMA ring 3,
+// 6 BN 256 DMA ring 3
 void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st) {
   float2* sp = reinterpret_cast<float2*>(stats);
   if (g.ln) {
@@ -382,34 +503,46 @@ void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st) {
     else if (g.a.Ktot == 512) hipLaunchKernelGGL((ln_stats_kernel<512>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
     else hipLaunchKernelGGL((ln_stats_kernel<1024>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
   }
-  // tiling: 256 channels where that still gives every CU two tiles (the A panel is read half as
-  // often), else 128 (two blocks per CU); allow_g9 2 / 3 force 256 / 128 (tools/g9bench)
-  const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + 255) / 256) : (g.M + 255) / 256;
-  const bool wide = g.allow_g9 == 2 || (g.allow_g9 == 1 && g.N % 256 == 0 && mt * (g.N / 256) >= 512);
-  if (wide) g9_launch<256>(g, sp, st);
-  else g9_launch<128>(g, sp, st);
+  int v = g.allow_g9;
+  if (v == 1) {
+    // 256 channels on the LDS-DMA ring wherever every CU still gets a tile (the A panel is read
+    // half as often; fastest on the latent shapes, tools/g9bench), else 128 register-staged
+    const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + 255) / 256) : (g.M + 255) / 256;
+    v = g.N % 256 == 0 && mt * (g.N / 256) >= 256 ? 4 : 3;
+  }
+  switch (v) {
+    case 2: g9_launch<256, 0>(g, sp, st); break;
+    case 4: g9_launch<256, 4>(g, sp, st); break;
+    case 5: g9_launch<128, 3>(g, sp, st); break;
+    case 6: g9_launch<256, 3>(g, sp, st); break;
+    default: g9_launch<128, 0>(g, sp, st);
+  }
 }
 
 #ifdef TURTLE_G9_ABLATIONS
-template <int DBG, int BN>
+template <int DBG, int BN, int NSL>
 static void g9_launch_dbg(const GemmArgs& g, void* stats, hipStream_t st) {
   const dim3 grid((unsigned)(((g.M + 255) / 256) * ((g.N + BN - 1) / BN))), blk(2 * BN);
   float2* sp = reinterpret_cast<float2*>(stats);
-  if (g.ln) hipLaunchKernelGGL((gemm9_kernel<true, false, BN, DBG>), grid, blk, 0, st, g, sp);
-  else if (g.a.n > 1) hipLaunchKernelGGL((gemm9_kernel<false, true, BN, DBG>), grid, blk, 0, st, g, sp);
-  else hipLaunchKernelGGL((gemm9_kernel<false, false, BN, DBG>), grid, blk, 0, st, g, sp);
+  if (g.ln) hipLaunchKernelGGL((gemm9_kernel<true, false, BN, NSL, DBG>), grid, blk, 0, st, g, sp);
+  else if (g.a.n > 1) hipLaunchKernelGGL((gemm9_kernel<false, true, BN, NSL, DBG>), grid, blk, 0, st, g, sp);
+  else hipLaunchKernelGGL((gemm9_kernel<false, false, BN, NSL, DBG>), grid, blk, 0, st, g, sp);
 }
 template <int DBG>
 static void g9_dbg2(const GemmArgs& g, void* stats, hipStream_t st) {
-  if (g.allow_g9 == 2) g9_launch_dbg<DBG, 256>(g, stats, st);   // (g9bench: 1 and 3 both BN = 128 here)
-  else g9_launch_dbg<DBG, 128>(g, stats, st);
+  switch (g.allow_g9) {
+    case 2: g9_launch_dbg<DBG, 256, 0>(g, stats, st); break;
+    case 4: g9_launch_dbg<DBG, 256, 4>(g, stats, st); break;
+    case 5: g9_launch_dbg<DBG, 128, 3>(g, stats, st); break;
+    case 6: g9_launch_dbg<DBG, 256, 3>(g, stats, st); break;
+    default: g9_launch_dbg<DBG, 128, 0>(g, stats, st);
+  }
 }
 void launch_gemm9_dbg(const GemmArgs& g, void* stats, int dbg, hipStream_t st) {
   switch (dbg) {
     case 1: g9_dbg2<1>(g, stats, st); break;
     case 2: g9_dbg2<2>(g, stats, st); break;
     case 4: g9_dbg2<4>(g, stats, st); break;
-    case 6: g9_dbg2<6>(g, stats, st); break;
     case 16: g9_dbg2<16>(g, stats, st); break;
     case 22: g9_dbg2<22>(g, stats, st); break;
     default: g9_dbg2<0>(g, stats, st);

@@ -801,14 +801,16 @@ struct Runner {
       if (gemm8_ok(g) && pick) lt = false;
       else g.allow_g8 = 0;
     }
-    // four-wave 256 x 256 GEMM: 1 in place of hipBLASLt, 2 every eligible bf16 projection
+    // 256-row-tile GEMM (gemm9.hip): 1 in place of hipBLASLt - gemm9 for the latent-level shapes
+    // (<= 65536 pixels), the in-tree dispatcher (ar / pn / kt) for the larger ones -, 2 every
+    // eligible bf16 projection
     bool use9 = false;
-    if (ES == 2 && h->gemm9) {
+    if (ES == 2 && h->gemm9 && (h->gemm9 == 2 || lt)) {
       GemmArgs t9 = g;
       t9.allow_g9 = 1;
-      if ((h->gemm9 == 2 || lt) && gemm9_ok(t9) && (!g.ln || st9)) {
+      lt = false;
+      if ((h->gemm9 == 2 || M <= 65536) && gemm9_ok(t9) && (!g.ln || st9)) {
         use9 = true;
-        lt = false;
         g.allow_g8 = 0;
         g.allow_g9 = 1;
       }
