@@ -1,7 +1,8 @@
 // Microbenchmark + cross-check of the row-walk fused kernel (fused2.hip) against the tile-fused
 // kernel (fused.hip) on the Turtle 1080p launch shapes, GPU box only:
-//   hipcc -O3 --offload-arch=gfx950 -I turtlevsr_amd/csrc tools/f2bench.cpp -L turtlevsr_amd/lib -lturtle_hip \
-//         -Wl,-rpath,$PWD/turtlevsr_amd/lib -o tools/f2bench && tools/f2bench [reps]
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTURTLE_F2_ABLATIONS -I turtlevsr_amd/csrc tools/f2bench.cpp \
+//         turtlevsr_amd/csrc/fused2.hip -L turtlevsr_amd/lib -lturtle_hip -Wl,-rpath,'$ORIGIN/../turtlevsr_amd/lib' \
+//         -o tools/f2bench && tools/f2bench [reps] [shape substring] [variants] [abl]
 // Same random inputs for every kernel (LayerNorm statistics, biases, scales all live). Reference:
 // fused.hip in fp32 (the parity-tested path) on the bf16 values widened to fp32. Prints per kernel
 // the average launch time (HIP events) and the relative RMS / max error against that reference.
@@ -47,6 +48,7 @@ int main(int argc, char** argv) {
   std::vector<int> vlist;
   if (argc > 3) for (const char* p = argv[3]; *p;) { vlist.push_back(atoi(p)); while (*p && *p != ',') ++p; if (*p) ++p; }
   const int only_v = vlist.empty() ? -1 : vlist[0];
+  const bool abl = argc > 4 && !strcmp(argv[4], "abl");   // per-phase ablation table (TURTLE_F2_ABLATIONS build)
   const Shape shapes[] = {
       {1088, 1920, 64, 320, 64, F_GATE, 1, "L1 GFFW gate"},
       {1088, 1920, 64, 128, 64, F_GELU, 1, "L1 ReducedAttn"},
@@ -149,7 +151,16 @@ int main(int argc, char** argv) {
       printf("%-16s %-10s %9.1f %9.2e %9.2e\n", s.tag, name, ms * 1e3 / reps, sqrt(se / o.size()) / rr, mx);
     };
     if (only_v < 0 && has_ref) run("fused", [&] { launch_fused<bf16>(ab, 0); });
-    if (fused2_ok(ab)) {
+    if (fused2_ok(ab) && abl) {
+      // per-phase ablations of the default configuration (fused2.hip ABL bits): 1 no GELU, 2 no
+      // depthwise, 4 no GEMM2, 8 no LN, 16 no stores, 32 no GEMM1
+      for (int ab_bits : {0, 1, 2, 4, 8, 16, 32, 3, 7, 39, 63}) {
+        if (s.mode == F_DWONLY && (ab_bits & 5) && ab_bits != 63) continue;
+        FusedArgs c = ab; c.dbg = ab_bits << 8;
+        char nm[16]; snprintf(nm, sizeof nm, "abl.%d", ab_bits);
+        run(nm, [&] { launch_fused2(c, 0); });
+      }
+    } else if (fused2_ok(ab)) {
       for (int v = 0; v < 9; ++v) {
         if (only_v >= 0 && std::find(vlist.begin(), vlist.end(), v) == vlist.end()) continue;
         if (v >= 6 && !(ab.mode == F_GATE && ab.C == 64)) continue;

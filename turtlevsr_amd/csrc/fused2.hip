@@ -88,7 +88,10 @@ struct F2L {
 // loaded once per block instead of once per tile)
 // TG: per-channel tables (taps, LN / bias vectors) read from global memory (L2) at the start of each
 // walk instead of staged in LDS: 32 * N1M fewer LDS bytes per block, i.e. more blocks per CU
-template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE, int TPB = 1, bool TG = false>
+// ABL: per-phase ablations (tools/f2bench built with TURTLE_F2_ABLATIONS; 0 in the library): 1 no GELU,
+// 2 no depthwise (the centre row only), 4 no GEMM2 MFMAs, 8 no LayerNorm prologue, 16 no output
+// stores, 32 no GEMM1 (MFMAs and their LDS reads)
+template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE, int TPB = 1, bool TG = false, int ABL = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void fused2_kernel(FusedArgs a) {
   using L = F2L<CM, R, HPM, TG ? 0 : N1M>;
   constexpr int KS = CM / 32;                       // GEMM1 K steps
@@ -167,7 +170,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
   // becomes (x - mu) rs (BiasFree: x rs, uncentred), rounded to bf16 once - the resident-panel
   // GEMM does the same - so GEMM1's epilogue is only + (W1 b_ln + b1), carried in as the MFMA's
   // initial accumulator. The residual of GEMM2 is re-read from HBM/L2 (the raw tile is gone). ----
-  if (a.ln) {                                      // uniform: the shuffles run in whole waves
+  if (a.ln && !(ABL & 8)) {                       // uniform: the shuffles run in whole waves
     for (int e = tid; e < 2 * L::NXP; e += NT) {
       const int p = e >> 1, h = e & 1;
       bf16* row = reinterpret_cast<bf16*>(sX + p * L::XP);
@@ -252,8 +255,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     (void)s4;
     auto gemm1 = [&](const bf16x8 (&xf)[KS]) {
       f32x4 acc = tbm;
+      if constexpr (!(ABL & 32)) {
 #pragma unroll
-      for (int k = 0; k < KS; ++k) acc = mfma(wf[k], xf[k], acc);
+        for (int k = 0; k < KS; ++k) acc = mfma(wf[k], xf[k], acc);
+      }
       return acc;
     };
     // rows outside the image are 0 (depthwise zero padding): one packed multiply by a wave-uniform
@@ -329,9 +334,14 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
           for (int q = 0; q < 4; ++q) fmac_shl1(d[q], w[q], wt[t0 + 2][q]);
         };
-        row(wc[s0], 0);
-        row(wc[s1], 3);
-        row(wc[s2], 6);
+        if constexpr (!(ABL & 2)) {
+          row(wc[s0], 0);
+          row(wc[s1], 3);
+          row(wc[s2], 6);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) d[q] = wc[s1][q];
+        }
         emit(hr - 2, f32x4{d[0], d[1], d[2], d[3]});
       });
     }
@@ -373,7 +383,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
           } else {
             off = ((int64_t)img * a.H + y) * rowstep + colpart;
           }
-          *reinterpret_cast<bf16x4*>(dp + off) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
+          if (!(ABL & 16) || d[0] == 1.2345f) *reinterpret_cast<bf16x4*>(dp + off) = bf16x4{(bf16)d[0], (bf16)d[1], (bf16)d[2], (bf16)d[3]};
         });
       };
       if (u + NW < nunit) load_w1(wb, (u + NW) * 16);
@@ -427,7 +437,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             bf16x4 g;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-              const f32x2 r = gelu_bf16_2(f32x2{d[2 * h], d[2 * h + 1]});
+              const f32x2 r = (ABL & 1) ? f32x2{d[2 * h], d[2 * h + 1]} : gelu_bf16_2(f32x2{d[2 * h], d[2 * h + 1]});
               g[2 * h] = (bf16)r.x; g[2 * h + 1] = (bf16)r.y;
             }
             *reinterpret_cast<bf16x4*>(gcol + (orow * 16 + px) * L::GP) = g;
@@ -462,7 +472,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
           const char* grow = sG + (r * 16 + px) * L::GP + grp * 16;
 #pragma unroll
           for (int k = 0; k < KP; ++k)
-            if (k < kst) acc2[o][r] = mfma(w2f[o][k], *reinterpret_cast<const bf16x8*>(grow + k * 64), acc2[o][r]);
+            if (k < kst && !(ABL & 4)) acc2[o][r] = mfma(w2f[o][k], *reinterpret_cast<const bf16x8*>(grow + k * 64), acc2[o][r]);
         }
       }
     }
@@ -486,7 +496,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         bf16x4 ov;
 #pragma unroll
         for (int q = 0; q < 4; ++q) ov[q] = (bf16)fmaf(acc2[o][r][q] + b[q], sc[q], (float)xr[q]);
-        if (out_lane && y < a.H)
+        if (out_lane && y < a.H && (!(ABL & 16) || (float)ov[0] == 1.2345f))
           *reinterpret_cast<bf16x4*>(out + (((int64_t)img * a.H + y) * a.W + xg) * a.ldo + a.offo + ch) = ov;
       }
     }
@@ -496,7 +506,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
 // (MODE, C) -> (tile rows, waves, hidden per pass); units per pass chosen so every wave of a pass
 // gets the same number of units
-template <int MODE, int CM, int R, int NW, int HPM, int WPE, int TPB = 1, bool TG = false>
+template <int MODE, int CM, int R, int NW, int HPM, int WPE, int TPB = 1, bool TG = false, int ABL = 0>
 static void f2_launch(const FusedArgs& a0, hipStream_t st) {
   FusedArgs a = a0;
   a.up = HPM / 16;
@@ -505,7 +515,7 @@ static void f2_launch(const FusedArgs& a0, hipStream_t st) {
   constexpr int N1M = MODE == F_GATE ? 5 * CM : (MODE == F_GELU ? 2 * CM : 6 * CM);
   const int64_t tiles = (int64_t)a.nimg * ((a.H + R - 1) / R) * ((a.W + F2_TX - 1) / F2_TX);
   const int64_t blocks = (tiles + TPB - 1) / TPB;
-  hipLaunchKernelGGL((fused2_kernel<MODE, CM, R, NW, HPM, N1M, WPE, TPB, TG>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, a);
+  hipLaunchKernelGGL((fused2_kernel<MODE, CM, R, NW, HPM, N1M, WPE, TPB, TG, ABL>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, a);
 }
 
 bool fused2_ok(const FusedArgs& a) {
@@ -522,10 +532,43 @@ bool fused2_ok(const FusedArgs& a) {
 // Configurations: tile rows R (a multiple of 3: window slots), hidden channels per pass HPM,
 // minimum waves per SIMD WPE. `a.dbg` (tools/f2bench only; 0 in the product path) selects an
 // alternative configuration for the same shape.
+#ifdef TURTLE_F2_ABLATIONS
+// the default configuration of each shape family with ablation bits `abl` (a.dbg >> 8)
+template <int ABL>
+static void f2_abl(const FusedArgs& a, hipStream_t st) {
+  if (a.mode == F_DWONLY) {
+    if (a.C == 64) f2_launch<F_DWONLY, 64, 12, 4, 0, 4, 1, false, ABL>(a, st);
+    else f2_launch<F_DWONLY, 128, 9, 4, 0, 4, 1, false, ABL>(a, st);
+  } else if (a.mode == F_GATE) {
+    if (a.C == 64) f2_launch<F_GATE, 64, 6, 4, 64, 3, 1, false, ABL>(a, st);
+    else f2_launch<F_GATE, 128, 6, 4, 64, 2, 1, false, ABL>(a, st);
+  } else {
+    if (a.C == 64) f2_launch<F_GELU, 64, 6, 4, 128, 3, 1, false, ABL>(a, st);
+    else f2_launch<F_GELU, 128, 9, 4, 64, 2, 1, false, ABL>(a, st);
+  }
+}
+#endif
+
 void launch_fused2(const FusedArgs& a, hipStream_t st) {
   // defaults (v = 0) are the fastest measured per shape family on MI355X (tools/f2bench, 1080p);
   // v = 1..5 are the alternatives of the last sweep (profiles/r02h_f2bench_sweep.log)
-  const int v = a.dbg;
+  const int v = a.dbg & 255;
+#ifdef TURTLE_F2_ABLATIONS
+  switch (a.dbg >> 8) {
+    case 0: break;
+    case 1: f2_abl<1>(a, st); return;
+    case 2: f2_abl<2>(a, st); return;
+    case 4: f2_abl<4>(a, st); return;
+    case 8: f2_abl<8>(a, st); return;
+    case 16: f2_abl<16>(a, st); return;
+    case 32: f2_abl<32>(a, st); return;
+    case 3: f2_abl<3>(a, st); return;
+    case 7: f2_abl<7>(a, st); return;
+    case 39: f2_abl<39>(a, st); return;
+    case 63: f2_abl<63>(a, st); return;
+    default: return;
+  }
+#endif
   if (a.mode == F_DWONLY) {
     if (a.C == 64) {
       switch (v) {
