@@ -135,11 +135,12 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
  *   "gemm_kt"      [1] 2-D tiled deep-ring GEMM (3x3 up/down convolutions, K >= 640, small maps)
  *   "gemm_lds"     [1] LDS-pipelined GEMM (fallback where the kernels above do not apply)
  *   "panel_gemm"   [1] register-panel GEMM fallback; 0: K-loop GEMM
- *   "blaslt"       [1] hipBLASLt for the latent-level plain projections it wins (blas.cpp)
- *   "gemm8"        [3] 256 x 256 four-phase GEMM (gemm8.hip): 1 in place of hipBLASLt, 2 every eligible projection,
+ *   "gemm9"        [1] 256-pixel-row GEMM (gemm9.hip): 1 the 'wide' projection class (latent LN projections, project_out
+ *                  K = 1280, latent / level-3 W_eff; hipBLASLt until round 4 - the library links no vendor GEMM now),
+ *                  2 every eligible projection, 0 never
+ *   "gemm8"        [3] 256 x 256 four-phase GEMM (gemm8.hip): 1 the 'wide' class, 2 every eligible projection,
  *                  3 the multi-source projections with K >= 1024 (where it measures fastest), 0 never
  *   "gemm8_ps"     [0] ... in its persistent form (one block per CU walks its tiles as one K-tile stream)
- *   "blas_multi_img" [0] hipBLASLt also for multi-image W_eff (one call per image; 0: one 2-D tiled launch)
  *   "kt_max_px"    [32768] (integer) below this many pixels every eligible GEMM goes to the 2-D tiled kernel
  *   "attn_fin"     [0] channel-attention row softmax inside the W_eff launch (attn.hip)
  *   "sab_waves"    [0] waves per SAB score block: 4 (64 queries) or 8 (128 queries per staged key tile); 0 = 8 at

@@ -1,4 +1,5 @@
-// Vendor GEMM (hipBLASLt) for the plain bf16 projections where it beats the in-tree kernels.
+// Vendor GEMM (hipBLASLt) reference of the GEMM microbenchmarks (tools/g8bench, g9bench, kbench):
+// the library ran these shapes on hipBLASLt until round 4; since round 5 they run on gemm9.hip.
 //
 // Measured on MI355X (tools/torch_gemm_probe.py vs tools/kbench): the in-tree kernels win the
 // LayerNorm-folded, multi-source, implicit-3x3 and narrow high-M shapes (levels 1-2), hipBLASLt
@@ -15,7 +16,7 @@
 #include <map>
 #include <tuple>
 
-#include "kernels.h"
+#include "blas_ref.h"
 
 namespace turtle {
 

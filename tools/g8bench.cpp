@@ -1,6 +1,6 @@
 // Microbenchmark of the 256 x 256 four-phase GEMM (gemm8.hip) against the 2-D tiled kernel (gemm5.hip,
 // the parity reference here) and hipBLASLt on the Turtle projection shapes (GPU box, no Python).
-//   hipcc -O3 --offload-arch=gfx950 -I turtlevsr_amd/csrc tools/g8bench.cpp -L turtlevsr_amd/lib -lturtle_hip \
+//   hipcc -O3 --offload-arch=gfx950 -I turtlevsr_amd/csrc tools/g8bench.cpp tools/blas_ref.cpp -L turtlevsr_amd/lib -lturtle_hip -lhipblaslt \
 //         -Wl,-rpath,'$ORIGIN/../turtlevsr_amd/lib' -o tools/g8bench
 //   ./g8bench [reps]
 // Per shape: max |g8 - kt| over the output, and a race screen - the g8 output of every timed launch
@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "blas_ref.h"
 
 using namespace turtle;
 

@@ -1,7 +1,7 @@
 // Microbenchmark of the 256-pixel-row GEMM (gemm9.hip, BN = 128 and 256 channel tilings) against the 2-D tiled kernel
 // (gemm5.hip, the parity reference here) and hipBLASLt on the Turtle projection shapes (GPU box).
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTURTLE_G9_ABLATIONS -I turtlevsr_amd/csrc \
-//         tools/g9bench.cpp turtlevsr_amd/csrc/gemm9.hip -L turtlevsr_amd/lib -lturtle_hip \
+//         tools/g9bench.cpp tools/blas_ref.cpp turtlevsr_amd/csrc/gemm9.hip -L turtlevsr_amd/lib -lturtle_hip -lhipblaslt \
 //         -Wl,-rpath,'$ORIGIN/../turtlevsr_amd/lib' -o tools/g9bench
 //   ./g9bench [reps] [abl]
 // Per shape: max |g9 - kt| (LN shapes: kt on the same folded LN), and a race screen - 8 fresh g9
@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "blas_ref.h"
 
 using namespace turtle;
 namespace turtle { void launch_gemm9_dbg(const GemmArgs& g, void* stats, int dbg, hipStream_t st); }

@@ -48,7 +48,7 @@ for s in $STEPS; do
       rc=$?; echo "modprobe rc=$rc"; [ $rc -ne 0 ] && exit $rc ;;
     ab)
       # launch-shape reports of the default build and kernel-switch variants (AB_OPTS, ';'-separated)
-      IFS=';' read -ra VARS <<< "${AB_OPTS:-;blaslt=0}"
+      IFS=';' read -ra VARS <<< "${AB_OPTS:-;gemm9=0}"
       i=0
       for v in "${VARS[@]}"; do
         extra=""; for o in $v; do extra="$extra --opt $o"; done

@@ -1,5 +1,5 @@
 // Kernel microbenchmark for the GEMM variants of libturtle_hip (GPU box, no Python).
-//   hipcc -O3 --offload-arch=gfx950 -I turtlevsr_amd/csrc tools/kbench.cpp -L turtlevsr_amd/lib -lturtle_hip
+//   hipcc -O3 --offload-arch=gfx950 -I turtlevsr_amd/csrc tools/kbench.cpp tools/blas_ref.cpp -L turtlevsr_amd/lib -lturtle_hip -lhipblaslt
 //   ./kbench [reps]
 // For each Turtle GEMM shape: random bf16 operands, the LDS-pipelined kernel against the panel /
 // K-loop kernel (max |diff| over the output), average launch time of each from HIP events.
@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "kernels.h"
+#include "blas_ref.h"
 
 using namespace turtle;
 

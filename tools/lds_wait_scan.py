@@ -23,25 +23,56 @@ def regs(spec):
 
 
 def scan(asm_lines):
-    bad, kernel, pending = [], None, set()
+    """Per kernel, a forward dataflow over the basic blocks: the registers of LDS reads still in flight
+    at each label are the union over every edge into it (fall-through and s_branch / s_cbranch_*,
+    back-edges included: iterated to a fixpoint), so a use after a join or at a loop header is
+    judged on every path into it, and code after an unconditional branch inherits nothing."""
+    kernels, cur = [], None
     for ln in asm_lines:
         if re.match(r"^[A-Za-z_.$][\w.$]*:", ln) and not ln.startswith("."):
-            kernel, pending = ln.split(":")[0], set()
+            cur = (ln.split(":")[0], [])
+            kernels.append(cur)
             continue
-        t = ln.split("//")[0].strip()
-        parts = t.split(None, 1)
-        if not parts:
-            continue
-        op = parts[0]
-        ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
-        if op == "s_waitcnt" and "lgkmcnt" in t:
-            pending = set()          # conservative: any lgkm wait is taken to cover the reads
-        elif op.startswith("ds_read") and ops:
-            pending |= regs(ops[0])
-        elif op.startswith("v_mfma") and len(ops) >= 3:
-            used = regs(ops[1]) | regs(ops[2])
-            if used & pending:
-                bad.append((kernel, t))
+        if cur is not None:
+            cur[1].append(ln)
+    bad = []
+    for kernel, body in kernels:
+        entry = {}                   # label -> registers in flight on some edge into it
+        for _ in range(8):
+            changed, found = False, []
+            pending, live = set(), True
+            for ln in body:
+                t = ln.split("//")[0].split(";")[0].strip()
+                m = re.match(r"^(\.LBB\w+):", t)
+                if m:
+                    pending = (pending if live else set()) | entry.get(m.group(1), set())
+                    live = True
+                    continue
+                parts = t.split(None, 1)
+                if not parts or not live:
+                    continue
+                op = parts[0]
+                ops = [o.strip() for o in parts[1].split(",")] if len(parts) > 1 else []
+                if op == "s_waitcnt" and "lgkmcnt" in t:
+                    pending = set()          # conservative: any lgkm wait is taken to cover the reads
+                elif op.startswith("ds_read") and ops:
+                    pending = pending | regs(ops[0])
+                elif op.startswith("v_mfma") and len(ops) >= 3:
+                    used = regs(ops[1]) | regs(ops[2])
+                    if used & pending:
+                        found.append((kernel, t))
+                elif op.startswith("s_cbranch") or op == "s_branch":
+                    tgt = ops[0] if ops else ""
+                    if pending - entry.get(tgt, set()):
+                        entry[tgt] = entry.get(tgt, set()) | pending
+                        changed = True
+                    if op == "s_branch":
+                        live = False
+                elif op == "s_endpgm":
+                    live = False
+            if not changed:
+                break
+        bad += found
     return bad
 
 

@@ -14,7 +14,7 @@ from turtlevsr_amd.synthetic import synthetic_frames  # noqa: E402
 _, meta = load("clip_gopro_64")
 x = torch.from_numpy(synthetic_frames((1, 2, 3, 256, 256), 23)).cuda()
 ALL0 = {"fuse": 0, "panel_gemm": 0, "dw_rows": 0, "gemm_lds": 0, "gemm_pn": 0,
-        "sab_mfma": 0, "stem_mfma": 0, "blaslt": 0}
+        "sab_mfma": 0, "stem_mfma": 0}
 for opts in ({}, ALL0):
     m = TurtleHIP(meta["opt"], dtype="bf16")
     m.load_state_dict(synth_sd({k: tuple(v.shape) for k, v in m.state_dict().items()}, meta["seed"]))

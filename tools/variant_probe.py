@@ -15,7 +15,7 @@ from turtlevsr_amd.model import TurtleHIP  # noqa: E402
 from turtlevsr_amd.synthetic import synthetic_frames  # noqa: E402
 
 BASE = {"fuse": 0, "fused2": 0, "panel_gemm": 0, "dw_rows": 0, "gemm_lds": 0, "gemm_pn": 0,
-        "sab_mfma": 0, "stem_mfma": 0, "blaslt": 0, "gemm_ar": 0, "gemm_kt": 0, "dwgemm": 0,
+        "sab_mfma": 0, "stem_mfma": 0, "gemm_ar": 0, "gemm_kt": 0, "dwgemm": 0,
         "dwgemm_min_blocks": 0, "ffn": 0, "down_tile": 0}
 
 

@@ -18,7 +18,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "lib", "libturtle_hip.so")
-SOURCES = ["gemm.hip", "gemm2.hip", "gemm3.hip", "gemm5.hip", "spatial.hip", "attn.hip", "sab.hip", "fused.hip", "fused2.hip", "dwgemm.hip", "tilepd.hip", "gemm8.hip", "gemm9.hip", "ffn.hip", "t0.hip", "train_ops.hip", "blas.cpp", "turtle.cpp"]
+SOURCES = ["gemm.hip", "gemm2.hip", "gemm3.hip", "gemm5.hip", "spatial.hip", "attn.hip", "sab.hip", "fused.hip", "fused2.hip", "dwgemm.hip", "tilepd.hip", "gemm8.hip", "gemm9.hip", "ffn.hip", "t0.hip", "train_ops.hip", "turtle.cpp"]
 ARCH = os.environ.get("TURTLE_OFFLOAD_ARCH", "gfx950")
 
 
@@ -54,8 +54,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), SOURCES))
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
-        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + [
-            "-L", "/opt/rocm/lib", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"]
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-8000:]}")

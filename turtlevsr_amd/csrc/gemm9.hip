@@ -506,9 +506,10 @@ void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st) {
   int v = g.allow_g9;
   if (v == 1) {
     // 256 channels on the LDS-DMA ring wherever every CU still gets a tile (the A panel is read
-    // half as often; fastest on the latent shapes, tools/g9bench), else 128 register-staged
+    // half as often; fastest on the latent shapes, tools/g9bench), else - and for the K = 256, N = 256
+    // level-3 W_eff (47.8 vs 51.5 us, profiles/r05a_g9bench.log) - 128 register-staged
     const int64_t mt = g.wstride ? (g.M / g.HW) * ((g.HW + 255) / 256) : (g.M + 255) / 256;
-    v = g.N % 256 == 0 && mt * (g.N / 256) >= 256 ? 4 : 3;
+    v = g.N % 256 == 0 && mt * (g.N / 256) >= 256 && !(g.a.Ktot <= 256 && g.N <= 256) ? 4 : 3;
   }
   switch (v) {
     case 2: g9_launch<256, 0>(g, sp, st); break;

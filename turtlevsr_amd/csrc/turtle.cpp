@@ -324,15 +324,14 @@ struct TurtleHandle {
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
   int kt_max_px = 32768;                              // below this many pixels the 2-D tiled GEMM takes every shape it can
-  int blas_multi_img = 0;                             // 1: hipBLASLt also for multi-image W_eff (per-image calls)
   int sab_waves = 0;                                  // waves per SAB score block: 4 (64 queries), 8 (128), 0 = 8 at
                                                       // d >= 256, else 4 (tools/sabbench, profiles/r04_sabbench_waves.log)
   bool attn_fin = false;                              // channel-attention softmax rows inside the W_eff kernel (attn.hip)
   bool gemm8_ps = false;                              // ... in its persistent form (one block per CU walks its tiles)
-  int gemm8 = 3;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 in place of
-                                                      // hipBLASLt, 2 every eligible projection
-  int gemm9 = 0;                                      // four-wave 256 x 256 bf16 GEMM (gemm9.hip): 1 in place of
-                                                      // hipBLASLt, 2 on every eligible projection
+  int gemm8 = 3;                                      // 256 x 256 four-phase bf16 GEMM (gemm8.hip): 1 for the
+                                                      // 'wide' projection class (below), 2 every eligible projection
+  int gemm9 = 1;                                      // 256-pixel-row bf16 GEMM (gemm9.hip): 1 for the 'wide'
+                                                      // projection class (below), 2 every eligible projection, 0 off
   bool stem_mfma = true;                              // bf16 matrix-core stem / ending (spatial.hip)
   int sab_db = 0;                                     // SAB A.v: 0 two blocks / CU; 1 double-buffered, one block / CU;
                                                       // 2 two blocks / CU with the tail rows fetched a chunk ahead
@@ -350,9 +349,6 @@ struct TurtleHandle {
   bool split_out = true;                              // split-bf16 weights for reduce_chan_level1 (bf16 builds)
   bool dwgemm_attn = true;                            // channel attention: v's depthwise inside the W_eff GEMM (dwgemm.hip)
   int dwgemm_min_blocks = 384;                        // one 160 KB block per CU: below ~1.5 rounds (latent level) dw + GEMM is faster
-  bool blaslt = getenv("TURTLE_NO_BLASLT") == nullptr; // hipBLASLt for the plain projections it wins (blas.cpp)
-  BlasCtx* blas = nullptr;                            // created on the first bf16 forward
-  bool blas_failed = false;                           // creation failed once: never retried
   bool bf16() const { return arch.cfg.dtype == TURTLE_DTYPE_BF16; }
   const void* ptr(size_t off) const { return off == NONE ? nullptr : dev + off; }
   const float* fptr(size_t off) const { return reinterpret_cast<const float*>(ptr(off)); }
@@ -747,18 +743,10 @@ struct Runner {
             const void* res = nullptr, int64_t ldr = 0, int offr = 0, int gelu = 0,
             int store = STORE_NHWC, const void* wptr = nullptr, int64_t wstride = 0, int wdiv = 1,
             int N = -1, const float* bias = nullptr, int conv3 = 0, int cin = 0) {
-    // LN-folded projections with K >= 512 (latent level) may run as an explicit LayerNorm pass +
-    // hipBLASLt: their normalised rows need workspace (sized in the dry run as well)
-    // (the workspace test is shape-only, so sizing - which runs without packed weights - and every
-    // switch setting reserve the same bytes; <= 32 Mi elements keeps it to the latent level at 1080p)
-    const bool ln_ws = ES == 2 && a.n == 1 && !conv3 && !gelu && store == STORE_NHWC && a.Ktot >= 512 &&
-                       a.Ktot <= 64 * 8 * 4 && a.Ktot % 8 == 0 && M * a.Ktot <= ((int64_t)32 << 20);
-    T* xn = ln_ws ? buf(M * a.Ktot) : nullptr;
-    // per-pixel LayerNorm statistics of the four-wave GEMM (gemm9.hip; shape-only, as above)
+    // per-pixel LayerNorm statistics of the gemm9 kernel (gemm9.hip): workspace reserved by shape only,
+    // so sizing - which runs without packed weights - and every switch setting reserve the same bytes
     const bool g9_ws = ES == 2 && w.ln && a.n == 1 && !conv3 && (a.Ktot == 256 || a.Ktot == 512 || a.Ktot == 1024);
     float* st9 = g9_ws ? fbuf(2 * M) : nullptr;
-    const bool ln_cand = ln_ws && h->blaslt && w.ln && w.scale == NONE && a.s[0].img_mul == 1 &&
-                         a.s[0].img_add == 0 && !wptr && !bias && w.tb != NONE;
     if (dry()) return;
     GemmArgs g{};
     g.a = a; g.M = M; g.N = N >= 0 ? N : w.N; g.HW = HW; g.Wimg = Wimg;
@@ -784,13 +772,9 @@ struct Runner {
     const double Ka = conv3 ? cin : a.Ktot;
     const double nset = wstride ? (double)(M / HW) / wdiv : 1.0;
     const double bytes = ES * ((double)M * Ka + nset * g.N * a.Ktot + (double)M * g.N * (res ? 2 : 1));
-    GemmArgs gl = g;   // vendor form of an LN GEMM: operand = normalised rows, bias = W b_ln + bias
-    if (ln_cand) {
-      gl.a = src1(xn, a.Ktot, 0, a.Ktot); gl.ln = 0; gl.ln_s = gl.ln_t = nullptr; gl.bias = h->fptr(w.tb);
-    }
-    bool lt = ln_cand ? use_blas(gl) : use_blas(g);
+    bool lt = wide_class(g);
     if (ES == 2 && h->gemm8) {
-      // 1: in place of hipBLASLt, 2: every eligible projection, 3: the K-concatenated multi-source
+      // 1: the wide class, 2: every eligible projection, 3: the K-concatenated multi-source
       // projections with K >= 1024 (the FHR / CHM W_eff GEMMs, where it measures ~7-10 % faster than
       // the 2-D tiled kernel: profiles/r04_g8bench.log; elsewhere hipBLASLt / pn / kt stay faster)
       g.allow_g8 = h->gemm8_ps ? 2 : 1;           // 2: the persistent form (gemm8.hip)
@@ -801,69 +785,40 @@ struct Runner {
       if (gemm8_ok(g) && pick) lt = false;
       else g.allow_g8 = 0;
     }
-    // 256-row-tile GEMM (gemm9.hip): 1 in place of hipBLASLt - gemm9 for the latent-level shapes
-    // (<= 65536 pixels), the in-tree dispatcher (ar / pn / kt) for the larger ones -, 2 every
-    // eligible bf16 projection
+    // 256-pixel-row GEMM (gemm9.hip): 1 the wide class over <= 65536 pixels (the latent level; above
+    // it the ar / kt kernels measure faster in the frame: level-3 W_eff 57 vs 64 us,
+    // profiles/r05d_1080p_launch_report.txt), 2 every eligible projection
     bool use9 = false;
-    if (ES == 2 && h->gemm9 && (h->gemm9 == 2 || lt)) {
+    if (ES == 2 && h->gemm9 && (h->gemm9 == 2 || (lt && M <= 65536))) {
       GemmArgs t9 = g;
       t9.allow_g9 = 1;
-      lt = false;
-      if ((h->gemm9 == 2 || M <= 65536) && gemm9_ok(t9) && (!g.ln || st9)) {
+      if (gemm9_ok(t9) && (!g.ln || st9)) {
         use9 = true;
         g.allow_g8 = 0;
         g.allow_g9 = 1;
       }
     }
     tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s%s%s%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
-        res != nullptr, store, a.n, a.cb_px ? " cb" : "", lt ? " lt" : "", g.allow_g8 ? " g8" : "", use9 ? " g9" : "");
-    launch(TURTLE_K_GEMM, bytes + (ln_cand && lt ? 2.0 * ES * M * a.Ktot : 0.0), 2.0 * M * g.N * a.Ktot, [&] {
-      if (use9) {
-        launch_gemm9(g, st9, st);
-      } else if (lt && ln_cand) {
-        LnRowsArgs la{a.s[0].base, a.s[0].ld, a.s[0].off, xn, a.Ktot, M, a.Ktot, h->arch.cfg.layernorm_biasfree ? 0 : 1};
-        launch_ln_rows<T>(la, st);
-        run_blas(gl);
-      } else if (lt) {
-        run_blas(g);
-      } else {
-        launch_gemm<T>(g, st);
-      }
+        res != nullptr, store, a.n, a.cb_px ? " cb" : "", lt ? " wide" : "", g.allow_g8 ? " g8" : "", use9 ? " g9" : "");
+    launch(TURTLE_K_GEMM, bytes, 2.0 * M * g.N * a.Ktot, [&] {
+      if (use9) launch_gemm9(g, st9, st);
+      else launch_gemm<T>(g, st);
     });
   }
-  // plain bf16 projections where hipBLASLt beats the in-tree kernels (measured, blas.cpp): no LN
-  // prologue, activation, scale, 3x3 or multi-source operand; K >= 512, or <= 140k pixels x >= 256
-  // output channels. Per-image weight sets (W_eff) run one call per image.
-  bool use_blas(const GemmArgs& g) {
-    if (ES != 2 || !h->blaslt || g.a.cb_px || g.conv3 || g.ln || g.gelu || g.scale || g.store_mode != STORE_NHWC || g.a.n != 1)
-      return false;
+  // The 'wide' projection class: single-source bf16 projections, NHWC stores, no activation or
+  // scale, K >= 512 or (<= 140k pixels per weight set and >= 256 output channels) - the latent-level
+  // LN projections (qkv, GatedFFN project_in), project_out (K = 1280), the latent / level-3 W_eff
+  // GEMMs. Until round 4 these ran on hipBLASLt (measured faster than the ar / pn / kt kernels,
+  // DESIGN.md §3.4); gemm9 takes them in-tree. Multi-image per-image weight sets stay on the 2-D
+  // tiled kernel (one launch over all images, profiles/r04_256_b8_launch_report*.txt).
+  bool wide_class(const GemmArgs& g) const {
+    if (ES != 2 || g.a.cb_px || g.conv3 || g.gelu || g.scale || g.store_mode != STORE_NHWC || g.a.n != 1) return false;
     const SrcDesc& s = g.a.s[0];
     if (s.img_mul != 1 || s.img_add != 0 || s.K != g.a.Ktot) return false;
-    if (g.wstride && (g.HW <= 0 || g.M % g.HW || g.wstride % 8)) return false;
-    // per-image weight sets (W_eff) over several images: one hipBLASLt call per image (8 launches at
-    // 256x256 B = 8: 58 us per site) against one 2-D tiled launch over all of them
-    if (g.wstride && g.M / g.HW > 1 && h->blas_multi_img == 0) return false;
+    if (g.wstride && (g.HW <= 0 || g.M % g.HW || g.M / g.HW > 1)) return false;
+    if (g.ln && g.a.Ktot < 512) return false;     // the pn kernel's LN projections (levels 1-3)
     const int64_t Mi = g.wstride ? g.HW : g.M;
-    const int K = g.a.Ktot;
-    if (!(K >= 512 || (Mi <= 140000 && g.N >= 256))) return false;
-    if (s.ld % 8 || s.off % 8 || g.ldo % 8 || g.offo % 8 || g.ldw % 8 || K % 8 || g.N % 8) return false;
-    if (g.res && (g.ldr % 8 || g.offr % 8)) return false;
-    if (h->blas_failed) return false;
-    if (!h->blas) h->blas = blas_create();
-    if (!h->blas) { h->blas_failed = true; return false; }
-    return blas_ready(h->blas, Mi, g.N, K, s.ld, g.ldw, g.res ? g.ldr : 0, g.ldo, g.res != nullptr, g.bias != nullptr);
-  }
-  void run_blas(const GemmArgs& g) {
-    const SrcDesc& s = g.a.s[0];
-    const int64_t nimg = g.wstride ? g.M / g.HW : 1, Mi = g.wstride ? g.HW : g.M;
-    for (int64_t i = 0; i < nimg; ++i) {
-      const T* X = reinterpret_cast<const T*>(s.base) + s.off + i * Mi * s.ld;
-      const T* Wp = reinterpret_cast<const T*>(g.w) + (g.wstride ? (i / g.wdiv) * g.wstride : 0);
-      const T* Cp = g.res ? reinterpret_cast<const T*>(g.res) + g.offr + i * Mi * g.ldr : nullptr;
-      T* D = reinterpret_cast<T*>(g.out) + g.offo + i * Mi * g.ldo;
-      if (!blas_gemm_bf16(h->blas, Mi, g.N, g.a.Ktot, X, s.ld, Wp, g.ldw, g.bias, Cp, g.ldr, D, g.ldo, st))
-        TFAIL(TURTLE_EHIP, "hipBLASLt matmul failed");
-    }
+    return g.a.Ktot >= 512 || (Mi <= 140000 && g.N >= 256);
   }
   void dw(const DwW& w, const void* in, int64_t ldi, int offi, void* out, int64_t ldo, int offo,
           int nimg, int H, int Wd, int mode, int tok_ws = 0, int64_t tok_stride = 0) {
@@ -1632,7 +1587,6 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "fuse_fp32") h->fuse_fp32 = value != 0;
     else if (n == "panel_gemm") h->panel = value != 0;
     else if (n == "dw_rows") h->dw_rows = value != 0;
-    else if (n == "blaslt") h->blaslt = value != 0;
     else if (n == "dwgemm") h->dwgemm = value != 0;
     else if (n == "dwgemm_attn") h->dwgemm_attn = value != 0;
     else if (n == "dwgemm_cb") h->dwgemm_cb = value != 0;
@@ -1657,7 +1611,6 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm9") h->gemm9 = (int)value;
     else if (n == "attn_fin") h->attn_fin = value != 0;
     else if (n == "sab_waves") h->sab_waves = (int)value;
-    else if (n == "blas_multi_img") h->blas_multi_img = (int)value;
     else if (n == "kt_max_px") h->kt_max_px = (int)value;
     else if (n == "sab_mfma") h->sab_mfma = value != 0;
     else if (n == "stem_mfma") h->stem_mfma = value != 0;
@@ -1685,7 +1638,6 @@ void turtle_destroy(TurtleHandle* h) {
   if (!h) return;
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->dev) (void)hipFree(h->dev);
-  blas_destroy(h->blas);
   delete h;
 }
 

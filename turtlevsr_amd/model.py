@@ -329,7 +329,7 @@ class TurtleHIP(TrainGraph, TurtleParams):
 
     # ---------------------------------------------------------------------------------------
     def set_option(self, name: str, value: int):
-        """Kernel-selection switch (turtle_set_option): 'fuse', 'panel_gemm', 'gemm_lds', 'sab_mfma', 'stem_mfma', 'dw_rows', 'blaslt', .... Same results."""
+        """Kernel-selection switch (turtle_set_option): 'fuse', 'panel_gemm', 'gemm_lds', 'sab_mfma', 'stem_mfma', 'dw_rows', 'gemm9', .... Same results."""
         if self._handle is None or self._sig is None:
             self.refresh_weights()
         _lib.check(_lib.lib().turtle_set_option(self._handle.h, name.encode(), int(value)))
