@@ -45,6 +45,26 @@ int turtle_train_gate_fwd(const void* x, int64_t ldx, void* y, int64_t ldy, int6
 int turtle_train_gate_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx, int64_t P, int h,
                           int dtype, void* stream);
 
+/* plain GELU (exact erf form; FeedForward's conv4 activation turtle_t1_arch.py:181-210, ReducedAttn's
+ * after conv2 704-742): y [P][ldy] = gelu(x) over C channels; backward dx = dy * gelu'(x). Replaces
+ * torch.nn.functional.gelu in the training graph. */
+int turtle_train_gelu_fwd(const void* x, int64_t ldx, void* y, int64_t ldy, int64_t P, int C, int dtype, void* stream);
+int turtle_train_gelu_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx, int64_t P, int C,
+                          int dtype, void* stream);
+
+/* SAB window convolution nn.Conv2d(C, C, ws, stride=ws, padding=1, groups=C) (k2_dwconv / q2_dwconv,
+ * turtle_t1_arch.py:306-308 and their use in StateAlignBlock.forward 560-571) on NHWC rows:
+ * x [N][H][W][ldx] -> y [N][th][tw][ldy], th = (H + 2 - ws) / ws + 1 (tw likewise); wt fp32 [ws*ws][C] (the
+ * weight [C][1][ws][ws] transposed tap-major), b [C] or NULL. dgrad: dx [N][H][W][lddx] from dy (input
+ * pixels no token covers get 0). wgrad: dwt [ws*ws][C] fp32 += (caller zeroes it); the bias gradient is
+ * turtle_train_colsum over dy. Replaces MIOpen's grouped convolution (forward and both backward passes). */
+int turtle_train_window_fwd(const void* x, int64_t ldx, const float* wt, const float* b, void* y, int64_t ldy, int64_t N, int C,
+                            int H, int W, int ws, int th, int tw, int dtype, void* stream);
+int turtle_train_window_dgrad(const void* dy, int64_t lddy, const float* wt, void* dx, int64_t lddx, int64_t N, int C, int H, int W,
+                              int ws, int th, int tw, int dtype, void* stream);
+int turtle_train_window_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* dwt, int64_t N, int C, int H, int W,
+                              int ws, int th, int tw, int dtype, void* stream);
+
 /* column sums db[n] += sum_p dy[p][n] (a 1x1 convolution's bias gradient), N % 8 == 0 */
 int turtle_train_colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, int dtype, void* stream);
 /* per-image column sums of squares (the channel-attention L2 norms over HW, turtle_t1_arch.py:690-691):
@@ -75,6 +95,18 @@ int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride
 size_t turtle_train_rgemm_workspace(int64_t P, int N, int K, int64_t img_px);
 int turtle_train_rgemm(const void* a, int64_t lda, const void* b, int64_t ldb, float* c, int64_t P, int N, int K, int64_t img_px,
                        int accumulate, int dtype, void* ws, size_t ws_bytes, void* stream);
+
+/* dense 3x3 convolution, stride 1, padding 1, on NHWC rows (Down / Upsample body[0] 3x3 convolutions,
+ * turtle_t1_arch.py:136-154): y [P][ldy] = conv3x3(x) (+ bias), w [N][9][Cin] in the activation dtype
+ * (tap = 3 ky + kx), bias fp32 [N] or NULL; Cin % 8 == N % 8 == 0. The inference implicit-GEMM family.
+ * The input gradient is the same call on dy with w'[ci][tap][n] = w[n][8 - tap][ci]. */
+int turtle_train_conv3x3(const void* x, int64_t ldx, const void* w, const float* bias, void* y, int64_t ldy, int64_t B, int H,
+                         int W, int Cin, int N, int dtype, void* stream);
+/* its weight gradient: dw fp32 [9][N][Cin] = sum_p dy[p][n] x[p + off(tap)][ci] (zero padding), deterministic;
+ * needs turtle_train_conv3x3_wgrad_workspace(B * H * W, N, Cin) bytes of workspace */
+size_t turtle_train_conv3x3_wgrad_workspace(int64_t P, int N, int Cin);
+int turtle_train_conv3x3_wgrad(const void* dy, int64_t lddy, const void* x, int64_t ldx, float* dw, int64_t B, int H, int W, int N,
+                               int Cin, int dtype, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

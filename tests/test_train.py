@@ -308,6 +308,64 @@ def test_hip_train_ops_match_autograd(dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_hip_gelu_window_conv3x3_match_autograd(dtype):
+    """The plain GELU and the SAB window convolution (ws x ws, stride ws, padding 1, one group per
+    channel: turtle_t1_arch.py:306-308) on the HIP kernels against torch autograd: outputs, input,
+    weight and bias gradients, at the config-5 window shapes (ws 8 and 16), ragged maps and a map
+    whose last row / column no window covers."""
+    from turtlevsr_amd.train_ops import HipOps
+    torch.manual_seed(1)
+    dev = "cuda"
+    tol = dict(rtol=1e-4, atol=1e-5) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    x = (torch.randn(2, 48, 9, 13, device=dev) * 2).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    gy = torch.randn(2, 48, 9, 13, device=dev).to(dtype)
+    y = HipOps.gelu(x)
+    (gx,) = torch.autograd.grad(y, [x], gy)
+    x2 = x.detach().float().requires_grad_()
+    y2 = torch.nn.functional.gelu(x2)
+    (rx,) = torch.autograd.grad(y2, [x2], gy.float())
+    torch.testing.assert_close(y.float(), y2, **tol)
+    torch.testing.assert_close(gx.float(), rx, **tol)
+    for (B, C, H, W, ws) in [(2, 128, 64, 64, 16), (2, 64, 40, 48, 8), (1, 16, 17, 23, 4), (3, 8, 8, 8, 8)]:
+        x = torch.randn(B, C, H, W, device=dev).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+        w = (0.2 * torch.randn(C, 1, ws, ws, device=dev)).requires_grad_()
+        b = (0.1 * torch.randn(C, device=dev)).requires_grad_()
+        y = HipOps.window_conv(x, w, b, ws)
+        gy = torch.randn(y.shape, device=dev).to(dtype)
+        gx, gw, gb = torch.autograd.grad(y, [x, w, b], gy)
+        x2, w2, b2 = (t.detach().float().requires_grad_() for t in (x, w, b))
+        y2 = torch.nn.functional.conv2d(x2, w2, b2, stride=ws, padding=1, groups=C)
+        rx, rw, rb = torch.autograd.grad(y2, [x2, w2, b2], gy.float())
+        assert y.shape == y2.shape
+        torch.testing.assert_close(y.float(), y2, rtol=tol["rtol"], atol=tol["atol"] * 10)
+        torch.testing.assert_close(gx.float(), rx, **tol)
+        scale = float(rw.abs().max())
+        torch.testing.assert_close(gw, rw, rtol=tol["rtol"] * 10, atol=tol["atol"] * 10 * max(scale, 1.0))
+        torch.testing.assert_close(gb, rb, rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
+    # Down / Upsample 3x3 convolutions (bias-free in the reference; a bias checked too)
+    for (B, Cin, N, H, W, bias) in [(2, 64, 32, 20, 24, False), (1, 128, 256, 16, 8, False), (2, 24, 40, 9, 13, True),
+                                    (1, 512, 1024, 4, 6, False)]:
+        x = torch.randn(B, Cin, H, W, device=dev).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+        w = (torch.randn(N, Cin, 3, 3, device=dev) / (3 * Cin ** 0.5)).requires_grad_()
+        b = (0.1 * torch.randn(N, device=dev)).requires_grad_() if bias else None
+        y = HipOps.conv3x3(x, w, b)
+        gy = torch.randn(y.shape, device=dev).to(dtype)
+        gs = torch.autograd.grad(y, [x, w] + ([b] if bias else []), gy)
+        x2, w2 = x.detach().float().requires_grad_(), w.detach().requires_grad_()
+        b2 = b.detach().requires_grad_() if bias else None
+        y2 = torch.nn.functional.conv2d(x2, w2, b2, 1, 1)
+        rs = torch.autograd.grad(y2, [x2, w2] + ([b2] if bias else []), gy.float())
+        ctol = dict(rtol=tol["rtol"], atol=tol["atol"] * 3)
+        torch.testing.assert_close(y.float(), y2, **ctol)
+        torch.testing.assert_close(gs[0].float(), rs[0], **ctol)
+        scale = float(rs[1].abs().max())
+        torch.testing.assert_close(gs[1], rs[1], rtol=tol["rtol"] * 10, atol=tol["atol"] * 10 * max(scale, 1.0))
+        if bias:
+            torch.testing.assert_close(gs[2], rs[2], rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["train_tiny", "train_tiny_hetero", "train_gopro"])
 def test_hip_training_graph_matches_reference_gradients(name):
     """fp32 on the GPU with the HIP kernels: loss and every parameter gradient vs the reference

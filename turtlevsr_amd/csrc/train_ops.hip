@@ -441,6 +441,158 @@ __global__ __launch_bounds__(256) void gate_bwd_kernel(const T* __restrict__ x, 
   st8f(dx + p * lddx + h + c, o2);
 }
 
+// plain GELU (exact erf form; FeedForward 181-210 after conv4, ReducedAttn 704-742 after conv2):
+// y = gelu(x); backward dx = dy gelu'(x)
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const T* __restrict__ x, int64_t ldx, T* __restrict__ y, int64_t ldy,
+                                                       int64_t P, int C) {
+  const int nch = C / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P * nch) return;
+  const int64_t p = gid / nch;
+  const int c = 8 * (int)(gid % nch);
+  float a[8], o[8];
+  ld8f(x + p * ldx + c, a);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = gelu_exact(a[e]);
+  st8f(y + p * ldy + c, o);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy, int64_t lddy,
+                                                       T* __restrict__ dx, int64_t lddx, int64_t P, int C) {
+  const int nch = C / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P * nch) return;
+  const int64_t p = gid / nch;
+  const int c = 8 * (int)(gid % nch);
+  float a[8], g[8], o[8];
+  ld8f(x + p * ldx + c, a);
+  ld8f(dy + p * lddy + c, g);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = g[e] * gelu_exact_grad(a[e]);
+  st8f(dx + p * lddx + c, o);
+}
+
+// ---------------------------------------------------------------------------------------------
+// SAB window convolution (k2_dwconv / q2_dwconv, turtle_t1_arch.py:306-308, 560-571):
+// nn.Conv2d(C, C, ws, stride=ws, padding=1, groups=C) on NHWC rows. Token (i, j) of the th x tw
+// output grid covers input rows i ws - 1 .. i ws + ws - 2 and columns j ws - 1 .. (zero padding
+// outside; the last input rows / columns past the grid are not read). Weights transposed on the
+// host to wt [ws*ws][C] fp32 (tap-major: 8 channels of a tap are one 32-byte read).
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void win_fwd_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ wt,
+                                                      const float* __restrict__ b, T* __restrict__ y, int64_t ldy, int64_t N,
+                                                      int C, int H, int W, int ws, int th, int tw) {
+  const int nch = C / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= N * th * tw * nch) return;
+  const int c = 8 * (int)(gid % nch);
+  const int64_t t = gid / nch;                     // token row of y: (img, i, j)
+  const int j = (int)(t % tw), i = (int)((t / tw) % th);
+  const int64_t img = t / ((int64_t)tw * th);
+  float acc[8];
+  if (b) {
+    const float4 b0 = *reinterpret_cast<const float4*>(b + c), b1 = *reinterpret_cast<const float4*>(b + c + 4);
+    acc[0] = b0.x; acc[1] = b0.y; acc[2] = b0.z; acc[3] = b0.w; acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  }
+  const int y0 = i * ws - 1, x0 = j * ws - 1;
+  for (int u = 0; u < ws; ++u) {
+    const int yy = y0 + u;
+    if (yy < 0 || yy >= H) continue;
+    const T* row = x + ((img * H + yy) * W) * ldx + c;
+    for (int v = 0; v < ws; ++v) {
+      const int xx = x0 + v;
+      if (xx < 0 || xx >= W) continue;
+      float a[8];
+      ld8f(row + (int64_t)xx * ldx, a);
+      const float* wp = wt + (int64_t)(u * ws + v) * C + c;
+      const float4 w0 = *reinterpret_cast<const float4*>(wp), w1 = *reinterpret_cast<const float4*>(wp + 4);
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf(a[e], wv[e], acc[e]);
+    }
+  }
+  st8f(y + t * ldy + c, acc);
+}
+// input gradient: every input pixel feeds exactly one token (or none): dx = dy[token] wt[tap]
+template <typename T>
+__global__ __launch_bounds__(256) void win_dgrad_kernel(const T* __restrict__ dy, int64_t lddy, const float* __restrict__ wt,
+                                                        T* __restrict__ dx, int64_t lddx, int64_t N, int C, int H, int W, int ws,
+                                                        int th, int tw) {
+  const int nch = C / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= N * H * W * nch) return;
+  const int c = 8 * (int)(gid % nch);
+  const int64_t p = gid / nch;
+  const int xx = (int)(p % W), yy = (int)((p / W) % H);
+  const int64_t img = p / ((int64_t)W * H);
+  const int i = (yy + 1) / ws, u = (yy + 1) - i * ws, j = (xx + 1) / ws, v = (xx + 1) - j * ws;
+  float o[8];
+  if (i < th && j < tw) {
+    float g[8];
+    ld8f(dy + ((img * th + i) * tw + j) * lddy + c, g);
+    const float* wp = wt + (int64_t)(u * ws + v) * C + c;
+    const float4 w0 = *reinterpret_cast<const float4*>(wp), w1 = *reinterpret_cast<const float4*>(wp + 4);
+    const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = g[e] * wv[e];
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
+  }
+  st8f(dx + p * lddx + c, o);
+}
+// weight gradient dwt[tap][c] += sum over (img, token) of dy[token][c] x[pixel(token, tap)][c]: block
+// = (tap, 64-channel chunk, token split); thread = (token lane 0..31, channel vector 0..7); token-lane
+// partials reduced by shuffles inside a wave and through LDS across the 4 waves, one fp32 atomic
+// add per (tap, channel) and block into the caller-zeroed dwt
+template <typename T>
+__global__ __launch_bounds__(256) void win_wgrad_kernel(const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy,
+                                                        int64_t lddy, float* __restrict__ dwt, int64_t N, int C, int H, int W,
+                                                        int ws, int th, int tw, int64_t tpb) {
+  __shared__ float red[4][64];
+  const int tap = blockIdx.x, u = tap / ws, v = tap - u * ws;
+  const int cv = threadIdx.x & 7, tl = threadIdx.x >> 3;         // channel vector, token lane (0..31)
+  const int c = blockIdx.y * 64 + cv * 8;
+  const int64_t ntok = N * th * tw;
+  const int64_t t0 = (int64_t)blockIdx.z * tpb, t1 = min(ntok, t0 + tpb);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    for (int64_t t = t0 + tl; t < t1; t += 32) {
+      const int j = (int)(t % tw), i = (int)((t / tw) % th);
+      const int64_t img = t / ((int64_t)tw * th);
+      const int yy = i * ws - 1 + u, xx = j * ws - 1 + v;
+      if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
+      float a[8], g[8];
+      ld8f(x + ((img * H + yy) * W + xx) * ldx + c, a);
+      ld8f(dy + t * lddy + c, g);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf(a[e], g[e], acc[e]);
+    }
+  }
+  // token lanes tl and tl ^ 1, ^ 2, ^ 4 share a wave (lane = 8 tl + cv): xor 8, 16, 32
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    acc[e] += __shfl_xor(acc[e], 8, 64);
+    acc[e] += __shfl_xor(acc[e], 16, 64);
+    acc[e] += __shfl_xor(acc[e], 32, 64);
+  }
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane < 8)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[wv][lane * 8 + e] = acc[e];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int cc = blockIdx.y * 64 + threadIdx.x;
+    const float s = (red[0][threadIdx.x] + red[1][threadIdx.x]) + (red[2][threadIdx.x] + red[3][threadIdx.x]);
+    if (cc < C) atomicAdd(dwt + (int64_t)tap * C + cc, s);
+  }
+}
+
 // column sums db[n] = sum_p dy[p][n] (8 channels per thread, pixel lanes, LDS reduction, atomics)
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, int64_t ld, float* __restrict__ db, int64_t P,
@@ -523,9 +675,12 @@ TURTLE_DEV uint2 ds_read_tr16(const char* lds_ptr) {
   return r;
 }
 
+// shW > 0 (3x3 convolution weight gradient, img_px = 0): blockIdx.y = tap t of a 3x3 stencil
+// (dy, dx) = (t / 3 - 1, t % 3 - 1), B's pixel p read at (y + dy, x + dx) of its shH x shW image (zero
+// outside): part[split][t] = sum_p A[p] B[p + shift(t)]^T
 __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B,
                                                          int64_t ldb, float* __restrict__ part, int64_t img_px, int nimg_out,
-                                                         int N, int K, int64_t P, int64_t ppb) {
+                                                         int N, int K, int64_t P, int64_t ppb, int shH = 0, int shW = 0) {
   typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
   // two stage buffers: the global loads of stage s + 1 are in flight (in registers) while the
   // MFMAs of stage s read the other buffer; one barrier per stage
@@ -541,6 +696,7 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
   const int64_t plen = img_px > 0 ? img_px : P;
   const int64_t p0 = (int64_t)split * ppb, p1 = min(plen, p0 + ppb);
   const int wn = wid >> 1, wk = wid & 1;
+  const int sdy = img / 3 - 1, sdx = img % 3 - 1;   // (tap mode only)
   f32x4 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -559,22 +715,30 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
     pb_[u] = B + pbase * ldb + min(k0 + 8 * (sch + u), K - 8);
   }
   uint4 ra[2], rb[2];
-  uint32_t live_mask = 0;
+  uint32_t live_mask = 0, b_mask = 0;
   auto gload = [&](int64_t pbk) {
     const int64_t p = pbk + srow;
     live_mask = p < p1 ? 0xffffffffu : 0u;
     const int64_t pc = p < p1 ? p : p1 - 1;
+    int64_t pcb = pc;
+    b_mask = live_mask;
+    if (shW > 0) {                                 // (uniform branch)
+      const int64_t xq = pc % shW, yq = (pc / shW) % shH;
+      const bool ok = yq + sdy >= 0 && yq + sdy < shH && xq + sdx >= 0 && xq + sdx < shW;
+      pcb = ok ? pc + (int64_t)sdy * shW + sdx : pc;
+      b_mask = ok ? live_mask : 0u;
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       ra[u] = *reinterpret_cast<const uint4*>(pa[u] + pc * lda);
-      rb[u] = *reinterpret_cast<const uint4*>(pb_[u] + pc * ldb);
+      rb[u] = *reinterpret_cast<const uint4*>(pb_[u] + pcb * ldb);
     }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const uint4 va = make_uint4(ra[u].x & live_mask, ra[u].y & live_mask, ra[u].z & live_mask, ra[u].w & live_mask);
-      const uint4 vb = make_uint4(rb[u].x & live_mask, rb[u].y & live_mask, rb[u].z & live_mask, rb[u].w & live_mask);
+      const uint4 vb = make_uint4(rb[u].x & b_mask, rb[u].y & b_mask, rb[u].z & b_mask, rb[u].w & b_mask);
       *reinterpret_cast<uint4*>(sA[buf] + srow * RG_PITCH + 16 * (sch + u)) = va;
       *reinterpret_cast<uint4*>(sB[buf] + srow * RG_PITCH + 16 * (sch + u)) = vb;
     }
@@ -639,7 +803,7 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
 
 __global__ __launch_bounds__(256) void rgemm_f32_kernel(const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
                                                         int64_t ldb, float* __restrict__ part, int64_t img_px, int nimg_out,
-                                                        int N, int K, int64_t P, int64_t ppb) {
+                                                        int N, int K, int64_t P, int64_t ppb, int shH = 0, int shW = 0) {
   __shared__ float sA[32][65], sB[32][65];
   const int tid = threadIdx.x;
   const int ntn = (N + 63) / 64, ntk = (K + 63) / 64;
@@ -651,13 +815,21 @@ __global__ __launch_bounds__(256) void rgemm_f32_kernel(const float* __restrict_
   const int64_t plen = img_px > 0 ? img_px : P;
   const int64_t p0 = (int64_t)split * ppb, p1 = min(plen, p0 + ppb);
   const int tn = tid >> 4, tk = tid & 15;          // 4 x 4 outputs per thread
+  const int sdy = img / 3 - 1, sdx = img % 3 - 1;   // (tap mode: shW > 0, see rgemm_bf16_kernel)
   float acc[4][4] = {};
   for (int64_t pb = p0; pb < p1; pb += 32) {
     for (int i = tid; i < 32 * 64; i += 256) {
       const int r = i / 64, cc = i % 64;
       const int64_t p = pb + r;
+      int64_t pbq = pbase + p;
+      bool bok = true;
+      if (shW > 0) {
+        const int64_t xq = p % shW, yq = (p / shW) % shH;
+        bok = yq + sdy >= 0 && yq + sdy < shH && xq + sdx >= 0 && xq + sdx < shW;
+        pbq = p + (int64_t)sdy * shW + sdx;
+      }
       sA[r][cc] = (p < p1 && n0 + cc < N) ? A[(pbase + p) * lda + n0 + cc] : 0.f;
-      sB[r][cc] = (p < p1 && k0 + cc < K) ? B[(pbase + p) * ldb + k0 + cc] : 0.f;
+      sB[r][cc] = (p < p1 && bok && k0 + cc < K) ? B[pbq * ldb + k0 + cc] : 0.f;
     }
     __syncthreads();
     for (int r = 0; r < 32; ++r)
@@ -799,6 +971,49 @@ int gate_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx,
   return 0;
 }
 template <typename T>
+int gelu_fwd(const void* x, int64_t ldx, void* y, int64_t ldy, int64_t P, int C, hipStream_t st) {
+  const int64_t tot = P * (C / 8);
+  hipLaunchKernelGGL(gelu_fwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, ldx, (T*)y, ldy, P, C);
+  return 0;
+}
+template <typename T>
+int gelu_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx, int64_t P, int C, hipStream_t st) {
+  const int64_t tot = P * (C / 8);
+  hipLaunchKernelGGL(gelu_bwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, ldx, (const T*)dy,
+                     lddy, (T*)dx, lddx, P, C);
+  return 0;
+}
+template <typename T>
+int win_fwd(const void* x, int64_t ldx, const float* wt, const float* b, void* y, int64_t ldy, int64_t N, int C, int H, int W,
+            int ws, int th, int tw, hipStream_t st) {
+  const int64_t tot = N * th * tw * (C / 8);
+  hipLaunchKernelGGL(win_fwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, ldx, wt, b, (T*)y, ldy,
+                     N, C, H, W, ws, th, tw);
+  return 0;
+}
+template <typename T>
+int win_dgrad(const void* dy, int64_t lddy, const float* wt, void* dx, int64_t lddx, int64_t N, int C, int H, int W, int ws, int th,
+              int tw, hipStream_t st) {
+  const int64_t tot = N * H * W * (C / 8);
+  hipLaunchKernelGGL(win_dgrad_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)dy, lddy, wt, (T*)dx,
+                     lddx, N, C, H, W, ws, th, tw);
+  return 0;
+}
+template <typename T>
+int win_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* dwt, int64_t N, int C, int H, int W, int ws, int th,
+              int tw, hipStream_t st) {
+  const int64_t ntok = N * th * tw;
+  const int nchunk = (C + 63) / 64;
+  // token splits: ~2048 blocks in all, each split at least 64 tokens
+  int64_t nsplit = std::max<int64_t>(1, std::min<int64_t>((2048 + ws * ws * nchunk - 1) / (ws * ws * nchunk), ntok / 64));
+  nsplit = std::min<int64_t>(nsplit, 65535);
+  const int64_t tpb = (ntok + nsplit - 1) / nsplit;
+  nsplit = (ntok + tpb - 1) / tpb;
+  hipLaunchKernelGGL(win_wgrad_kernel<T>, dim3((unsigned)(ws * ws), (unsigned)nchunk, (unsigned)nsplit), dim3(256), 0, st,
+                     (const T*)x, ldx, (const T*)dy, lddy, dwt, N, C, H, W, ws, th, tw, tpb);
+  return 0;
+}
+template <typename T>
 int colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, hipStream_t st) {
   const int64_t blocks = std::min<int64_t>(1024, std::max<int64_t>(1, P / 256));
   const int64_t ppb = (P + blocks - 1) / blocks;
@@ -843,9 +1058,9 @@ static const float* train_consts(int which) {
   return which ? it->second + 16384 : it->second;
 }
 
-static int64_t rgemm_splits(int64_t P, int N, int K, int64_t img_px) {
+static int64_t rgemm_splits(int64_t P, int N, int K, int64_t img_px, int ntap = 1) {
   const int64_t plen = img_px > 0 ? img_px : P;
-  const int64_t nimg = img_px > 0 ? P / img_px : 1;
+  const int64_t nimg = (img_px > 0 ? P / img_px : 1) * ntap;
   const int64_t tiles = ((N + RG_BN - 1) / RG_BN) * ((K + RG_BK - 1) / RG_BK) * nimg;
   return std::max<int64_t>(1, std::min<int64_t>((1024 + tiles - 1) / tiles, (plen + 511) / 512));
 }
@@ -939,6 +1154,40 @@ int turtle_train_gate_bwd(const void* x, int64_t ldx, const void* dy, int64_t ld
   TT_DISPATCH(dtype, gate_bwd, x, ldx, dy, lddy, dx, lddx, P, h, (hipStream_t)stream);
 }
 
+int turtle_train_gelu_fwd(const void* x, int64_t ldx, void* y, int64_t ldy, int64_t P, int C, int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || P <= 0 || C <= 0 || C % 8 || ldx < C || ldy < C) return -1;
+  TT_DISPATCH(dtype, gelu_fwd, x, ldx, y, ldy, P, C, (hipStream_t)stream);
+}
+
+int turtle_train_gelu_bwd(const void* x, int64_t ldx, const void* dy, int64_t lddy, void* dx, int64_t lddx, int64_t P, int C,
+                          int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(dy, lddy, dtype) || !rows_ok(dx, lddx, dtype) || P <= 0 || C <= 0 || C % 8) return -1;
+  TT_DISPATCH(dtype, gelu_bwd, x, ldx, dy, lddy, dx, lddx, P, C, (hipStream_t)stream);
+}
+
+static bool win_ok(int64_t N, int C, int H, int W, int ws, int th, int tw) {
+  return N > 0 && C > 0 && C % 8 == 0 && H > 0 && W > 0 && ws > 0 && ws <= 64 && th > 0 && tw > 0 &&
+         th == (H + 2 - ws) / ws + 1 && tw == (W + 2 - ws) / ws + 1 && H + 2 >= ws && W + 2 >= ws;
+}
+
+int turtle_train_window_fwd(const void* x, int64_t ldx, const float* wt, const float* b, void* y, int64_t ldy, int64_t N, int C,
+                            int H, int W, int ws, int th, int tw, int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !wt || !win_ok(N, C, H, W, ws, th, tw)) return -1;
+  TT_DISPATCH(dtype, win_fwd, x, ldx, wt, b, y, ldy, N, C, H, W, ws, th, tw, (hipStream_t)stream);
+}
+
+int turtle_train_window_dgrad(const void* dy, int64_t lddy, const float* wt, void* dx, int64_t lddx, int64_t N, int C, int H, int W,
+                              int ws, int th, int tw, int dtype, void* stream) {
+  if (!rows_ok(dy, lddy, dtype) || !rows_ok(dx, lddx, dtype) || !wt || !win_ok(N, C, H, W, ws, th, tw)) return -1;
+  TT_DISPATCH(dtype, win_dgrad, dy, lddy, wt, dx, lddx, N, C, H, W, ws, th, tw, (hipStream_t)stream);
+}
+
+int turtle_train_window_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* dwt, int64_t N, int C, int H, int W,
+                              int ws, int th, int tw, int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(dy, lddy, dtype) || !dwt || !win_ok(N, C, H, W, ws, th, tw)) return -1;
+  TT_DISPATCH(dtype, win_wgrad, x, ldx, dy, lddy, dwt, N, C, H, W, ws, th, tw, (hipStream_t)stream);
+}
+
 int turtle_train_colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, int dtype, void* stream) {
   if (!rows_ok(dy, ld, dtype) || !db || P <= 0 || N <= 0 || N % 8 || N > 2048) return -1;
   TT_DISPATCH(dtype, colsum, dy, ld, db, P, N, (hipStream_t)stream);
@@ -979,6 +1228,74 @@ int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride
   } catch (...) {
     return -1;
   }
+  return (int)hipGetLastError();
+}
+
+/* dense 3x3 convolution, stride 1, padding 1 (Down / Upsample body[0], turtle_t1_arch.py:136-154):
+ * y[p][n] = sum_{tap, ci} x[p + off(tap)][ci] w[n][tap][ci] (+ bias[n]) on the inference implicit-GEMM
+ * family (GemmArgs.conv3: no im2col); the input gradient is the same call on dy with the rotated,
+ * transposed weights */
+int turtle_train_conv3x3(const void* x, int64_t ldx, const void* w, const float* bias, void* y, int64_t ldy, int64_t B, int H,
+                         int W, int Cin, int N, int dtype, void* stream) {
+  if (dtype != 0 && dtype != 1) return -1;
+  const int64_t P = B * H * W;
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !w || B <= 0 || H <= 0 || W <= 0 || Cin <= 0 || N <= 0 ||
+      Cin % 8 || N % 8 || ldx < Cin || ldy < N || (int64_t)H * W >= ((int64_t)1 << 31))
+    return -1;
+  GemmArgs g{};
+  g.a.n = 1; g.a.Ktot = 9 * Cin;
+  g.a.s[0] = SrcDesc{x, ldx, 0, 9 * Cin, 1, 0};
+  g.M = P; g.N = N; g.HW = H * W; g.Wimg = W;
+  g.conv3 = 1; g.cin = Cin;
+  g.w = w; g.ldw = 9 * Cin; g.wdiv = 1;
+  g.bias = bias; g.out = y; g.ldo = ldy; g.offo = 0; g.store_mode = STORE_NHWC;
+  g.zeros = train_consts(0); g.ones = train_consts(1);
+  if (!g.zeros) return (int)hipErrorOutOfMemory;
+  g.allow_panel = g.allow_lds = g.allow_pn = g.allow_ar = g.allow_kt = 1;
+  try {
+    if (dtype == 1) launch_gemm<bf16>(g, (hipStream_t)stream);
+    else launch_gemm<float>(g, (hipStream_t)stream);
+  } catch (...) {
+    return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+size_t turtle_train_conv3x3_wgrad_workspace(int64_t P, int N, int Cin) {
+  return (size_t)rgemm_splits(P, N, Cin, 0, 9) * 9 * N * Cin * sizeof(float);
+}
+
+/* its weight gradient dw[tap][n][ci] = sum_p dy[p][n] x[p + off(tap)][ci] (fp32 [9][N][Cin]): the reduction
+ * GEMM with its B operand read at the tap's shifted pixel (zero outside the image), one block row per
+ * tap; deterministic */
+int turtle_train_conv3x3_wgrad(const void* dy, int64_t lddy, const void* x, int64_t ldx, float* dw, int64_t B, int H, int W, int N,
+                               int Cin, int dtype, void* ws, size_t ws_bytes, void* stream) {
+  if (dtype != 0 && dtype != 1) return -1;
+  const int64_t P = B * H * W;
+  if (!rows_ok(dy, lddy, dtype) || !rows_ok(x, ldx, dtype) || !dw || B <= 0 || H <= 0 || W <= 0 || N <= 0 || Cin <= 0 || N % 8 ||
+      Cin % 8 || lddy < N || ldx < Cin)
+    return -1;
+  int64_t nsplit = rgemm_splits(P, N, Cin, 0, 9);
+  if (!ws || ws_bytes < (size_t)nsplit * 9 * N * Cin * sizeof(float)) return -1;
+  int64_t ppb = (P + nsplit - 1) / nsplit;
+  ppb = (ppb + RG_BP - 1) / RG_BP * RG_BP;
+  nsplit = (P + ppb - 1) / ppb;
+  hipStream_t st = (hipStream_t)stream;
+  float* part = reinterpret_cast<float*>(ws);
+  if (dtype == 1) {
+    const dim3 grid((unsigned)(((N + RG_BN - 1) / RG_BN) * ((Cin + RG_BK - 1) / RG_BK) * nsplit), 9u);
+    hipLaunchKernelGGL(rgemm_bf16_kernel, grid, dim3(256), 0, st, (const bf16*)dy, lddy, (const bf16*)x, ldx, part, (int64_t)0, 9,
+                       N, Cin, P, ppb, H, W);
+  } else {
+    const dim3 grid((unsigned)(((N + 63) / 64) * ((Cin + 63) / 64) * nsplit), 9u);
+    hipLaunchKernelGGL(rgemm_f32_kernel, grid, dim3(256), 0, st, (const float*)dy, lddy, (const float*)x, ldx, part, (int64_t)0, 9,
+                       N, Cin, P, ppb, H, W);
+  }
+  const int64_t n = 9 * (int64_t)N * Cin;
+  if ((n + 63) / 64 >= 512)
+    hipLaunchKernelGGL(rgemm_reduce_kernel<64>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, part, dw, n, (int)nsplit, 0);
+  else
+    hipLaunchKernelGGL(rgemm_reduce_kernel<16>, dim3((unsigned)((n + 15) / 16)), dim3(256), 0, st, part, dw, n, (int)nsplit, 0);
   return (int)hipGetLastError();
 }
 

@@ -6,11 +6,11 @@ base_model.py:340-365, dist_util.py:15-30) on the GPU:
 * ``TurtleTrain`` is the differentiable Turtle_t1 graph over the SAME parameter tree as the
   inference module (633 keys, turtlevsr_amd/params.py), so checkpoints move between training and
   the HIP inference path unchanged. On the GPU its LayerNorms, depthwise 3x3 convolutions, GELU
-  gates, pointwise 1x1 convolutions (forward, input and weight gradients) and the channel-attention
-  Gram run on hand-written HIP kernels with hand-written backward (``train_ops.HipOps``,
-  include/turtle_train.h), on channels-last activations; the dense / window 3x3 convolutions
-  (stem, ending, Down/Upsample, SAB q2/k2) and the SAB dense scores / top-5 / A.v are torch ops
-  (MIOpen / hipBLASLt), differentiated by autograd.
+  gates and plain GELUs, pointwise 1x1 convolutions (forward, input and weight gradients), the
+  channel-attention Gram, the Down / Upsample 3x3 convolutions and the SAB window convolutions run on
+  hand-written HIP kernels with hand-written backward (``train_ops.HipOps``, include/turtle_train.h),
+  on channels-last activations; the 3-channel stem / ending convolutions, the FHR / CHM attention with
+  its caches and the SAB dense scores / top-5 / A.v are torch ops, differentiated by autograd.
 * caches are NOT detached between frames: the loss of frame j back-propagates into frames < j
   through the history state (video_restoration_model.py:85-95);
 * ``Trainer.train_step``: zero_grad -> autocast forward over the T frames -> L1 per frame summed,
@@ -167,6 +167,14 @@ class TrainGraph:
         y = F.conv2d(_ToNCHW.apply(x) if cl else x.contiguous(), w, b, stride, padding, 1, groups)
         return y.contiguous(memory_format=torch.channels_last) if cl else y
 
+    def _conv3(self, x, w):
+        """Down / Upsample 3x3 convolution (bias-free, turtle_t1_arch.py:136-154): the op set's implicit-GEMM
+        kernel when it has one and the widths allow it, else F.conv2d."""
+        ops = self._ops()
+        if hasattr(ops, "conv3x3") and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0:
+            return ops.conv3x3(x, w)
+        return self._dense(x, w)
+
     def _c1(self, m, x):                            # nn.Conv2d(K, N, 1): the op set's GEMM when it has one
         ops = self._ops()
         if hasattr(ops, "conv1x1"):
@@ -189,11 +197,29 @@ class TrainGraph:
     def _gffw(self, m, x):                          # GatedFeedForward 159-178
         return self._c1(m.project_out, self._ops().gelu_gate(self._dw(m.dwconv, self._c1(m.project_in, x))))
 
+    def _gelu(self, x):
+        ops = self._ops()
+        return ops.gelu(x) if hasattr(ops, "gelu") else F.gelu(x)
+
     def _ffw(self, m, x):                           # FeedForward 181-210
-        return self._c1_scaled(m.conv5, F.gelu(self._c1(m.conv4, x)), m.gamma)
+        return self._c1_scaled(m.conv5, self._gelu(self._c1(m.conv4, x)), m.gamma)
 
     def _reduced(self, m, x):                       # ReducedAttn 704-742
-        return self._c1_scaled(m.conv3, F.gelu(self._dw(m.conv2, self._c1(m.conv1, x))), m.beta)
+        return self._c1_scaled(m.conv3, self._gelu(self._dw(m.conv2, self._c1(m.conv1, x))), m.beta)
+
+    def _window(self, x, conv, ws, g):
+        """SAB window convolution (k2_dwconv / q2_dwconv: ws x ws, stride ws, padding 1, groups = channels;
+        turtle_t1_arch.py:306-308) -> tokens [b, 1, 1, n, g]: on the op set's kernel when it has one
+        (channels-last output, whose [b, n, g] view is free), else F.conv2d."""
+        ops = self._ops()
+        b = x.shape[0]
+        if hasattr(ops, "window_conv"):
+            y = ops.window_conv(x, conv.weight, conv.bias, ws)
+            th, tw = y.shape[2], y.shape[3]
+            return y.permute(0, 2, 3, 1).reshape(b, 1, 1, th * tw, g), th, tw
+        y = self._dense(x, conv.weight, conv.bias, ws, 1, g)
+        th, tw = y.shape[2], y.shape[3]
+        return y.reshape(b, g, th * tw).transpose(1, 2).reshape(b, 1, 1, th * tw, g), th, tw
 
     @staticmethod
     def _heads(t, heads):
@@ -277,15 +303,14 @@ class TrainGraph:
         q, k = _split(qk, c, c)
         v = self._dw(m.v_dwconv, self._c1(m.v, x))
         g = 2 * c
-        k = self._dense(self._c1(m.k2, k), m.k2_dwconv.weight, m.k2_dwconv.bias, ws, 1, g)
-        q = self._dense(self._c1(m.q2, q), m.q2_dwconv.weight, m.q2_dwconv.bias, ws, 1, g)
-        th, tw = q.shape[2], q.shape[3]
+        k, _, _ = self._window(self._c1(m.k2, k), m.k2_dwconv, ws, g)
+        q, th, tw = self._window(self._c1(m.q2, q), m.q2_dwconv, ws, g)
         hh, ww = hl // ws, wl // ws
         if th * tw != hh * ww:
             raise RuntimeError(f"SAB q/k token grid {th}x{tw} != v token grid {hh}x{ww} (turtle_t1_arch.py:599)")
         n = th * tw
-        q = _l2n(q.reshape(b, g, n).transpose(1, 2).reshape(b, 1, 1, n, g), -1)
-        k = _l2n(k.reshape(b, g, n).transpose(1, 2).reshape(b, 1, 1, n, g), -1)
+        q = _l2n(q, -1)
+        k = _l2n(k, -1)
         vt = self._dilated(v, ws)
         if kc is not None and vc is not None:
             k = torch.cat([kc.to(k.dtype), k], dim=1)
@@ -398,8 +423,8 @@ class TrainGraph:
         # residual stream stays NCHW and every LayerNorm / GEMM of the level re-lays its input out
         cl = (lambda t: t.contiguous(memory_format=torch.channels_last)) if getattr(self._ops(), "channels_last", False) \
             else (lambda t: t)
-        down = lambda m, t: cl(F.pixel_unshuffle(self._dense(t, m.body[0].weight), 2))
-        up = lambda m, t: cl(F.pixel_shuffle(self._dense(t, m.body[0].weight), 2))
+        down = lambda m, t: cl(F.pixel_unshuffle(self._conv3(t, m.body[0].weight), 2))
+        up = lambda m, t: cl(F.pixel_shuffle(self._conv3(t, m.body[0].weight), 2))
         e2, k, v = self._level("encoder_level2", down(self.down1_2, e1), k_cached[1], v_cached[1]); ks.append(k); vs.append(v)
         e3, k, v = self._level("encoder_level3", down(self.down2_3, e2), k_cached[2], v_cached[2]); ks.append(k); vs.append(v)
         lat, k1, v1, k2, v2 = self._latent(down(self.down3_4, e3), k_cached[3], v_cached[3], k_cached[4], v_cached[4])

@@ -13,7 +13,12 @@ libturtle_hip.so, forward and backward:
                    reduction GEMM; its backward as GEMMs with block-diagonal per-image weights;
 * ``layer_norm``   per-pixel LayerNorm over channels (turtle_t1_arch.py:67-112), 98 per frame;
 * ``dwconv3x3``    depthwise 3x3 / pad 1 convolutions (99 per frame);
-* ``gelu_gate``    gelu(x1) * x2 of the GatedFeedForward (turtle_t1_arch.py:176).
+* ``gelu_gate``    gelu(x1) * x2 of the GatedFeedForward (turtle_t1_arch.py:176);
+* ``gelu``         the plain GELU of FeedForward / ReducedAttn (turtle_t1_arch.py:181-210, 704-742);
+* ``conv3x3``      the dense 3x3 convolutions of Down / Upsample (turtle_t1_arch.py:136-154), forward,
+                   input and weight gradients;
+* ``window_conv``  the SAB window convolutions k2_dwconv / q2_dwconv (ws x ws, stride ws, pad 1, one group
+                   per channel: turtle_t1_arch.py:306-308), forward, input and weight gradients.
 
 They run on the caller's current HIP stream; weights and their gradients are fp32, activations
 fp32 or bf16 (autocast), fp16 for the elementwise kernels; the GEMMs take fp16 autocast operands
@@ -50,6 +55,15 @@ def lib():
     L.turtle_train_rgemm.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, i64, ci, ci, vp, sz, vp]
     L.turtle_train_colsumsq.argtypes = [vp, i64, vp, i64, ci, i64, ci, vp]
     L.turtle_train_gram_wd.argtypes = [vp, vp, vp, vp, i64, ci, ci, ci, vp]
+    L.turtle_train_gelu_fwd.argtypes = [vp, i64, vp, i64, i64, ci, ci, vp]
+    L.turtle_train_gelu_bwd.argtypes = [vp, i64, vp, i64, vp, i64, i64, ci, ci, vp]
+    L.turtle_train_window_fwd.argtypes = [vp, i64, vp, vp, vp, i64, i64, ci, ci, ci, ci, ci, ci, ci, vp]
+    L.turtle_train_window_dgrad.argtypes = [vp, i64, vp, vp, i64, i64, ci, ci, ci, ci, ci, ci, ci, vp]
+    L.turtle_train_window_wgrad.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, ci, ci, ci, ci, ci, vp]
+    L.turtle_train_conv3x3.argtypes = [vp, i64, vp, vp, vp, i64, i64, ci, ci, ci, ci, ci, vp]
+    L.turtle_train_conv3x3_wgrad_workspace.argtypes = [i64, ci, ci]
+    L.turtle_train_conv3x3_wgrad_workspace.restype = sz
+    L.turtle_train_conv3x3_wgrad.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, ci, ci, ci, vp, sz, vp]
     _train = L
     return L
 
@@ -208,6 +222,126 @@ class _Gate(torch.autograd.Function):
         _check(lib().turtle_train_gate_bwd(_p(x), ctx.ldx, _p(dy), lddy, _p(dx), C2, B * H * W, C2 // 2, _dt(x), _stream(x)),
                "gate_bwd")
         return dx
+
+
+class _Gelu(torch.autograd.Function):
+    """y = gelu(x) (exact erf form) on NHWC rows; backward dx = dy gelu'(x) (turtle_train_gelu_*)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x, ldx = rows(x)
+        B, Cc, H, W = x.shape
+        y = _empty(B, Cc, H, W, x)
+        _check(lib().turtle_train_gelu_fwd(_p(x), ldx, _p(y), Cc, B * H * W, Cc, _dt(x), _stream(x)), "gelu_fwd")
+        ctx.save_for_backward(x)
+        ctx.ldx = ldx
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dy, lddy = rows(dy.to(x.dtype))
+        B, Cc, H, W = x.shape
+        dx = _empty(B, Cc, H, W, x)
+        _check(lib().turtle_train_gelu_bwd(_p(x), ctx.ldx, _p(dy), lddy, _p(dx), Cc, B * H * W, Cc, _dt(x), _stream(x)), "gelu_bwd")
+        return dx
+
+
+def window_grid(H: int, W: int, ws: int):
+    """Token grid of nn.Conv2d(kernel ws, stride ws, padding 1): ((H + 2 - ws) // ws + 1, ...)."""
+    return (H + 2 - ws) // ws + 1, (W + 2 - ws) // ws + 1
+
+
+class _WinConv(torch.autograd.Function):
+    """SAB window convolution nn.Conv2d(C, C, ws, stride=ws, padding=1, groups=C) (k2_dwconv /
+    q2_dwconv, turtle_t1_arch.py:306-308) on NHWC rows, forward and both gradients on the HIP
+    kernels (turtle_train_window_*); the bias gradient is a column sum of dy."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, ws: int):
+        x, ldx = rows(x)
+        B, Cc, H, W = x.shape
+        th, tw = window_grid(H, W, ws)
+        wt = w.detach().float().reshape(Cc, ws * ws).t().contiguous()          # [ws*ws][C]
+        b32 = None if b is None else b.detach().float().contiguous()
+        y = _empty(B, Cc, th, tw, x)
+        _check(lib().turtle_train_window_fwd(_p(x), ldx, _p(wt), _p(b32), _p(y), Cc, B, Cc, H, W, ws, th, tw, _dt(x), _stream(x)),
+               "window_fwd")
+        ctx.save_for_backward(x, wt)
+        ctx.ldx, ctx.ws, ctx.has_b, ctx.w_dt = ldx, ws, b is not None, w.dtype
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wt = ctx.saved_tensors
+        B, Cc, H, W = x.shape
+        ws = ctx.ws
+        th, tw = window_grid(H, W, ws)
+        dy, lddy = rows(dy.to(x.dtype))
+        st = _stream(x)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = _empty(B, Cc, H, W, x)
+            _check(lib().turtle_train_window_dgrad(_p(dy), lddy, _p(wt), _p(dx), Cc, B, Cc, H, W, ws, th, tw, _dt(x), st),
+                   "window_dgrad")
+        if ctx.needs_input_grad[1]:
+            dwt = torch.zeros(ws * ws, Cc, dtype=torch.float32, device=x.device)
+            _check(lib().turtle_train_window_wgrad(_p(x), ctx.ldx, _p(dy), lddy, _p(dwt), B, Cc, H, W, ws, th, tw, _dt(x), st),
+                   "window_wgrad")
+            dw = dwt.t().reshape(Cc, 1, ws, ws).to(ctx.w_dt)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.zeros(Cc, dtype=torch.float32, device=x.device)
+            _check(lib().turtle_train_colsum(_p(dy), lddy, _p(db), B * th * tw, Cc, _dt(dy), st), "colsum")
+        return dx, dw, db, None
+
+
+class _Conv3x3(torch.autograd.Function):
+    """Dense 3x3 convolution, stride 1, padding 1 (Down / Upsample body[0], turtle_t1_arch.py:136-154) on
+    NHWC rows: forward and input gradient on the inference implicit-GEMM family (turtle_train_conv3x3;
+    the input gradient with the rotated, transposed weights), weight gradient by the tap-shifted
+    reduction GEMM (turtle_train_conv3x3_wgrad). No NCHW copies, no MIOpen."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        gdt = _gemm_dt(x)
+        out_dt = x.dtype
+        xg, ldx = rows(x.to(gdt))
+        B, Cin, H, W = xg.shape
+        N = w.shape[0]
+        wf = w.detach().permute(0, 2, 3, 1).reshape(N, 9 * Cin).to(gdt).contiguous()     # [N][tap][Cin]
+        b32 = None if b is None else b.detach().float().contiguous()
+        y = _empty(B, N, H, W, xg)
+        _check(lib().turtle_train_conv3x3(_p(xg), ldx, _p(wf), _p(b32), _p(y), N, B, H, W, Cin, N, _dt(xg), _stream(xg)), "conv3x3")
+        ctx.save_for_backward(xg, w)
+        ctx.ldx, ctx.has_b, ctx.in_dt = ldx, b is not None, x.dtype
+        return y.to(out_dt)
+
+    @staticmethod
+    def backward(ctx, dy):
+        xg, w = ctx.saved_tensors
+        B, Cin, H, W = xg.shape
+        N = w.shape[0]
+        P = B * H * W
+        dy, lddy = rows(dy.to(xg.dtype))
+        st = _stream(xg)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wr = w.detach().flip(2, 3).permute(1, 2, 3, 0).reshape(Cin, 9 * N).to(xg.dtype).contiguous()   # [Cin][tap][N]
+            dx = _empty(B, Cin, H, W, xg)
+            _check(lib().turtle_train_conv3x3(_p(dy), lddy, _p(wr), None, _p(dx), Cin, B, H, W, N, Cin, _dt(xg), st), "conv3x3_dgrad")
+            dx = dx.to(ctx.in_dt)
+        if ctx.needs_input_grad[1]:
+            L = lib()
+            nws = L.turtle_train_conv3x3_wgrad_workspace(P, N, Cin)
+            ws = torch.empty(max(int(nws), 16), dtype=torch.uint8, device=xg.device)
+            dw9 = torch.empty(9, N, Cin, dtype=torch.float32, device=xg.device)
+            _check(L.turtle_train_conv3x3_wgrad(_p(dy), lddy, _p(xg), ctx.ldx, _p(dw9), B, H, W, N, Cin, _dt(xg), _p(ws), ws.numel(), st),
+                   "conv3x3_wgrad")
+            dw = dw9.permute(1, 2, 0).reshape(N, Cin, 3, 3).to(w.dtype)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.zeros(N, dtype=torch.float32, device=xg.device)
+            _check(lib().turtle_train_colsum(_p(dy), lddy, _p(db), P, N, _dt(dy), st), "colsum")
+        return dx, dw, db
 
 
 def _rgemm(a, lda, b, ldb, P, N, K, img_px):
@@ -492,6 +626,20 @@ class HipOps:
     @staticmethod
     def gelu_gate(x):
         return _Gate.apply(_act(x))
+
+    @staticmethod
+    def gelu(x):
+        return _Gelu.apply(_act(x))
+
+    @staticmethod
+    def window_conv(x, w, b, ws: int):
+        """nn.Conv2d(C, C, ws, stride=ws, padding=1, groups=C)(x), channels-last in and out."""
+        return _WinConv.apply(_act(x), w, b, ws)
+
+    @staticmethod
+    def conv3x3(x, w, b=None):
+        """nn.Conv2d(Cin, N, 3, 1, 1)(x) with Cin % 8 == N % 8 == 0, channels-last in and out."""
+        return _Conv3x3.apply(_act(x), w, b)
 
     grad_sink = GradSink
 
