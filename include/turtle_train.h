@@ -71,6 +71,19 @@ int turtle_train_colsum(const void* dy, int64_t ld, float* db, int64_t P, int N,
  * out[img][n] += sum over the img_px pixels of image img of x[p][n]^2; out fp32 [P / img_px][N], zeroed by the caller */
 int turtle_train_colsumsq(const void* x, int64_t ld, float* out, int64_t P, int N, int64_t img_px, int dtype, void* stream);
 
+/* per-image column dot products out[img][n] += sum over the img_px pixels of image img of a[p][n] b[p][n]
+ * (the L2-normalisation backward's sum dy . y); out fp32 [P / img_px][N], zeroed by the caller */
+int turtle_train_coldot(const void* a, int64_t lda, const void* b, int64_t ldb, float* out, int64_t P, int N, int64_t img_px,
+                        int dtype, void* stream);
+/* per-image column scaling y[p][c] = x[p][c] s[img][c] (s fp32 [P / img_px][C]): the forward of the per-channel
+ * L2 normalisation over HW (turtle_t1_arch.py:236-237, 649-651: F.normalize(dim=-1) of the [b, heads, ch, HW]
+ * view) with s = 1 / max(|x_col|, 1e-12) from turtle_train_colsumsq */
+int turtle_train_colscale(const void* x, int64_t ldx, const float* s, void* y, int64_t ldy, int64_t P, int C, int64_t img_px,
+                          int dtype, void* stream);
+/* its backward dx = (dy - y d) s, d fp32 [P / img_px][C] = sum_p dy y (0 where the norm was clamped) */
+int turtle_train_l2n_bwd(const void* dy, int64_t lddy, const void* y, int64_t ldy, const float* d, const float* s, void* dx,
+                         int64_t lddx, int64_t P, int C, int64_t img_px, int dtype, void* stream);
+
 /* the per-image weight of the normalised channel-attention Gram backward (turtle_t1_arch.py:690-697
  * differentiated): wd[b] [2c][2c] = [[diag(aq[b]), D[b]], [D[b]^T, diag(ak[b])]], D [B][heads][ch][ch] fp32
  * block-diagonal per head (ch = c / heads), aq / ak fp32 [B][c]; wd in the activation dtype, dense */

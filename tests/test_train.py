@@ -343,6 +343,31 @@ def test_hip_gelu_window_conv3x3_match_autograd(dtype):
         scale = float(rw.abs().max())
         torch.testing.assert_close(gw, rw, rtol=tol["rtol"] * 10, atol=tol["atol"] * 10 * max(scale, 1.0))
         torch.testing.assert_close(gb, rb, rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
+    # FHR / CHM attention pieces: per-channel L2 normalisation over HW (incl. an all-zero channel: the
+    # clamp) and the cross Gram q^T K per image
+    x = torch.randn(3, 40, 9, 11, device=dev)
+    x[1, 5] = 0
+    x = x.to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    y = HipOps.norm_cols(x)
+    gy = torch.randn(y.shape, device=dev).to(dtype)
+    (gx,) = torch.autograd.grad(y, [x], gy)
+    x2 = x.detach().float().requires_grad_()
+    y2 = torch.nn.functional.normalize(x2.reshape(3, 40, 99), dim=-1).reshape(3, 40, 9, 11)
+    (rx,) = torch.autograd.grad(y2, [x2], gy.float())
+    torch.testing.assert_close(y.float(), y2, **tol)
+    torch.testing.assert_close(gx.float(), rx, rtol=tol["rtol"], atol=tol["atol"] * 10)
+    q = torch.randn(2, 32, 12, 10, device=dev).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    K = torch.randn(2, 96, 12, 10, device=dev).to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    G = HipOps.cross_gram(q, K)
+    gG = torch.randn_like(G)
+    gq, gK = torch.autograd.grad(G, [q, K], gG)
+    q2, K2 = q.detach().float().requires_grad_(), K.detach().float().requires_grad_()
+    G2 = q2.reshape(2, 32, 120) @ K2.reshape(2, 96, 120).transpose(1, 2)
+    rq, rK = torch.autograd.grad(G2, [q2, K2], gG)
+    gtol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=2e-1)
+    torch.testing.assert_close(G, G2, rtol=gtol["rtol"], atol=gtol["atol"] * 10)
+    torch.testing.assert_close(gq.float(), rq, **gtol)
+    torch.testing.assert_close(gK.float(), rK, **gtol)
     # Down / Upsample 3x3 convolutions (bias-free in the reference; a bias checked too)
     for (B, Cin, N, H, W, bias) in [(2, 64, 32, 20, 24, False), (1, 128, 256, 16, 8, False), (2, 24, 40, 9, 13, True),
                                     (1, 512, 1024, 4, 6, False)]:

@@ -161,9 +161,9 @@ int main(int argc, char** argv) {
         run(nm, [&] { launch_fused2(c, 0); });
       }
     } else if (fused2_ok(ab)) {
-      for (int v = 0; v < 9; ++v) {
+      for (int v = 0; v < 12; ++v) {
         if (only_v >= 0 && std::find(vlist.begin(), vlist.end(), v) == vlist.end()) continue;
-        if (v >= 6 && !(ab.mode == F_GATE && ab.C == 64)) continue;
+        if (v >= 6 && v < 10 && !(ab.mode == F_GATE && ab.C == 64)) continue;
         FusedArgs c = ab; c.dbg = v;
         char nm[16]; snprintf(nm, sizeof nm, "fused2.%d", v);
         run(nm, [&] { launch_fused2(c, 0); });

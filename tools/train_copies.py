@@ -116,6 +116,31 @@ class MimicOps:
         return _Mimic.apply(x, fn, *((w, b) if b is not None else (w,)))
 
     @staticmethod
+    def gelu(x):
+        return _Mimic.apply(_act(x), lambda t: F.gelu(t))
+
+    @staticmethod
+    def window_conv(x, w, b, ws):
+        if b is None:
+            return _Mimic.apply(_act(x), lambda t, ww: F.conv2d(t, ww.to(t.dtype), None, ws, 1, 1, t.shape[1]), w)
+        return _Mimic.apply(_act(x), lambda t, ww, bb: F.conv2d(t, ww.to(t.dtype), bb.to(t.dtype), ws, 1, 1, t.shape[1]), w, b)
+
+    @staticmethod
+    def conv3x3(x, w, b=None):
+        return _Mimic.apply(_act(x), lambda t, ww: F.conv2d(t, ww.to(t.dtype), None, 1, 1), w)
+
+    @staticmethod
+    def norm_gram(qk, heads, sink=None):
+        qk = rows(_act(qk))
+        b, c2, h, w = qk.shape
+        c = c2 // 2
+        qh = qk[:, :c].reshape(b, heads, c // heads, h * w).float()
+        kh = qk[:, c:].reshape(b, heads, c // heads, h * w).float()
+        qh = qh / qh.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+        kh = kh / kh.norm(dim=-1, keepdim=True).clamp_min(1e-12)
+        return qh @ kh.transpose(-2, -1)
+
+    @staticmethod
     def gram(q, k, heads):
         q, k = rows(_act(q)), rows(_act(k))
         b, c, h, w = q.shape

@@ -38,6 +38,12 @@ with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=True
     torch.cuda.synchronize()
 ka = prof.key_averages(group_by_input_shape=True)
 print(ka.table(sort_by="self_device_time_total", row_limit=60, max_name_column_width=50, max_shapes_column_width=70))
+# torch ops and autograd nodes outside the HIP op set (which ops the remaining ATen time belongs to)
+ko = [e for e in prof.key_averages() if (e.key.startswith("aten::") or "Backward" in e.key) and not e.key.startswith("_")]
+ko.sort(key=lambda e: -e.device_time_total)
+print("\n==== torch ops / autograd nodes by device time (incl. children) ====")
+for e in ko[:60]:
+    print(f"{e.device_time_total / 1e3:9.2f} ms  n={e.count:5d}  {e.key}")
 ks = prof.key_averages(group_by_stack_n=6)
 rows = [e for e in ks if any(s in e.key for s in ("copy", "to", "contiguous", "clone", "cat", "permute"))]
 rows.sort(key=lambda e: -e.self_device_time_total)

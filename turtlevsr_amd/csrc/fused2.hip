@@ -91,7 +91,9 @@ struct F2L {
 // ABL: per-phase ablations (tools/f2bench built with TURTLE_F2_ABLATIONS; 0 in the library): 1 no GELU,
 // 2 no depthwise (the centre row only), 4 no GEMM2 MFMAs, 8 no LayerNorm prologue, 16 no output
 // stores, 32 no GEMM1 (MFMAs and their LDS reads)
-template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE, int TPB = 1, bool TG = false, int ABL = 0>
+// PF (TPB > 1): the next tile's input fetched into registers during this tile's walks (true), or at
+// the start of each tile (false: no registers live across the walks, the occupancy of TPB = 1)
+template <int MODE, int CM, int R, int NW, int HPM, int N1M, int WPE, int TPB = 1, bool TG = false, int ABL = 0, bool PF = true>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) void fused2_kernel(FusedArgs a) {
   using L = F2L<CM, R, HPM, TG ? 0 : N1M>;
   constexpr int KS = CM / 32;                       // GEMM1 K steps
@@ -153,18 +155,19 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
       vx[i] = ld16(ok ? reinterpret_cast<const void*>(X + off) : g_zero_f2);
     }
   };
-  if (t_begin < t_end) fetch_x(t_begin);
+  if (PF && t_begin < t_end) fetch_x(t_begin);
   for (int tile = t_begin; tile < t_end; ++tile) {
   const int img = tile / (tx_n * ty_n);
   const int trem = tile - img * tx_n * ty_n;
   const int y0 = (trem / tx_n) * R, x0 = (trem % tx_n) * F2_TX;
+  if constexpr (!PF) fetch_x(tile);
   if (tile > t_begin) __syncthreads();               // every wave is done with the previous tile's LDS
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int e = tid + NT * i, p = e / CV, k = (e - p * CV) * 8;
     if (p < L::NXP) *reinterpret_cast<uint4*>(sX + p * L::XP + k * 2) = vx[i];
   }
-  if (tile + 1 < t_end) fetch_x(tile + 1);           // in flight during this tile's walks
+  if (PF && tile + 1 < t_end) fetch_x(tile + 1);     // in flight during this tile's walks
   __syncthreads();
   // ---- LayerNorm of every haloed pixel in place (2 threads per pixel, shifted sums): the tile
   // becomes (x - mu) rs (BiasFree: x rs, uncentred), rounded to bf16 once - the resident-panel
@@ -506,7 +509,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
 // (MODE, C) -> (tile rows, waves, hidden per pass); units per pass chosen so every wave of a pass
 // gets the same number of units
-template <int MODE, int CM, int R, int NW, int HPM, int WPE, int TPB = 1, bool TG = false, int ABL = 0>
+template <int MODE, int CM, int R, int NW, int HPM, int WPE, int TPB = 1, bool TG = false, int ABL = 0, bool PF = true>
 static void f2_launch(const FusedArgs& a0, hipStream_t st) {
   FusedArgs a = a0;
   a.up = HPM / 16;
@@ -515,7 +518,7 @@ static void f2_launch(const FusedArgs& a0, hipStream_t st) {
   constexpr int N1M = MODE == F_GATE ? 5 * CM : (MODE == F_GELU ? 2 * CM : 6 * CM);
   const int64_t tiles = (int64_t)a.nimg * ((a.H + R - 1) / R) * ((a.W + F2_TX - 1) / F2_TX);
   const int64_t blocks = (tiles + TPB - 1) / TPB;
-  hipLaunchKernelGGL((fused2_kernel<MODE, CM, R, NW, HPM, N1M, WPE, TPB, TG, ABL>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, a);
+  hipLaunchKernelGGL((fused2_kernel<MODE, CM, R, NW, HPM, N1M, WPE, TPB, TG, ABL, PF>), dim3((unsigned)blocks), dim3(NW * 64), 0, st, a);
 }
 
 bool fused2_ok(const FusedArgs& a) {
@@ -549,10 +552,28 @@ static void f2_abl(const FusedArgs& a, hipStream_t st) {
 }
 #endif
 
+// the default configuration of each shape family walking TPB consecutive tiles per block, each
+// tile's input fetched at its start (variants 10 / 11 of tools/f2bench)
+template <int TPB>
+static void f2_runs(const FusedArgs& a, hipStream_t st) {
+  if (a.mode == F_DWONLY) {
+    if (a.C == 64) f2_launch<F_DWONLY, 64, 12, 4, 0, 4, TPB, false, 0, false>(a, st);
+    else f2_launch<F_DWONLY, 128, 9, 4, 0, 4, TPB, false, 0, false>(a, st);
+  } else if (a.mode == F_GATE) {
+    if (a.C == 64) f2_launch<F_GATE, 64, 6, 4, 64, 3, TPB, false, 0, false>(a, st);
+    else f2_launch<F_GATE, 128, 6, 4, 64, 2, TPB, false, 0, false>(a, st);
+  } else {
+    if (a.C == 64) f2_launch<F_GELU, 64, 6, 4, 128, 3, TPB, false, 0, false>(a, st);
+    else f2_launch<F_GELU, 128, 9, 4, 64, 2, TPB, false, 0, false>(a, st);
+  }
+}
+
 void launch_fused2(const FusedArgs& a, hipStream_t st) {
   // defaults (v = 0) are the fastest measured per shape family on MI355X (tools/f2bench, 1080p);
   // v = 1..5 are the alternatives of the last sweep (profiles/r02h_f2bench_sweep.log)
   const int v = a.dbg & 255;
+  if (v == 10) { f2_runs<2>(a, st); return; }
+  if (v == 11) { f2_runs<4>(a, st); return; }
 #ifdef TURTLE_F2_ABLATIONS
   switch (a.dbg >> 8) {
     case 0: break;

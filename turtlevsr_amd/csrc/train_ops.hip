@@ -593,12 +593,58 @@ __global__ __launch_bounds__(256) void win_wgrad_kernel(const T* __restrict__ x,
   }
 }
 
+// Per-image column L2 normalisation over the pixels (F.normalize(x, dim=-1) of a [b, heads, ch, HW]
+// view, turtle_t1_arch.py:236-237 / 649-651, on NHWC rows): y[p][c] = x[p][c] s[img(p)][c] with
+// s = 1 / max(|x_col|, 1e-12); backward dx = (dy - y d) s with d[img][c] = sum_p dy y (0 where the clamp
+// was active, whose norm gets no gradient)
+template <typename T>
+__global__ __launch_bounds__(256) void colscale_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ s,
+                                                       T* __restrict__ y, int64_t ldy, int64_t P, int C, int64_t img_px) {
+  const int nch = C / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P * nch) return;
+  const int64_t p = gid / nch;
+  const int c = 8 * (int)(gid % nch);
+  const float* sp = s + (p / img_px) * C + c;
+  float v[8];
+  ld8f(x + p * ldx + c, v);
+  const float4 s0 = *reinterpret_cast<const float4*>(sp), s1 = *reinterpret_cast<const float4*>(sp + 4);
+  const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] *= sv[e];
+  st8f(y + p * ldy + c, v);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void l2n_bwd_kernel(const T* __restrict__ dy, int64_t lddy, const T* __restrict__ y, int64_t ldy,
+                                                      const float* __restrict__ d, const float* __restrict__ s, T* __restrict__ dx,
+                                                      int64_t lddx, int64_t P, int C, int64_t img_px) {
+  const int nch = C / 8;
+  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (gid >= P * nch) return;
+  const int64_t p = gid / nch;
+  const int c = 8 * (int)(gid % nch);
+  const int64_t o = (p / img_px) * C + c;
+  float g[8], v[8];
+  ld8f(dy + p * lddy + c, g);
+  ld8f(y + p * ldy + c, v);
+  const float4 d0 = *reinterpret_cast<const float4*>(d + o), d1 = *reinterpret_cast<const float4*>(d + o + 4);
+  const float4 s0 = *reinterpret_cast<const float4*>(s + o), s1 = *reinterpret_cast<const float4*>(s + o + 4);
+  const float dv[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+  const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+  for (int e = 0; e < 8; ++e) g[e] = (g[e] - v[e] * dv[e]) * sv[e];
+  st8f(dx + p * lddx + c, g);
+}
+
 // column sums db[n] = sum_p dy[p][n] (8 channels per thread, pixel lanes, LDS reduction, atomics)
 template <typename T>
+// square: sums of squares; dy2 != NULL: column dot products sum_p dy[p][n] dy2[p][n]
 __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, int64_t ld, float* __restrict__ db, int64_t P,
-                                                     int N, int64_t ppb, int square) {
+                                                     int N, int64_t ppb, int square, const T* __restrict__ dy2 = nullptr,
+                                                     int64_t ld2 = 0) {
   extern __shared__ float sred[];
   dy += (int64_t)blockIdx.y * P * ld;              // image blockIdx.y of P pixels (one image: y = 0)
+  if (dy2) dy2 += (int64_t)blockIdx.y * P * ld2;
   db += (int64_t)blockIdx.y * N;
   for (int i = threadIdx.x; i < N; i += 256) sred[i] = 0.f;
   __syncthreads();
@@ -610,7 +656,12 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, i
     for (int64_t p = p0 + pl; p < p1; p += lanes) {
       float v[8];
       ld8f(dy + p * ld + 8 * ch, v);
-      if (square) {
+      if (dy2) {
+        float v2[8];
+        ld8f(dy2 + p * ld2 + 8 * ch, v2);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] = fmaf(v[e], v2[e], a[e]);
+      } else if (square) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) a[e] = fmaf(v[e], v[e], a[e]);
       } else {
@@ -1031,6 +1082,31 @@ int colsumsq(const void* x, int64_t ld, float* out, int64_t P, int N, int64_t im
   return 0;
 }
 
+// per-image column dot products out[img][n] += sum over the image's pixels of a[p][n] b[p][n]
+template <typename T>
+int coldot(const void* a, int64_t lda, const void* b, int64_t ldb, float* out, int64_t P, int N, int64_t img_px, hipStream_t st) {
+  const int64_t nimg = P / img_px;
+  const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 512 / nimg), std::max<int64_t>(1, img_px / 256));
+  const int64_t ppb = (img_px + blocks - 1) / blocks;
+  hipLaunchKernelGGL(colsum_kernel<T>, dim3((unsigned)blocks, (unsigned)nimg), dim3(256), N * sizeof(float), st, (const T*)a, lda, out,
+                     img_px, N, ppb, 0, (const T*)b, ldb);
+  return 0;
+}
+template <typename T>
+int colscale(const void* x, int64_t ldx, const float* s, void* y, int64_t ldy, int64_t P, int C, int64_t img_px, hipStream_t st) {
+  const int64_t tot = P * (C / 8);
+  hipLaunchKernelGGL(colscale_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)x, ldx, s, (T*)y, ldy, P, C,
+                     img_px);
+  return 0;
+}
+template <typename T>
+int l2n_bwd(const void* dy, int64_t lddy, const void* y, int64_t ldy, const float* d, const float* s, void* dx, int64_t lddx, int64_t P,
+            int C, int64_t img_px, hipStream_t st) {
+  const int64_t tot = P * (C / 8);
+  hipLaunchKernelGGL(l2n_bwd_kernel<T>, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, (const T*)dy, lddy, (const T*)y, ldy, d,
+                     s, (T*)dx, lddx, P, C, img_px);
+  return 0;
+}
 // per-image Gram-backward weights (gram_wd_kernel)
 template <typename T>
 int gram_wd(const float* D, const float* aq, const float* ak, void* wd, int64_t B, int c, int heads, hipStream_t st) {
@@ -1197,6 +1273,29 @@ int turtle_train_colsumsq(const void* x, int64_t ld, float* out, int64_t P, int 
   if (!rows_ok(x, ld, dtype) || !out || P <= 0 || N <= 0 || N % 8 || N > 2048 || img_px <= 0 || P % img_px || P / img_px > 65535)
     return -1;
   TT_DISPATCH(dtype, colsumsq, x, ld, out, P, N, img_px, (hipStream_t)stream);
+}
+
+int turtle_train_coldot(const void* a, int64_t lda, const void* b, int64_t ldb, float* out, int64_t P, int N, int64_t img_px,
+                        int dtype, void* stream) {
+  if (!rows_ok(a, lda, dtype) || !rows_ok(b, ldb, dtype) || !out || P <= 0 || N <= 0 || N % 8 || N > 2048 || img_px <= 0 ||
+      P % img_px || P / img_px > 65535)
+    return -1;
+  TT_DISPATCH(dtype, coldot, a, lda, b, ldb, out, P, N, img_px, (hipStream_t)stream);
+}
+
+int turtle_train_colscale(const void* x, int64_t ldx, const float* s, void* y, int64_t ldy, int64_t P, int C, int64_t img_px,
+                          int dtype, void* stream) {
+  if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !s || P <= 0 || C <= 0 || C % 8 || img_px <= 0 || P % img_px)
+    return -1;
+  TT_DISPATCH(dtype, colscale, x, ldx, s, y, ldy, P, C, img_px, (hipStream_t)stream);
+}
+
+int turtle_train_l2n_bwd(const void* dy, int64_t lddy, const void* y, int64_t ldy, const float* d, const float* s, void* dx,
+                         int64_t lddx, int64_t P, int C, int64_t img_px, int dtype, void* stream) {
+  if (!rows_ok(dy, lddy, dtype) || !rows_ok(y, ldy, dtype) || !rows_ok(dx, lddx, dtype) || !d || !s || P <= 0 || C <= 0 || C % 8 ||
+      img_px <= 0 || P % img_px)
+    return -1;
+  TT_DISPATCH(dtype, l2n_bwd, dy, lddy, y, ldy, d, s, dx, lddx, P, C, img_px, (hipStream_t)stream);
 }
 
 int turtle_train_gram_wd(const float* D, const float* aq, const float* ak, void* wd, int64_t B, int c, int heads, int dtype,

@@ -114,6 +114,14 @@ class _ToNCHW(torch.autograd.Function):
         return g.contiguous(memory_format=torch.channels_last) if ctx.cl else g
 
 
+class _Frames:
+    """T consecutive frames per batch element as one channels-last [b * T, C, H, W] map (the CHM's aligned
+    k / v), passed to TrainGraph._hist_cat in place of a [b, heads, T ch, HW] cache view."""
+
+    def __init__(self, x, t):
+        self.x, self.t = x, t
+
+
 def positional_encoding_2d(c: int, h: int, w: int) -> torch.Tensor:
     """Sinusoidal 2-D encoding of the t0 StateAlignBlock (turtle_arch.py:412-439): channels
     [0, c/2) encode the column, [c/2, c) the row, sin on even and cos on odd channels, frequencies
@@ -259,6 +267,8 @@ class TrainGraph:
             wp = m.project_out.weight.reshape(c, heads, ch)
             weff = torch.einsum("ohi,bhij->bohj", wp, a).reshape(b, c, c)
             return ops.conv1x1(v, weff, m.project_out.bias), None, None
+        if hasattr(ops, "cross_gram"):
+            return self._chan_hist(m, qkv, heads, kc, vc, ntc)
         q, k, v = _split(qkv, c, c, c)
         q, k, v = _l2n(self._heads(q, heads), -1), _l2n(self._heads(k, heads), -1), self._heads(v, heads)
         if kc is not None and vc is not None:
@@ -270,6 +280,55 @@ class TrainGraph:
             return out, None, None
         keep = int(ntc * c / heads)
         return out, k[:, :, -keep:, :], v[:, :, -keep:, :]
+
+    @staticmethod
+    def _hist_cat(cache, cur, heads):
+        """[cache ; cur] per head as a channels-last [b, heads * (T+1) * ch, h, w] tensor, head-major
+        (channel h (T+1) ch + t ch + i: a head's rows are its cached frames, then the current one, as
+        torch.cat(dim=2) of the [b, heads, rows, HW] views, turtle_t1_arch.py:238-240). ``cache``: None,
+        a [b, heads, T ch, HW] view (the reference layout, or a slice of an earlier result of this), or
+        a ``_Frames`` (CHM: T per-frame channels-last maps of the batch)."""
+        b, c, h, w = cur.shape
+        ch = c // heads
+        if cache is None:
+            return cur, 0
+        cur6 = cur.permute(0, 2, 3, 1).reshape(b, h, w, heads, 1, ch)
+        if isinstance(cache, _Frames):
+            t = cache.t
+            c6 = cache.x.permute(0, 2, 3, 1).reshape(b, t, h, w, heads, ch).permute(0, 2, 3, 4, 1, 5)
+        else:
+            t = cache.shape[2] // ch
+            c6 = cache.permute(0, 3, 1, 2).reshape(b, h, w, heads, t, ch)
+        out = torch.cat([c6.to(cur.dtype), cur6], dim=4)
+        return out.reshape(b, h, w, heads * (t + 1) * ch).permute(0, 3, 1, 2), t
+
+    def _chan_hist(self, m, qkv, heads, kc, vc, ntc):
+        """FrameHistoryRouter / the CHM's channel attention over the cached frames (turtle_t1_arch.py:218-286,
+        649-660) on the op set's kernels: q, k L2-normalised over HW per channel (norm_cols), the scores
+        q_hat [k_cache ; k_hat]^T of all head pairs as one reduction GEMM (cross_gram; each head's block
+        taken), softmax, then project_out . blockdiag(A) as one per-image weight set applied to
+        [v_cache ; v] - the A v product and project_out in one GEMM, as the inference path does."""
+        ops = self._ops()
+        c = qkv.shape[1] // 3
+        b, _, h, w = qkv.shape
+        ch = c // heads
+        q, k, v = _split(qkv, c, c, c)
+        qn, kn = ops.norm_cols(q), ops.norm_cols(k)
+        K, t = self._hist_cat(kc, kn, heads)
+        V, _ = self._hist_cat(vc, v, heads)
+        L = (t + 1) * ch
+        G = ops.cross_gram(qn, K)                                           # [b, c, heads * L]
+        Gh = G.view(b, heads, ch, heads, L).diagonal(dim1=1, dim2=3).permute(0, 3, 1, 2)   # [b, heads, ch, L]
+        a = torch.softmax(Gh * m.temperature, dim=-1)
+        wp = m.project_out.weight.reshape(c, heads, ch)
+        weff = torch.einsum("ohi,bhik->bohk", wp, a).reshape(b, c, heads * L)
+        out = ops.conv1x1(V, weff, m.project_out.bias)
+        if ntc is None:
+            return out, None, None
+        keep = int(ntc * c / heads)
+        s0 = max(0, L - keep)
+        view = lambda T: T.permute(0, 2, 3, 1).reshape(b, h * w, heads, L)[:, :, :, s0:].permute(0, 2, 3, 1)
+        return out, view(K), view(V)
 
     def _ball_mask(self, th, tw, dev, dtype):
         cache = self.__dict__.setdefault("_ball", {})
@@ -357,6 +416,12 @@ class TrainGraph:
         t = xs.shape[1]
         kv = self._dw(m.kv_dwconv, self._c1(m.kv, xs.reshape(b * t, c, h, w)))
         kh, vh = _split(kv, c, c)
+        ops = self._ops()
+        if hasattr(ops, "cross_gram"):
+            # the aligned frames' k, v as per-frame channels-last maps: the history concatenation
+            # (_hist_cat) reads them in place; k L2-normalised per frame and channel over HW (649-651)
+            out, _, _ = self._chan(m.ChanAttn, x, heads, _Frames(ops.norm_cols(kh), t), _Frames(vh, t), ntc=1)
+            return out, k_keep, v_keep
         ch = c // heads
         kh = kh.reshape(b, t, heads, ch, h * w).transpose(1, 2).reshape(b, heads, t * ch, h * w)
         vh = vh.reshape(b, t, heads, ch, h * w).transpose(1, 2).reshape(b, heads, t * ch, h * w)

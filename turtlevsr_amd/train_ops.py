@@ -15,6 +15,8 @@ libturtle_hip.so, forward and backward:
 * ``dwconv3x3``    depthwise 3x3 / pad 1 convolutions (99 per frame);
 * ``gelu_gate``    gelu(x1) * x2 of the GatedFeedForward (turtle_t1_arch.py:176);
 * ``gelu``         the plain GELU of FeedForward / ReducedAttn (turtle_t1_arch.py:181-210, 704-742);
+* ``norm_cols`` / ``cross_gram``  the FHR / CHM attention with its caches (turtle_t1_arch.py:218-286,
+                   612-662): per-channel L2 normalisation over HW and the q [k_cache ; k]^T scores;
 * ``conv3x3``      the dense 3x3 convolutions of Down / Upsample (turtle_t1_arch.py:136-154), forward,
                    input and weight gradients;
 * ``window_conv``  the SAB window convolutions k2_dwconv / q2_dwconv (ws x ws, stride ws, pad 1, one group
@@ -61,6 +63,9 @@ def lib():
     L.turtle_train_window_dgrad.argtypes = [vp, i64, vp, vp, i64, i64, ci, ci, ci, ci, ci, ci, ci, vp]
     L.turtle_train_window_wgrad.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, ci, ci, ci, ci, ci, vp]
     L.turtle_train_conv3x3.argtypes = [vp, i64, vp, vp, vp, i64, i64, ci, ci, ci, ci, ci, vp]
+    L.turtle_train_coldot.argtypes = [vp, i64, vp, i64, vp, i64, ci, i64, ci, vp]
+    L.turtle_train_colscale.argtypes = [vp, i64, vp, vp, i64, i64, ci, i64, ci, vp]
+    L.turtle_train_l2n_bwd.argtypes = [vp, i64, vp, i64, vp, vp, vp, i64, i64, ci, i64, ci, vp]
     L.turtle_train_conv3x3_wgrad_workspace.argtypes = [i64, ci, ci]
     L.turtle_train_conv3x3_wgrad_workspace.restype = sz
     L.turtle_train_conv3x3_wgrad.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, ci, ci, ci, vp, sz, vp]
@@ -342,6 +347,80 @@ class _Conv3x3(torch.autograd.Function):
             db = torch.zeros(N, dtype=torch.float32, device=xg.device)
             _check(lib().turtle_train_colsum(_p(dy), lddy, _p(db), P, N, _dt(dy), st), "colsum")
         return dx, dw, db
+
+
+class _NormCols(torch.autograd.Function):
+    """Per-image, per-channel L2 normalisation over the pixels on NHWC rows: F.normalize(t, dim=-1) of the
+    [b, heads, ch, HW] view of q / k (turtle_t1_arch.py:236-237, 649-651), y = x / max(|x|, 1e-12), in
+    x's dtype. Forward: column sums of squares + one scaling pass; backward dx = (dy - y sum(dy y)) / |x|
+    (turtle_train_colsumsq / colscale / coldot / l2n_bwd) - no fp32 copies, no NCHW re-layout."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x, ldx = rows(x)
+        B, Cc, H, W = x.shape
+        HW, P = H * W, B * H * W
+        st = _stream(x)
+        ss = torch.zeros(B, Cc, dtype=torch.float32, device=x.device)
+        _check(lib().turtle_train_colsumsq(_p(x), ldx, _p(ss), P, Cc, HW, _dt(x), st), "colsumsq")
+        n = ss.sqrt()
+        inv = 1.0 / n.clamp_min(L2N_EPS)
+        y = _empty(B, Cc, H, W, x)
+        _check(lib().turtle_train_colscale(_p(x), ldx, _p(inv), _p(y), Cc, P, Cc, HW, _dt(x), st), "colscale")
+        ctx.save_for_backward(y, inv, (n > L2N_EPS).float())
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        y, inv, live = ctx.saved_tensors
+        B, Cc, H, W = y.shape
+        HW, P = H * W, B * H * W
+        st = _stream(y)
+        dy, lddy = rows(dy.to(y.dtype))
+        d = torch.zeros(B, Cc, dtype=torch.float32, device=y.device)
+        _check(lib().turtle_train_coldot(_p(dy), lddy, _p(y), Cc, _p(d), P, Cc, HW, _dt(y), st), "coldot")
+        d = (d * live).contiguous()
+        dx = _empty(B, Cc, H, W, y)
+        _check(lib().turtle_train_l2n_bwd(_p(dy), lddy, _p(y), Cc, _p(d), _p(inv), _p(dx), Cc, P, Cc, HW, _dt(y), st), "l2n_bwd")
+        return dx
+
+
+L2N_EPS = 1e-12
+
+
+class _CrossGram(torch.autograd.Function):
+    """G[b] [cq, cK] fp32 = sum over image b's pixels of q[p]^T K[p] (NHWC rows): the FHR / CHM attention
+    scores q_hat [k_cache ; k_hat]^T of every head pair (turtle_t1_arch.py:238-241, 649-660; the caller
+    takes the per-head blocks). Reduction GEMM forward; backward dq = K dG^T, dK = q dG as GEMMs with one
+    weight set per image."""
+
+    @staticmethod
+    def forward(ctx, q, K):
+        gdt = _gemm_dt(q)
+        in_q, in_k = q.dtype, K.dtype
+        q, ldq = rows(q.to(gdt))
+        K, ldk = rows(K.to(gdt))
+        B, cq, H, W = q.shape
+        cK = K.shape[1]
+        P, HW = B * H * W, H * W
+        G = _rgemm(q, ldq, K, ldk, P, cq, cK, HW)                       # [B, cq, cK]
+        ctx.save_for_backward(q, K)
+        ctx.ldq, ctx.ldk, ctx.in_q, ctx.in_k = ldq, ldk, in_q, in_k
+        return G
+
+    @staticmethod
+    def backward(ctx, dG):
+        q, K = ctx.saved_tensors
+        B, cq, H, W = q.shape
+        cK = K.shape[1]
+        P, HW = B * H * W, H * W
+        dG = dG.float()
+        dq = dk = None
+        if ctx.needs_input_grad[0]:
+            dq = _gemm_into(K, ctx.ldk, dG.to(K.dtype).contiguous(), HW, None, P, cK, cq).to(ctx.in_q)
+        if ctx.needs_input_grad[1]:
+            dk = _gemm_into(q, ctx.ldq, dG.transpose(1, 2).to(q.dtype).contiguous(), HW, None, P, cq, cK).to(ctx.in_k)
+        return dq, dk
 
 
 def _rgemm(a, lda, b, ldb, P, N, K, img_px):
@@ -635,6 +714,16 @@ class HipOps:
     def window_conv(x, w, b, ws: int):
         """nn.Conv2d(C, C, ws, stride=ws, padding=1, groups=C)(x), channels-last in and out."""
         return _WinConv.apply(_act(x), w, b, ws)
+
+    @staticmethod
+    def norm_cols(x):
+        """x / max(|x|, 1e-12) per image and channel over H x W (F.normalize of the [b, heads, ch, HW] view)."""
+        return _NormCols.apply(_act(x))
+
+    @staticmethod
+    def cross_gram(q, K):
+        """[b, cq, cK] fp32: sum over each image's pixels of q[p]^T K[p] (channels-last q, K)."""
+        return _CrossGram.apply(_act(q), _act(K))
 
     @staticmethod
     def conv3x3(x, w, b=None):
