@@ -84,6 +84,17 @@ int turtle_train_colscale(const void* x, int64_t ldx, const float* s, void* y, i
 int turtle_train_l2n_bwd(const void* dy, int64_t lddy, const void* y, int64_t ldy, const float* d, const float* s, void* dx,
                          int64_t lddx, int64_t P, int C, int64_t img_px, int dtype, void* stream);
 
+/* StateAlignBlock attention row (turtle_t1_arch.py:394-416 top-5, 448-464 L1 ball, 115-132 clipped_softmax,
+ * combined as in 585-599): s fp32 [R][n] (rows ordered (image, frame, query i), n keys on a (n / tw) x tw token
+ * grid); m_j = [j in the row's top-5] + [L1 distance of tokens i, j <= radius] (0 / 1 / 2: the reference's
+ * s * (top + ball)); entries with s_j m_j == 0 masked; a = softmax of s m over the rest, renormalised, in the
+ * activation dtype (dtype), plus a fp32 and m (uint8 [R][n]) for the backward. n <= 1024. */
+int turtle_train_sab_softmax_fwd(const float* s, int64_t R, int n, int tw, int radius, void* a, float* a_save, void* m_save,
+                                 int dtype, void* stream);
+/* its backward: ds fp32 [R][n] = m_j a_j (da_j - sum_k da_k a_k), da in dtype */
+int turtle_train_sab_softmax_bwd(const void* da, const float* a_save, const void* m_save, int64_t R, int n, float* ds, int dtype,
+                                 void* stream);
+
 /* the per-image weight of the normalised channel-attention Gram backward (turtle_t1_arch.py:690-697
  * differentiated): wd[b] [2c][2c] = [[diag(aq[b]), D[b]], [D[b]^T, diag(ak[b])]], D [B][heads][ch][ch] fp32
  * block-diagonal per head (ch = c / heads), aq / ak fp32 [B][c]; wd in the activation dtype, dense */

@@ -368,6 +368,26 @@ def test_hip_gelu_window_conv3x3_match_autograd(dtype):
     torch.testing.assert_close(G, G2, rtol=gtol["rtol"], atol=gtol["atol"] * 10)
     torch.testing.assert_close(gq.float(), rq, **gtol)
     torch.testing.assert_close(gK.float(), rK, **gtol)
+    # StateAlignBlock top-5 + L1-ball clipped softmax (turtle_t1_arch.py:115-132, 394-416, 448-464, 585-599)
+    for (n, tw) in [(64, 8), (256, 16), (120, 12)]:
+        s0 = torch.randn(2, 3, 1, 7, n, device=dev) * 3
+        i = torch.arange(7, device=dev)                       # rows = queries 0..6 of each (b, t) block
+        s0 = torch.randn(2, 3, 1, n, n, device=dev) * 3
+        s0 = s0.requires_grad_()
+        a = HipOps.sab_softmax(s0, tw, 4)
+        ga = torch.randn_like(a)
+        (gs,) = torch.autograd.grad(a, [s0], ga)
+        s2 = s0.detach().requires_grad_()
+        qi = torch.arange(n, device=dev)
+        ball = (((qi[:, None] // tw - qi[None, :] // tw).abs() + (qi[:, None] % tw - qi[None, :] % tw).abs()) <= 4).float()
+        top = torch.zeros_like(s2).scatter_(-1, torch.topk(s2, 5, dim=-1).indices, 1.0)
+        se = s2 * (top + ball)
+        zero = se == 0
+        p = torch.softmax(se.masked_fill(zero, float("-inf")), dim=-1).masked_fill(zero, 0.0)
+        a2 = p / p.sum(dim=-1, keepdim=True)
+        (rs,) = torch.autograd.grad(a2, [s2], ga)
+        torch.testing.assert_close(a, a2, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(gs, rs, rtol=1e-4, atol=1e-5)
     # Down / Upsample 3x3 convolutions (bias-free in the reference; a bias checked too)
     for (B, Cin, N, H, W, bias) in [(2, 64, 32, 20, 24, False), (1, 128, 256, 16, 8, False), (2, 24, 40, 9, 13, True),
                                     (1, 512, 1024, 4, 6, False)]:

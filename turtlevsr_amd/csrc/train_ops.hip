@@ -636,6 +636,114 @@ __global__ __launch_bounds__(256) void l2n_bwd_kernel(const T* __restrict__ dy, 
   st8f(dx + p * lddx + c, g);
 }
 
+// ---------------------------------------------------------------------------------------------
+// StateAlignBlock score -> attention row (turtle_t1_arch.py:394-416 top-5, 448-464 L1 ball,
+// 115-132 clipped_softmax, as used in 585-599): per row i of s [R][n] (n keys, rows ordered (b, t,
+// i)), m_j = [j in top-5 of the row] + [|dy| + |dx| <= radius on the th x tw token grid] (0 / 1 / 2,
+// the reference's s * (top + ball)), se = s m, entries with se == 0 masked, a = softmax over the rest,
+// renormalised. One wave per row, NV keys per lane (j = lane + 64 q). Writes a (output dtype) and
+// a fp32 + m (uint8) for the backward ds_j = m_j a_j (da_j - sum_k da_k a_k) (the clipped softmax's
+// renormalisation and masks differentiated: train_ops._SabSoftmax).
+// ---------------------------------------------------------------------------------------------
+TURTLE_DEV float wave_max_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+TURTLE_DEV float wave_sum_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int NV, typename TO>
+__global__ __launch_bounds__(256) void sab_softmax_fwd_kernel(const float* __restrict__ s, int64_t R, int n, int tw, int radius,
+                                                              TO* __restrict__ a_out, float* __restrict__ a_save,
+                                                              uint8_t* __restrict__ m_save) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;                              // wave-uniform
+  const int i = (int)(r % n), qy = i / tw, qx = i - (i / tw) * tw;
+  const float* sr = s + r * n;
+  float v[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const int j = lane + 64 * q;
+    v[q] = j < n ? sr[j] : -INFINITY;
+  }
+  // top-5: five wave-wide arg-max rounds (largest value, lowest index on ties), the winner excluded
+  unsigned sel = 0;
+  for (int kk = 0; kk < 5 && kk < n; ++kk) {
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < NV; ++q) {
+      const int j = lane + 64 * q;
+      if (j < n && !((sel >> q) & 1u) && (v[q] > best || (v[q] == best && j < bi) || bi == 0x7fffffff)) { best = v[q]; bi = j; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    if (bi != 0x7fffffff && (bi & 63) == lane) sel |= 1u << (bi >> 6);
+  }
+  float se[NV], mk[NV];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const int j = lane + 64 * q;
+    const int ky = j / tw, kx = j - (j / tw) * tw;
+    const int dd = abs(ky - qy) + abs(kx - qx);
+    mk[q] = j < n ? (float)((sel >> q) & 1u) + (dd <= radius ? 1.f : 0.f) : 0.f;
+    se[q] = j < n ? v[q] * mk[q] : 0.f;
+    if (se[q] != 0.f) mx = fmaxf(mx, se[q]);
+  }
+  mx = wave_max_f(mx);
+  float e[NV], sum = 0.f;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    e[q] = se[q] != 0.f ? __expf(se[q] - mx) : 0.f;
+    sum += e[q];
+  }
+  sum = wave_sum_f(sum);
+  float ps = 0.f;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) { e[q] = e[q] / sum; ps += e[q]; }
+  ps = wave_sum_f(ps);
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const int j = lane + 64 * q;
+    if (j >= n) continue;
+    const float a = e[q] / ps;
+    a_out[r * n + j] = (TO)a;
+    a_save[r * n + j] = a;
+    m_save[r * n + j] = (uint8_t)(se[q] != 0.f ? mk[q] : 0.f);
+  }
+}
+template <int NV, typename TG>
+__global__ __launch_bounds__(256) void sab_softmax_bwd_kernel(const TG* __restrict__ da, const float* __restrict__ a_save,
+                                                              const uint8_t* __restrict__ m_save, int64_t R, int n,
+                                                              float* __restrict__ ds) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  float g[NV], a[NV], dot = 0.f;
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const int j = lane + 64 * q;
+    g[q] = j < n ? (float)da[r * n + j] : 0.f;
+    a[q] = j < n ? a_save[r * n + j] : 0.f;
+    dot = fmaf(g[q], a[q], dot);
+  }
+  dot = wave_sum_f(dot);
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    const int j = lane + 64 * q;
+    if (j < n) ds[r * n + j] = (float)m_save[r * n + j] * a[q] * (g[q] - dot);
+  }
+}
+
 // column sums db[n] = sum_p dy[p][n] (8 channels per thread, pixel lanes, LDS reduction, atomics)
 template <typename T>
 // square: sums of squares; dy2 != NULL: column dot products sum_p dy[p][n] dy2[p][n]
@@ -1107,6 +1215,32 @@ int l2n_bwd(const void* dy, int64_t lddy, const void* y, int64_t ldy, const floa
                      s, (T*)dx, lddx, P, C, img_px);
   return 0;
 }
+template <typename TO>
+int sab_softmax_fwd(const float* s, int64_t R, int n, int tw, int radius, void* a, float* a_save, uint8_t* m_save, hipStream_t st) {
+  const dim3 grid((unsigned)((R + 3) / 4));
+#define SSF(NVV) hipLaunchKernelGGL((sab_softmax_fwd_kernel<NVV, TO>), grid, dim3(256), 0, st, s, R, n, tw, radius, (TO*)a, a_save, m_save)
+  if (n <= 64) SSF(1);
+  else if (n <= 128) SSF(2);
+  else if (n <= 256) SSF(4);
+  else if (n <= 512) SSF(8);
+  else if (n <= 1024) SSF(16);
+  else return -1;
+#undef SSF
+  return 0;
+}
+template <typename TG>
+int sab_softmax_bwd(const void* da, const float* a_save, const uint8_t* m_save, int64_t R, int n, float* ds, hipStream_t st) {
+  const dim3 grid((unsigned)((R + 3) / 4));
+#define SSB(NVV) hipLaunchKernelGGL((sab_softmax_bwd_kernel<NVV, TG>), grid, dim3(256), 0, st, (const TG*)da, a_save, m_save, R, n, ds)
+  if (n <= 64) SSB(1);
+  else if (n <= 128) SSB(2);
+  else if (n <= 256) SSB(4);
+  else if (n <= 512) SSB(8);
+  else if (n <= 1024) SSB(16);
+  else return -1;
+#undef SSB
+  return 0;
+}
 // per-image Gram-backward weights (gram_wd_kernel)
 template <typename T>
 int gram_wd(const float* D, const float* aq, const float* ak, void* wd, int64_t B, int c, int heads, hipStream_t st) {
@@ -1296,6 +1430,18 @@ int turtle_train_l2n_bwd(const void* dy, int64_t lddy, const void* y, int64_t ld
       img_px <= 0 || P % img_px)
     return -1;
   TT_DISPATCH(dtype, l2n_bwd, dy, lddy, y, ldy, d, s, dx, lddx, P, C, img_px, (hipStream_t)stream);
+}
+
+int turtle_train_sab_softmax_fwd(const float* s, int64_t R, int n, int tw, int radius, void* a, float* a_save, void* m_save,
+                                 int dtype, void* stream) {
+  if (!s || !a || !a_save || !m_save || R <= 0 || n <= 0 || n > 1024 || tw <= 0 || n % tw || radius < 0) return -1;
+  TT_DISPATCH(dtype, sab_softmax_fwd, s, R, n, tw, radius, a, a_save, (uint8_t*)m_save, (hipStream_t)stream);
+}
+
+int turtle_train_sab_softmax_bwd(const void* da, const float* a_save, const void* m_save, int64_t R, int n, float* ds, int dtype,
+                                 void* stream) {
+  if (!da || !a_save || !m_save || !ds || R <= 0 || n <= 0 || n > 1024) return -1;
+  TT_DISPATCH(dtype, sab_softmax_bwd, da, a_save, (const uint8_t*)m_save, R, n, ds, (hipStream_t)stream);
 }
 
 int turtle_train_gram_wd(const float* D, const float* aq, const float* ak, void* wd, int64_t B, int c, int heads, int dtype,

@@ -24,6 +24,7 @@ base_model.py:340-365, dist_util.py:15-30) on the GPU:
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -33,6 +34,7 @@ import torch.nn.functional as F
 from .params import TurtleParams
 
 LN_EPS = 1e-5
+_ATEN_SAB = os.environ.get("TURTLE_TRAIN_ATEN_SAB") == "1"     # A/B only: the SAB softmax chain as torch ops
 L2_EPS = 1e-12
 SAB_TOPK = 5
 SAB_RADIUS = 4
@@ -376,6 +378,12 @@ class TrainGraph:
             vt = torch.cat([vc.to(vt.dtype), vt], dim=1)
         t = k.shape[1]
         s = (q @ k.transpose(-2, -1)) * m.temperature                   # [b, t, 1, n, n]
+        ops = self._ops()
+        if hasattr(ops, "sab_softmax") and not _ATEN_SAB:
+            a = ops.sab_softmax(s, tw, SAB_RADIUS)
+            o = self._undilated(a @ vt, b * t, c, hl, wl, ws, getattr(ops, "channels_last", False))
+            o = self._c1(m.project_out, o).reshape(b, t, c, hl, wl)
+            return o, k[:, -ntc:], vt[:, -ntc:]
         top = torch.zeros_like(s).scatter_(-1, torch.topk(s, SAB_TOPK, dim=-1).indices, 1.0)
         # s * top + s * ball as s * (top + ball): the same values bit for bit (factors 0 / 1 / 2 are
         # exact), one full-size pass fewer forward and backward

@@ -64,6 +64,8 @@ def lib():
     L.turtle_train_window_wgrad.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, ci, ci, ci, ci, ci, vp]
     L.turtle_train_conv3x3.argtypes = [vp, i64, vp, vp, vp, i64, i64, ci, ci, ci, ci, ci, vp]
     L.turtle_train_coldot.argtypes = [vp, i64, vp, i64, vp, i64, ci, i64, ci, vp]
+    L.turtle_train_sab_softmax_fwd.argtypes = [vp, i64, ci, ci, ci, vp, vp, vp, ci, vp]
+    L.turtle_train_sab_softmax_bwd.argtypes = [vp, vp, vp, i64, ci, vp, ci, vp]
     L.turtle_train_colscale.argtypes = [vp, i64, vp, vp, i64, i64, ci, i64, ci, vp]
     L.turtle_train_l2n_bwd.argtypes = [vp, i64, vp, i64, vp, vp, vp, i64, i64, ci, i64, ci, vp]
     L.turtle_train_conv3x3_wgrad_workspace.argtypes = [i64, ci, ci]
@@ -386,6 +388,37 @@ class _NormCols(torch.autograd.Function):
 
 
 L2N_EPS = 1e-12
+
+
+class _SabSoftmax(torch.autograd.Function):
+    """StateAlignBlock scores -> attention (turtle_t1_arch.py:585-599): top-5 mask + L1 ball (radius on
+    the th x tw token grid), s * (top + ball), clipped softmax (115-132), renormalised - one HIP kernel
+    each way (turtle_train_sab_softmax_*) in place of topk / scatter / masks / softmax / sum / div and their
+    backward. s fp32 [..., n] (last dim keys); a in ``out_dtype``."""
+
+    @staticmethod
+    def forward(ctx, s, tw: int, radius: int, out_dtype):
+        s = s.float().contiguous()
+        n = s.shape[-1]
+        R = s.numel() // n
+        a = torch.empty(s.shape, dtype=out_dtype, device=s.device)
+        a32 = torch.empty(s.shape, dtype=torch.float32, device=s.device)
+        m = torch.empty(s.shape, dtype=torch.uint8, device=s.device)
+        _check(lib().turtle_train_sab_softmax_fwd(_p(s), R, n, tw, radius, _p(a), _p(a32), _p(m), _dt(a), _stream(s)), "sab_softmax_fwd")
+        ctx.save_for_backward(a32, m)
+        return a
+
+    @staticmethod
+    def backward(ctx, da):
+        a32, m = ctx.saved_tensors
+        n = a32.shape[-1]
+        R = a32.numel() // n
+        da = da.contiguous()
+        if da.dtype not in (torch.float32, torch.bfloat16, torch.float16):
+            da = da.float()
+        ds = torch.empty(a32.shape, dtype=torch.float32, device=a32.device)
+        _check(lib().turtle_train_sab_softmax_bwd(_p(da), _p(a32), _p(m), R, n, _p(ds), _dt(da), _stream(da)), "sab_softmax_bwd")
+        return ds, None, None, None
 
 
 class _CrossGram(torch.autograd.Function):
@@ -724,6 +757,12 @@ class HipOps:
     def cross_gram(q, K):
         """[b, cq, cK] fp32: sum over each image's pixels of q[p]^T K[p] (channels-last q, K)."""
         return _CrossGram.apply(_act(q), _act(K))
+
+    @staticmethod
+    def sab_softmax(s, tw: int, radius: int):
+        """The StateAlignBlock's s * (top5 + ball) clipped softmax (fp32 s [..., n keys])."""
+        out = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else torch.float32
+        return _SabSoftmax.apply(s, tw, radius, out)
 
     @staticmethod
     def conv3x3(x, w, b=None):
