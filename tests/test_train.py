@@ -388,6 +388,36 @@ def test_hip_gelu_window_conv3x3_match_autograd(dtype):
         (rs,) = torch.autograd.grad(a2, [s2], ga)
         torch.testing.assert_close(a, a2, rtol=1e-5, atol=1e-6)
         torch.testing.assert_close(gs, rs, rtol=1e-4, atol=1e-5)
+    # GEMMs wider than 8192 output channels (the SAB A.v at ws = 16: D = 16384; the constant bias / scale
+    # vectors once stopped at 8192 channels)
+    from turtlevsr_amd.train_ops import _gemm_rows
+    x = torch.randn(32, 16, device=dev).to(dtype)
+    w = torch.randn(2, 16384, 16, device=dev).to(dtype)
+    y = _gemm_rows(x, w).float()
+    ref = torch.einsum("imk,ink->imn", x.float().view(2, 16, 16), w.float()).reshape(32, 16384)
+    torch.testing.assert_close(y, ref, rtol=tol["rtol"], atol=tol["atol"] * 10)
+    # the StateAlignBlock core on HIP (scores, top-5 + ball softmax, A.v) against the ATen formulation
+    n, tw, g, D, t = 64, 8, 32, 48, 3
+    q = torch.nn.functional.normalize(torch.randn(2, n, g, device=dev), dim=-1).requires_grad_()
+    K = torch.nn.functional.normalize(torch.randn(2, t, n, g, device=dev), dim=-1).requires_grad_()
+    VT = torch.randn(2, t, D, n, device=dev).requires_grad_()
+    temp = torch.full((1, 1, 1), 1.7, device=dev, requires_grad=True)
+    o = HipOps.sab_attention(q, K, VT, temp, tw, 4)
+    go = torch.randn_like(o)
+    gq, gK, gV, gt = torch.autograd.grad(o, [q, K, VT, temp], go)
+    q2, K2, V2, t2 = (x.detach().requires_grad_() for x in (q, K, VT, temp))
+    s2 = (q2[:, None] @ K2.transpose(-1, -2)) * t2
+    qi = torch.arange(n, device=dev)
+    ball = (((qi[:, None] // tw - qi[None, :] // tw).abs() + (qi[:, None] % tw - qi[None, :] % tw).abs()) <= 4).float()
+    top = torch.zeros_like(s2).scatter_(-1, torch.topk(s2, 5, dim=-1).indices, 1.0)
+    se = s2 * (top + ball)
+    zero = se == 0
+    p = torch.softmax(se.masked_fill(zero, float("-inf")), dim=-1).masked_fill(zero, 0.0)
+    o2 = (p / p.sum(dim=-1, keepdim=True)) @ V2.transpose(-1, -2)
+    rq, rK, rV, rt = torch.autograd.grad(o2, [q2, K2, V2, t2], go)
+    torch.testing.assert_close(o, o2, rtol=1e-4, atol=1e-4)
+    for a_, r_ in ((gq, rq), (gK, rK), (gV, rV), (gt, rt)):
+        torch.testing.assert_close(a_, r_, rtol=1e-3, atol=1e-3)
     # Down / Upsample 3x3 convolutions (bias-free in the reference; a bias checked too)
     for (B, Cin, N, H, W, bias) in [(2, 64, 32, 20, 24, False), (1, 128, 256, 16, 8, False), (2, 24, 40, 9, 13, True),
                                     (1, 512, 1024, 4, 6, False)]:

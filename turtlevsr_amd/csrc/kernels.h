@@ -4,6 +4,10 @@
 
 namespace turtle {
 
+// length of the constant zero / one vectors (GemmArgs.zeros / ones) that stand in for absent per-channel
+// bias / scale / LayerNorm vectors: the GEMM kernels read them at the output channel, so N <= this
+constexpr int TURTLE_CONST_VEC = 65536;
+
 // STORE_CB16: channel-blocked [C / 16][pixels][16] (cb_px pixels per block): the hidden map of a
 // GatedFeedForward whose depthwise + gate runs in dwgemm.hip reads one K step as contiguous rows
 enum StoreMode { STORE_NHWC = 0, STORE_SHUFFLE = 1, STORE_UNSHUFFLE = 2, STORE_CB16 = 3 };

@@ -1259,13 +1259,15 @@ static const float* train_consts(int which) {
   auto it = mem.find(dev);
   if (it == mem.end()) {
     float* p = nullptr;
-    if (hipMalloc(&p, (16384 + 8192) * sizeof(float)) != hipSuccess) return nullptr;
-    std::vector<float> h(16384 + 8192, 0.f);
-    for (int i = 16384; i < 16384 + 8192; ++i) h[i] = 1.f;
+    // zeros then ones, TURTLE_CONST_VEC each (the GEMMs read them at every output channel: a shorter
+    // ones vector gave wrong outputs past channel 8192)
+    if (hipMalloc(&p, 2 * (size_t)TURTLE_CONST_VEC * sizeof(float)) != hipSuccess) return nullptr;
+    std::vector<float> h(2 * (size_t)TURTLE_CONST_VEC, 0.f);
+    for (int i = TURTLE_CONST_VEC; i < 2 * TURTLE_CONST_VEC; ++i) h[i] = 1.f;
     if (hipMemcpy(p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
     it = mem.emplace(dev, p).first;
   }
-  return which ? it->second + 16384 : it->second;
+  return which ? it->second + TURTLE_CONST_VEC : it->second;
 }
 
 static int64_t rgemm_splits(int64_t P, int N, int K, int64_t img_px, int ntap = 1) {
@@ -1455,7 +1457,8 @@ int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride
                       int64_t ldy, int64_t P, int K, int N, int dtype, void* stream) {
   if (dtype != 0 && dtype != 1) return -1;
   if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !w || P <= 0 || K <= 0 || N <= 0 || K % 8 || N % 8 || ldx < K ||
-      ldy < N || (wstride && (img_px <= 0 || P % img_px)) || (img_px > 0 && img_px >= ((int64_t)1 << 31)))
+      ldy < N || (wstride && (img_px <= 0 || P % img_px)) || (img_px > 0 && img_px >= ((int64_t)1 << 31)) || N > TURTLE_CONST_VEC ||
+      K > TURTLE_CONST_VEC)
     return -1;
   GemmArgs g{};
   g.a.n = 1; g.a.Ktot = K;
@@ -1485,7 +1488,8 @@ int turtle_train_conv3x3(const void* x, int64_t ldx, const void* w, const float*
   if (dtype != 0 && dtype != 1) return -1;
   const int64_t P = B * H * W;
   if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !w || B <= 0 || H <= 0 || W <= 0 || Cin <= 0 || N <= 0 ||
-      Cin % 8 || N % 8 || ldx < Cin || ldy < N || (int64_t)H * W >= ((int64_t)1 << 31))
+      Cin % 8 || N % 8 || ldx < Cin || ldy < N || (int64_t)H * W >= ((int64_t)1 << 31) || N > TURTLE_CONST_VEC ||
+      9 * Cin > TURTLE_CONST_VEC)
     return -1;
   GemmArgs g{};
   g.a.n = 1; g.a.Ktot = 9 * Cin;

@@ -658,8 +658,8 @@ static void pack_all(TurtleHandle* h) {
     }
     M.blocks.push_back(bws);
   }
-  M.zeros = pk.f32(std::vector<double>(16384, 0.0));
-  M.ones = pk.f32(std::vector<double>(8192, 1.0));
+  M.zeros = pk.f32(std::vector<double>(TURTLE_CONST_VEC, 0.0));
+  M.ones = pk.f32(std::vector<double>(TURTLE_CONST_VEC, 1.0));
   pk.align();
   // same arch and dtype -> same packed size: repack in place, so device addresses (and launches
   // captured against them) stay valid across a weight update
@@ -767,6 +767,7 @@ struct Runner {
       TFAIL(TURTLE_EINVAL, "channel-blocked store needs the pn GEMM (M " + std::to_string(M) + " N " + std::to_string(g.N) +
                                " K " + std::to_string(a.Ktot) + " HW " + std::to_string(HW) + ")");
     if (g.ln && a.n != 1) TFAIL(TURTLE_EINVAL, "LN GEMM needs a single source");
+    if (g.N > TURTLE_CONST_VEC || a.Ktot > TURTLE_CONST_VEC) TFAIL(TURTLE_EINVAL, "GEMM wider than the constant vectors");
     // algorithmic traffic: A once (a 3x3 reads each input pixel once), W per weight set, out
     // (+ residual) once
     const double Ka = conv3 ? cin : a.Ktot;

@@ -185,6 +185,25 @@ class TrainGraph:
             return ops.conv3x3(x, w)
         return self._dense(x, w)
 
+    def _conv3_any(self, x, w, b):
+        """The stem / ending 3x3 convolutions (input_projection 975-978: 3 (6) -> dim, ending 1035-1041:
+        dim -> 3) on the op set's implicit-GEMM kernel with the channel counts zero-padded to multiples of
+        8 (a padded input copy of the image, zero weight rows / columns sliced off again), else F.conv2d."""
+        ops = self._ops()
+        if not hasattr(ops, "conv3x3"):
+            return self._dense(x, w, b)
+        n, ci = w.shape[0], w.shape[1]
+        n8, c8 = -(-n // 8) * 8, -(-ci // 8) * 8
+        if c8 != ci:
+            xp = torch.empty((x.shape[0], c8, x.shape[2], x.shape[3]), dtype=x.dtype, device=x.device,
+                             memory_format=torch.channels_last).zero_()
+            xp[:, :ci] = x
+            x = xp
+        wp = F.pad(w, (0, 0, 0, 0, 0, c8 - ci, 0, n8 - n)) if (c8 != ci or n8 != n) else w
+        bp = None if b is None else (F.pad(b, (0, n8 - n)) if n8 != n else b)
+        y = ops.conv3x3(x, wp, bp)
+        return y[:, :n] if n8 != n else y
+
     def _c1(self, m, x):                            # nn.Conv2d(K, N, 1): the op set's GEMM when it has one
         ops = self._ops()
         if hasattr(ops, "conv1x1"):
@@ -349,6 +368,13 @@ class TrainGraph:
         return t.reshape(b, c, ws, hh, ws, ww).permute(0, 3, 5, 2, 4, 1).reshape(b, 1, 1, hh * ww, ws * ws * c)
 
     @staticmethod
+    def _dilated_t(t, ws):
+        """_dilated transposed: [b, 1, ws*ws*c, (h w)] (value tokens as columns)."""
+        b, c, hl, wl = t.shape
+        hh, ww = hl // ws, wl // ws
+        return t.reshape(b, c, ws, hh, ws, ww).permute(0, 2, 4, 1, 3, 5).reshape(b, 1, ws * ws * c, hh * ww)
+
+    @staticmethod
     def _undilated(o, bt, c, hl, wl, ws, cl=False):
         """Inverse of _dilated; ``cl``: the same values as a channels-last [bt, c, hl, wl] tensor (one
         NHWC copy instead of an NCHW one the next GEMM would re-lay out)."""
@@ -372,6 +398,20 @@ class TrainGraph:
         n = th * tw
         q = _l2n(q, -1)
         k = _l2n(k, -1)
+        ops = self._ops()
+        if hasattr(ops, "sab_attention") and not _ATEN_SAB and n % 8 == 0 and g % 8 == 0 and (ws * ws * c) % 8 == 0:
+            # the values as transposed tokens [b, 1, D, n] (written so by the dilation copy; the cache views
+            # handed back are their [b, t, 1, n, D] transposes), scores / top-5 / softmax / A.v on HIP
+            vT = self._dilated_t(v, ws)
+            K = k.reshape(b, 1, n, g)
+            if kc is not None and vc is not None:
+                K = torch.cat([kc.reshape(b, -1, n, g).to(K.dtype), K], dim=1)
+                vT = torch.cat([vc.reshape(b, -1, n, ws * ws * c).transpose(-1, -2).to(vT.dtype), vT], dim=1)
+            t = K.shape[1]
+            o = ops.sab_attention(q.reshape(b, n, g), K, vT, m.temperature, tw, SAB_RADIUS)     # [b, t, n, D]
+            o = self._undilated(o, b * t, c, hl, wl, ws, getattr(ops, "channels_last", False))
+            o = self._c1(m.project_out, o).reshape(b, t, c, hl, wl)
+            return o, K[:, -ntc:].unsqueeze(2), vT[:, -ntc:].transpose(-1, -2).unsqueeze(2)
         vt = self._dilated(v, ws)
         if kc is not None and vc is not None:
             k = torch.cat([kc.to(k.dtype), k], dim=1)
@@ -488,7 +528,7 @@ class TrainGraph:
             current = x5[:, 1]
             img = torch.cat([x5[:, 0], x5[:, 1]], dim=1) if self.arch.use_both else current
         ip = self.input_projection
-        e1 = self._dense(img.float(), ip.weight, ip.bias)
+        e1 = self._conv3_any(img.float(), ip.weight, ip.bias)
         ks, vs = [], []
         e1, k, v = self._level("encoder_level1", e1, k_cached[0], v_cached[0]); ks.append(k); vs.append(v)
         # Downsample 136-144 / Upsample 146-154. On the channels-last op set the shuffled map is made
@@ -509,7 +549,7 @@ class TrainGraph:
         d1 = self._c1(self.reduce_chan_level1, torch.cat([up(self.up2_1, d2), e1], 1))
         d1, k, v = self._level("decoder_level1", d1, k_cached[7], v_cached[7]); ks.append(k); vs.append(v)
         r, _, _ = self._level("refinement", d1)
-        out = self._dense(r, self.ending.weight, self.ending.bias) + current
+        out = self._conv3_any(r, self.ending.weight, self.ending.bias) + current
         return out[:, :, :h, :w], ks, vs
 
 

@@ -390,6 +390,73 @@ class _NormCols(torch.autograd.Function):
 L2N_EPS = 1e-12
 
 
+def _gemm_rows(x2d, w3d, bias=None):
+    """y [P, N] = x2d [P, K] w3d[img]^T with one weight set per run of P / nimg rows (turtle_train_gemm)."""
+    P, K = x2d.shape
+    nimg, N, _ = w3d.shape
+    y = torch.empty(P, N, dtype=x2d.dtype, device=x2d.device)
+    _check(lib().turtle_train_gemm(_p(x2d), K, _p(w3d), N * K, P // nimg, _p(bias), _p(y), N, P, K, N, _dt(x2d), _stream(x2d)),
+           "gemm")
+    return y
+
+
+def _rgemm_rows(a2d, b2d, nimg):
+    """c [nimg, N, K] fp32 = sum over each image's rows of a2d[p]^T b2d[p] (turtle_train_rgemm)."""
+    P, N = a2d.shape
+    K = b2d.shape[1]
+    return _rgemm(a2d, N, b2d, K, P, N, K, P // nimg)
+
+
+class _SabAttn(torch.autograd.Function):
+    """The StateAlignBlock attention core (turtle_t1_arch.py:585-599) on the HIP kernels: s = q k^T per
+    frame (one GEMM with a weight set per (image, frame)), the top-5 + ball clipped softmax
+    (turtle_train_sab_softmax_*), o = a v (one GEMM with the per-frame values, held transposed [D, n]:
+    the dilated value tokens are written that way, so no operand is transposed in the forward);
+    backward: da = dO v^T and ds -> dq = ds k as GEMMs, dk = ds^T q and dv^T = dO^T a as reduction GEMMs
+    over the query rows. q [b, n, g], K [b, t, n, g], VT [b, t, D, n] (activation dtype), temperature
+    [1, 1, 1] -> o [b, t, n, D]."""
+
+    @staticmethod
+    def forward(ctx, q, K, VT, temp, tw: int, radius: int):
+        b, t, n, g = K.shape
+        D = VT.shape[2]
+        dt = K.dtype
+        q_rep = q.to(dt)[:, None].expand(b, t, n, g).reshape(b * t * n, g).contiguous()
+        Kc = K.contiguous()
+        VTc = VT.contiguous()
+        S = _gemm_rows(q_rep, Kc.view(b * t, n, g))                          # [btn, n] raw scores
+        sc = S.float() * temp.reshape(()).float()
+        a = torch.empty(b * t * n, n, dtype=dt, device=K.device)
+        a32 = torch.empty(b * t * n, n, dtype=torch.float32, device=K.device)
+        m = torch.empty(b * t * n, n, dtype=torch.uint8, device=K.device)
+        _check(lib().turtle_train_sab_softmax_fwd(_p(sc), b * t * n, n, tw, radius, _p(a), _p(a32), _p(m), _dt(a), _stream(K)),
+               "sab_softmax_fwd")
+        o = _gemm_rows(a, VTc.view(b * t, D, n))                             # [btn, D]
+        ctx.save_for_backward(q_rep, Kc, VTc, S, a, a32, m, temp)
+        ctx.dims, ctx.q_dt = (b, t, n, g, D), q.dtype
+        return o.view(b, t, n, D)
+
+    @staticmethod
+    def backward(ctx, dO):
+        q_rep, Kc, VTc, S, a, a32, m, temp = ctx.saved_tensors
+        b, t, n, g, D = ctx.dims
+        dt = Kc.dtype
+        R = b * t * n
+        dO = dO.to(dt).reshape(R, D).contiguous()
+        V = VTc.view(b * t, D, n).transpose(1, 2).contiguous()              # [bt, n, D]
+        da = _gemm_rows(dO, V)                                               # [R, n]
+        ds = torch.empty(R, n, dtype=torch.float32, device=dO.device)
+        _check(lib().turtle_train_sab_softmax_bwd(_p(da), _p(a32), _p(m), R, n, _p(ds), _dt(da), _stream(dO)), "sab_softmax_bwd")
+        tau = temp.reshape(()).float()
+        dtemp = (ds * S.float()).sum().reshape(temp.shape).to(temp.dtype)
+        dS = (ds * tau).to(dt)
+        KT = Kc.view(b * t, n, g).transpose(1, 2).contiguous()              # [bt, g, n]
+        dq = _gemm_rows(dS, KT).view(b, t, n, g).float().sum(1).to(ctx.q_dt)
+        dK = _rgemm_rows(dS, q_rep, b * t).view(b, t, n, g).to(dt)           # sum_i ds[i][j] q[i]
+        dVT = _rgemm_rows(dO, a, b * t).view(b, t, D, n).to(dt)               # sum_i dO[i][d] a[i][j]
+        return dq, dK, dVT, dtemp, None, None
+
+
 class _SabSoftmax(torch.autograd.Function):
     """StateAlignBlock scores -> attention (turtle_t1_arch.py:585-599): top-5 mask + L1 ball (radius on
     the th x tw token grid), s * (top + ball), clipped softmax (115-132), renormalised - one HIP kernel
@@ -757,6 +824,14 @@ class HipOps:
     def cross_gram(q, K):
         """[b, cq, cK] fp32: sum over each image's pixels of q[p]^T K[p] (channels-last q, K)."""
         return _CrossGram.apply(_act(q), _act(K))
+
+    @staticmethod
+    def sab_attention(q, K, VT, temp, tw: int, radius: int):
+        """StateAlignBlock core: q [b, n, g], K [b, t, n, g], VT [b, t, D, n] -> a v [b, t, n, D] with a the
+        top-5 + ball clipped softmax of q k^T * temp (n, g, D multiples of 8)."""
+        dt = torch.get_autocast_dtype("cuda") if torch.is_autocast_enabled("cuda") else K.dtype
+        gdt = _gemm_dt(torch.empty(0, dtype=dt))        # fp16 autocast: the GEMMs take bf16 (as _Conv1x1)
+        return _SabAttn.apply(q, K.to(gdt), VT.to(gdt), temp, tw, radius).to(dt)
 
     @staticmethod
     def sab_softmax(s, tw: int, radius: int):
