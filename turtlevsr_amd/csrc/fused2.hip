@@ -598,7 +598,11 @@ void launch_fused2(const FusedArgs& a, hipStream_t st) {
         case 3: f2_launch<F_DWONLY, 64, 18, 4, 0, 4>(a, st); break;
         case 4: f2_launch<F_DWONLY, 64, 21, 4, 0, 3>(a, st); break;
         case 5: f2_launch<F_DWONLY, 64, 15, 4, 0, 4, 2>(a, st); break;
-        default: f2_launch<F_DWONLY, 64, 12, 4, 0, 4>(a, st);
+        default:
+          // N1 <= 192 (qkv / the CHM kv over its aligned frames): taller tiles, 3 waves per SIMD (L1 kv x3
+          // 905 -> 831 us, qkv unchanged: profiles/r05r_f2bench_sweep.log); wider maps keep R = 12
+          if (a.N1 <= 192) f2_launch<F_DWONLY, 64, 21, 4, 0, 3>(a, st);
+          else f2_launch<F_DWONLY, 64, 12, 4, 0, 4>(a, st);
       }
     } else {
       switch (v) {
