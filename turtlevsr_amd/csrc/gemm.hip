@@ -586,6 +586,8 @@ void launch_gemm(const GemmArgs& g, hipStream_t st) {
     if (gemm_lds_ok(g)) { launch_gemm_lds(g, st); return; }
     if (panel_ok(g)) { launch_panel_any(g, st); return; }
   }
+  if constexpr (sizeof(T) == 4)
+    if (gemm_f32_preferred(g)) { launch_gemm_f32(g, st); return; }
   // BN = 128 when it tiles N exactly (or N is large), else 64 (N = 64, 192, 320, tiny widths)
   const bool wide = g.N >= 128 && (g.N % 128 == 0 || g.N > 1024);
   if (wide) launch_cfg<T, 128, 128>(g, st);

@@ -47,8 +47,12 @@ struct GemmArgs {
   int allow_g8;                    // 256 x 256 four-phase kernel permitted (turtle_set_option "gemm8")
   int kt_max_px;                   // GEMMs over fewer pixels go to the 2-D tiled kernel (0: 32768)
   int allow_g9;                    // 256 x 256 four-wave kernel permitted (turtle_set_option "gemm9")
+  int allow_f32;                   // fp32 occupancy-tiled kernel permitted (turtle_set_option "gemm_f32")
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
+bool gemm_f32_ok(const GemmArgs& g);                              // gemm_f32.hip (fp32)
+bool gemm_f32_preferred(const GemmArgs& g);
+void launch_gemm_f32(const GemmArgs& g, hipStream_t st);
 bool gemm_lds_ok(const GemmArgs& g);                              // gemm2.hip (bf16)
 void launch_gemm_lds(const GemmArgs& g, hipStream_t st);
 bool gemm_pn_ok(const GemmArgs& g);                               // gemm3.hip (bf16)

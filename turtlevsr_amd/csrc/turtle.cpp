@@ -323,6 +323,7 @@ struct TurtleHandle {
   bool gemm_pn = true;                                // resident-panel bf16 GEMM, K <= 512 (gemm3.hip)
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
+  bool gemm_f32 = true;                               // fp32 occupancy-tiled GEMM (gemm_f32.hip)
   int kt_max_px = 32768;                              // below this many pixels the 2-D tiled GEMM takes every shape it can
   int sab_waves = 0;                                  // waves per SAB score block: 4 (64 queries), 8 (128), 0 = 8 at
                                                       // d >= 256, else 4 (tools/sabbench, profiles/r04_sabbench_waves.log)
@@ -757,7 +758,7 @@ struct Runner {
     g.res = res; g.ldr = ldr; g.offr = offr;
     g.out = out; g.ldo = ldo; g.offo = offo; g.store_mode = store; g.cb_px = store == STORE_CB16 ? M : 0;
     g.zeros = h->fptr(h->mw.zeros); g.ones = h->fptr(h->mw.ones); g.allow_panel = h->panel; g.allow_lds = h->gemm_lds; g.allow_pn = h->gemm_pn;
-    g.allow_ar = h->gemm_ar; g.allow_kt = h->gemm_kt; g.kt_max_px = h->kt_max_px;
+    g.allow_ar = h->gemm_ar; g.allow_kt = h->gemm_kt; g.allow_f32 = h->gemm_f32; g.kt_max_px = h->kt_max_px;
     // channel-blocked stores: the pn GEMM, or gemm8 when every projection may take it (eligibility
     // tested on a copy; g.allow_g8 is set in one place, below)
     GemmArgs g8t = g;
@@ -1607,6 +1608,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm_pn") h->gemm_pn = value != 0;
     else if (n == "gemm_ar") h->gemm_ar = value != 0;
     else if (n == "gemm_kt") h->gemm_kt = value != 0;
+    else if (n == "gemm_f32") h->gemm_f32 = value != 0;
     else if (n == "gemm8") h->gemm8 = (int)value;
     else if (n == "gemm8_ps") h->gemm8_ps = value != 0;
     else if (n == "gemm9") h->gemm9 = (int)value;
