@@ -117,6 +117,29 @@ int main(int argc, char** argv) {
     const float t_gm = time_it([&] { launch_gemm<bf16>(gm, 0); }, reps);
     printf("%s: P=%lld K=%d N=%d  max|dwgemm - (dw+gemm)| %.4g (max |update| %.3g)  dw %.1f us + gemm %.1f us = %.1f us\n",
            sh.tag, (long long)P, K, N, md, mx, t_dw, t_gm, t_dw + t_gm);
+    // the channel-blocked hidden map of the frame (STORE_CB16: [2K / 16][P][16], x2 blocks after x1's)
+    {
+      std::vector<uint16_t> hcb(hin.size());
+      for (int64_t p = 0; p < P; ++p)
+        for (int c = 0; c < 2 * K; ++c) hcb[((size_t)(c / 16) * P + p) * 16 + c % 16] = hin[p * 2 * K + c];
+      void* dcb;
+      CK(hipMalloc(&dcb, hcb.size() * 2));
+      CK(hipMemcpy(dcb, hcb.data(), hcb.size() * 2, hipMemcpyHostToDevice));
+      DwGemmArgs c = a;
+      c.in = dcb; c.cb_px = P; c.ldi = 0; c.offi = 0;
+      {
+        reset();
+        launch_dwgemm(c, 0);
+        CK(hipDeviceSynchronize());
+        CK(hipMemcpy(o2.data(), dx, o2.size() * 2, hipMemcpyDeviceToHost));
+        double mc = 0;
+        for (size_t i = 0; i < o1.size(); ++i) mc = std::max(mc, (double)fabsf(bf2f(o1[i]) - bf2f(o2[i])));
+        const float t_cb = time_it([&] { launch_dwgemm(c, 0); }, reps);
+        const float t_px = time_it([&] { launch_dwgemm(a, 0); }, reps);
+        printf("  channel-blocked input %.1f us (max|d| vs pixel-major %.3g), pixel-major %.1f us\n", t_cb, mc, t_px);
+      }
+      CK(hipFree(dcb));
+    }
     const int dbgs[] = {0, 1, 2, 3, 4, 8, 12, 16, 4 | 8 | 16, 1 | 2 | 16, 1 | 2 | 4 | 8 | 16};
     for (int dbg : dbgs) {
       if (only >= 0 && dbg) continue;
