@@ -18,7 +18,7 @@ REPO = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 OBJ = os.path.join(PKG, "build")
 LIB = os.path.join(PKG, "lib", "libturtle_hip.so")
-SOURCES = ["gemm.hip", "gemm2.hip", "gemm3.hip", "gemm5.hip", "spatial.hip", "attn.hip", "sab.hip", "fused.hip", "fused2.hip", "dwgemm.hip", "tilepd.hip", "gemm8.hip", "gemm9.hip", "gemm_f32.hip", "ffn.hip", "t0.hip", "train_ops.hip", "turtle.cpp"]
+SOURCES = ["gemm.hip", "gemm2.hip", "gemm3.hip", "gemm5.hip", "spatial.hip", "attn.hip", "sab.hip", "fused.hip", "fused2.hip", "dwgemm.hip", "tilepd.hip", "gemm8.hip", "gemm9.hip", "gemm_f32.hip", "gemm_sk.hip", "ffn.hip", "t0.hip", "train_ops.hip", "turtle.cpp"]
 ARCH = os.environ.get("TURTLE_OFFLOAD_ARCH", "gfx950")
 
 

@@ -493,16 +493,20 @@ static void g9_launch(const GemmArgs& g, float2* sp, hipStream_t st) {
 // g.allow_g9: 1 the measured choice per shape; 2..6 a fixed variant (tools/g9bench):
 // 2 BN 256 register-staged, 3 BN 128 register-staged, 4 BN 256 DMA ring 4, 5 BN 128 DMA ring 3,
 // 6 BN 256 DMA ring 3
+// per-pixel (mu, rstd) of the LN source a.s[0] (K in {256, 512, 1024}) into sp[M]; also the split-K
+// GEMM's statistics (gemm_sk.hip)
+void launch_ln_stats(const GemmArgs& g, float2* sp, hipStream_t st) {
+  const SrcDesc& s = g.a.s[0];
+  const bf16* x = reinterpret_cast<const bf16*>(s.base);
+  const dim3 gs((unsigned)((g.M + 31) / 32));
+  if (g.a.Ktot == 256) hipLaunchKernelGGL((ln_stats_kernel<256>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
+  else if (g.a.Ktot == 512) hipLaunchKernelGGL((ln_stats_kernel<512>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
+  else hipLaunchKernelGGL((ln_stats_kernel<1024>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
+}
+
 void launch_gemm9(const GemmArgs& g, void* stats, hipStream_t st) {
   float2* sp = reinterpret_cast<float2*>(stats);
-  if (g.ln) {
-    const SrcDesc& s = g.a.s[0];
-    const bf16* x = reinterpret_cast<const bf16*>(s.base);
-    const dim3 gs((unsigned)((g.M + 31) / 32));
-    if (g.a.Ktot == 256) hipLaunchKernelGGL((ln_stats_kernel<256>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
-    else if (g.a.Ktot == 512) hipLaunchKernelGGL((ln_stats_kernel<512>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
-    else hipLaunchKernelGGL((ln_stats_kernel<1024>), gs, dim3(256), 0, st, x, s.ld, s.off, g.M, sp);
-  }
+  if (g.ln) launch_ln_stats(g, sp, st);
   int v = g.allow_g9;
   if (v == 1) {
     // 256 channels on the LDS-DMA ring wherever every CU still gets a tile (the A panel is read

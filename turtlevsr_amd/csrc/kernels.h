@@ -51,6 +51,11 @@ struct GemmArgs {
 };
 template <typename T> void launch_gemm(const GemmArgs& g, hipStream_t st);
 bool gemm_f32_ok(const GemmArgs& g);                              // gemm_f32.hip (fp32)
+bool gemm_sk_ok(const GemmArgs& g);                               // gemm_sk.hip (bf16 split-K, small frames)
+int gemm_sk_splits(int64_t M, int N, int K);
+size_t gemm_sk_workspace_bytes(int64_t M, int N, int K);
+void launch_gemm_sk(const GemmArgs& g, void* ws, hipStream_t st);
+void launch_ln_stats(const GemmArgs& g, float2* stats, hipStream_t st);   // gemm9.hip
 bool gemm_f32_preferred(const GemmArgs& g);
 void launch_gemm_f32(const GemmArgs& g, hipStream_t st);
 bool gemm_lds_ok(const GemmArgs& g);                              // gemm2.hip (bf16)

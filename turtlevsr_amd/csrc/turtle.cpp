@@ -324,6 +324,7 @@ struct TurtleHandle {
   bool gemm_ar = true;                                // A-resident per-panel bf16 GEMM, K 256..1280 (gemm3.hip)
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
   bool gemm_f32 = true;                               // fp32 occupancy-tiled GEMM (gemm_f32.hip)
+  bool gemm_sk = true;                                // split-K bf16 GEMM for the small-frame wide projections (gemm_sk.hip)
   int kt_max_px = 32768;                              // below this many pixels the 2-D tiled GEMM takes every shape it can
   int sab_waves = 0;                                  // waves per SAB score block: 4 (64 queries), 8 (128), 0 = 8 at
                                                       // d >= 256, else 4 (tools/sabbench, profiles/r04_sabbench_waves.log)
@@ -674,6 +675,9 @@ static void pack_all(TurtleHandle* h) {
 // ------------------------------------------------------------------------------------------
 // frame driver
 // ------------------------------------------------------------------------------------------
+// the split-K GEMM (gemm_sk.hip) takes the wide projections of frames up to this many pixels per GEMM
+constexpr int64_t kSkMaxPx = 4096;
+
 struct Arena {
   char* base;
   size_t cap, off = 0, peak = 0;
@@ -747,7 +751,13 @@ struct Runner {
     // per-pixel LayerNorm statistics of the gemm9 kernel (gemm9.hip): workspace reserved by shape only,
     // so sizing - which runs without packed weights - and every switch setting reserve the same bytes
     const bool g9_ws = ES == 2 && w.ln && a.n == 1 && !conv3 && (a.Ktot == 256 || a.Ktot == 512 || a.Ktot == 1024);
+    const size_t mark = ar.off;                     // this GEMM's workspace: released after its launch (one stream)
     float* st9 = g9_ws ? fbuf(2 * M) : nullptr;
+    // split-K partials of the small-frame wide projections (gemm_sk.hip), reserved by shape only too
+    const int Nn = N >= 0 ? N : w.N;
+    const bool sk_ws = ES == 2 && M <= kSkMaxPx && a.n == 1 && !conv3 && a.Ktot % 64 == 0 && Nn % 8 == 0 && Nn > 0;
+    void* wsk = sk_ws ? ar.alloc(gemm_sk_workspace_bytes(M, Nn, a.Ktot)) : nullptr;
+    struct Release { Arena& a; size_t m; ~Release() { a.off = m; } } release{ar, mark};
     if (dry()) return;
     GemmArgs g{};
     g.a = a; g.M = M; g.N = N >= 0 ? N : w.N; g.HW = HW; g.Wimg = Wimg;
@@ -800,10 +810,21 @@ struct Runner {
         g.allow_g9 = 1;
       }
     }
-    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s%s%s%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
-        res != nullptr, store, a.n, a.cb_px ? " cb" : "", lt ? " wide" : "", g.allow_g8 ? " g8" : "", use9 ? " g9" : "");
+    // small frames (<= kSkMaxPx pixels): the deep-K wide projections (K >= 1024: the latent project_out)
+    // on the split-K kernel (gemm_sk.hip), whose 64 x 64 tiles x K splits fill the chip where a 256-row
+    // tile gives a handful of blocks (256x256 frame: 36 -> 18 us per launch); at K <= 640 its partial
+    // round trip costs more than it gains (M = 1024, N = 2560: 26 -> 43 us; profiles/r05sk2_*)
+    bool use_sk = false;
+    if (ES == 2 && h->gemm_sk && lt && wsk && !g.allow_g8 && a.Ktot >= 1024 && gemm_sk_ok(g)) {
+      use_sk = true;
+      use9 = false;
+    }
+    tag("gemm M=%lld N=%d K=%d conv3=%d ln=%d res=%d store=%d nsrc=%d%s%s%s%s%s", (long long)M, g.N, a.Ktot, conv3, g.ln,
+        res != nullptr, store, a.n, a.cb_px ? " cb" : "", lt ? " wide" : "", g.allow_g8 ? " g8" : "", use9 ? " g9" : "",
+        use_sk ? " sk" : "");
     launch(TURTLE_K_GEMM, bytes, 2.0 * M * g.N * a.Ktot, [&] {
-      if (use9) launch_gemm9(g, st9, st);
+      if (use_sk) launch_gemm_sk(g, wsk, st);
+      else if (use9) launch_gemm9(g, st9, st);
       else launch_gemm<T>(g, st);
     });
   }
@@ -1609,6 +1630,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm_ar") h->gemm_ar = value != 0;
     else if (n == "gemm_kt") h->gemm_kt = value != 0;
     else if (n == "gemm_f32") h->gemm_f32 = value != 0;
+    else if (n == "gemm_sk") h->gemm_sk = value != 0;
     else if (n == "gemm8") h->gemm8 = (int)value;
     else if (n == "gemm8_ps") h->gemm8_ps = value != 0;
     else if (n == "gemm9") h->gemm9 = (int)value;
