@@ -136,7 +136,8 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
  *   "gemm_lds"     [1] LDS-pipelined GEMM (fallback where the kernels above do not apply)
  *   "panel_gemm"   [1] register-panel GEMM fallback; 0: K-loop GEMM
  *   "gemm_f32"     [1] fp32 GEMM on an LDS-DMA ring (gemm_f32.hip) for the LN / GELU / multi-source fp32 GEMMs
- *   "gemm_sk"      [1] split-K GEMM (gemm_sk.hip) for the deep-K wide projections of frames <= 4096 pixels per GEMM
+ *   "gemm_sk"      [1] split-K GEMM (gemm_sk.hip): single-source projections of GEMMs over <= sk_max_px pixels
+ *   "sk_max_px"    [4096] ... its pixel limit (set before the workspace is sized)
  *   "gemm9"        [1] 256-pixel-row GEMM (gemm9.hip): 1 the 'wide' projection class (latent LN projections, project_out
  *                  K = 1280, latent / level-3 W_eff; hipBLASLt until round 4 - the library links no vendor GEMM now),
  *                  2 every eligible projection, 0 never

@@ -5,6 +5,9 @@
 //   partial[s][m][n] = sum_{k in chunk s} A[m][k] W[n][k]            gemm_sk_kernel (fp32 workspace)
 //   out[m][n] = epi( sum_s partial[s][m][n] )                        gemm_sk_epi_kernel
 //
+// (with >= 256 tiles of 64 x 64 there is one split and gemm_sk_kernel applies the epilogue itself: a
+// small-tile GEMM for the shapes whose 256-row tiles would give a few dozen blocks)
+//
 // with epi the GEMM family's epilogue (LayerNorm correction rs (acc - mu s[n]) + t[n] from the
 // per-pixel statistics of ln_stats_kernel (gemm9.hip), + bias, GELU, * scale, + residual). The splits
 // are summed in a fixed order: results are bitwise repeatable (no atomics).
@@ -24,7 +27,8 @@ __device__ __attribute__((aligned(64))) uint4 g_zero_sk[4];
 
 constexpr int SK_BM = 64, SK_BN = 64, SK_BK = 64, SK_ROWB = SK_BK * 2 + 16;
 
-__global__ __launch_bounds__(256) void gemm_sk_kernel(GemmArgs g, int kchunk, float* __restrict__ part) {
+template <bool FUSED>
+__global__ __launch_bounds__(256) void gemm_sk_kernel(GemmArgs g, int kchunk, float* __restrict__ part, const float2* __restrict__ stats) {
   typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
   __shared__ __attribute__((aligned(16))) char smem[(SK_BM + SK_BN) * SK_ROWB];
   char* sX = smem;
@@ -96,11 +100,37 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmArgs g, int kchunk, fl
   for (int tm = 0; tm < 2; ++tm) {
     const int64_t m = m0 + wm * 32 + 16 * tm + fr;
     if (m >= g.M) continue;
+    float mu = 0.f, rs = 1.f;
+    if (FUSED && g.ln) { const float2 st = stats[m]; mu = st.x; rs = st.y; }
 #pragma unroll
     for (int tn = 0; tn < 2; ++tn) {
       const int n = n0 + wn * 32 + 16 * tn + 4 * fq;
       if (n >= g.N) continue;                       // N % 8 == 0: 4 channels all in or all out
-      *reinterpret_cast<f32x4*>(part + ((int64_t)split * g.M + m) * g.N + n) = acc[tm][tn];
+      if constexpr (!FUSED) {
+        *reinterpret_cast<f32x4*>(part + ((int64_t)split * g.M + m) * g.N + n) = acc[tm][tn];
+      } else {                                      // one split: the epilogue here (as gemm_sk_epi_kernel)
+        const f32x4 vs = *reinterpret_cast<const f32x4*>((g.ln_s ? g.ln_s : g.zeros) + n);
+        const f32x4 vt = *reinterpret_cast<const f32x4*>((g.ln_t ? g.ln_t : g.zeros) + n);
+        const f32x4 vb = *reinterpret_cast<const f32x4*>((g.bias ? g.bias : g.zeros) + n);
+        const f32x4 vc = *reinterpret_cast<const f32x4*>((g.scale ? g.scale : g.ones) + n);
+        float r[4] = {0.f, 0.f, 0.f, 0.f};
+        if (g.res) {
+          const uint2 q = ld8(reinterpret_cast<const bf16*>(g.res) + m * g.ldr + g.offr + n);
+          r[0] = __uint_as_float(q.x << 16); r[1] = __uint_as_float(q.x & 0xffff0000u);
+          r[2] = __uint_as_float(q.y << 16); r[3] = __uint_as_float(q.y & 0xffff0000u);
+        }
+        typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+        bf16x4 ov;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = acc[tm][tn][e];
+          if (g.ln) x = rs * (x - mu * vs[e]);
+          x += vt[e] + vb[e];
+          if (g.gelu) x = gelu_bf16(x);
+          ov[e] = (bf16)(x * vc[e] + r[e]);
+        }
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(g.out) + m * g.ldo + g.offo + n) = ov;
+      }
     }
   }
 }
@@ -154,6 +184,7 @@ __global__ __launch_bounds__(256) void gemm_sk_epi_kernel(GemmArgs g, int nsplit
 // function: the frame driver reserves the workspace in its sizing pass from it)
 int gemm_sk_splits(int64_t M, int N, int K) {
   const int64_t tiles = ((M + SK_BM - 1) / SK_BM) * ((N + SK_BN - 1) / SK_BN);
+  if (tiles >= 256) return 1;                      // every CU has a tile: no split, epilogue fused
   int s = (int)std::max<int64_t>(1, (1024 + tiles - 1) / tiles);
   s = std::min(s, K / SK_BK);
   while (s > 1 && (K / SK_BK) % s) --s;           // equal chunks of whole K tiles
@@ -186,7 +217,11 @@ void launch_gemm_sk(const GemmArgs& g, void* ws, hipStream_t st) {
   float2* stats = reinterpret_cast<float2*>(part + (size_t)S * g.M * g.N);
   if (g.ln) launch_ln_stats(g, stats, st);
   const int64_t tiles = ((g.M + SK_BM - 1) / SK_BM) * ((g.N + SK_BN - 1) / SK_BN);
-  hipLaunchKernelGGL(gemm_sk_kernel, dim3((unsigned)(tiles * S)), dim3(256), 0, st, g, K / S, part);
+  if (S == 1) {
+    hipLaunchKernelGGL(gemm_sk_kernel<true>, dim3((unsigned)tiles), dim3(256), 0, st, g, K, part, stats);
+    return;
+  }
+  hipLaunchKernelGGL(gemm_sk_kernel<false>, dim3((unsigned)(tiles * S)), dim3(256), 0, st, g, K / S, part, stats);
   const int64_t n = g.M * (g.N / 8);
   hipLaunchKernelGGL(gemm_sk_epi_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, S, part, stats);
 }

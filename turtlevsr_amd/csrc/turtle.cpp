@@ -325,6 +325,7 @@ struct TurtleHandle {
   bool gemm_kt = true;                                // 2-D tiled deep-ring bf16 GEMM (gemm5.hip)
   bool gemm_f32 = true;                               // fp32 occupancy-tiled GEMM (gemm_f32.hip)
   bool gemm_sk = true;                                // split-K bf16 GEMM for the small-frame wide projections (gemm_sk.hip)
+  int64_t sk_max_px = 4096;                           // ... for GEMMs over at most this many pixels (set before sizing the workspace)
   int kt_max_px = 32768;                              // below this many pixels the 2-D tiled GEMM takes every shape it can
   int sab_waves = 0;                                  // waves per SAB score block: 4 (64 queries), 8 (128), 0 = 8 at
                                                       // d >= 256, else 4 (tools/sabbench, profiles/r04_sabbench_waves.log)
@@ -675,9 +676,6 @@ static void pack_all(TurtleHandle* h) {
 // ------------------------------------------------------------------------------------------
 // frame driver
 // ------------------------------------------------------------------------------------------
-// the split-K GEMM (gemm_sk.hip) takes the wide projections of frames up to this many pixels per GEMM
-constexpr int64_t kSkMaxPx = 4096;
-
 struct Arena {
   char* base;
   size_t cap, off = 0, peak = 0;
@@ -755,7 +753,7 @@ struct Runner {
     float* st9 = g9_ws ? fbuf(2 * M) : nullptr;
     // split-K partials of the small-frame wide projections (gemm_sk.hip), reserved by shape only too
     const int Nn = N >= 0 ? N : w.N;
-    const bool sk_ws = ES == 2 && M <= kSkMaxPx && a.n == 1 && !conv3 && a.Ktot % 64 == 0 && Nn % 8 == 0 && Nn > 0;
+    const bool sk_ws = ES == 2 && M <= h->sk_max_px && a.n == 1 && !conv3 && a.Ktot % 64 == 0 && Nn % 8 == 0 && Nn > 0;
     void* wsk = sk_ws ? ar.alloc(gemm_sk_workspace_bytes(M, Nn, a.Ktot)) : nullptr;
     struct Release { Arena& a; size_t m; ~Release() { a.off = m; } } release{ar, mark};
     if (dry()) return;
@@ -810,12 +808,15 @@ struct Runner {
         g.allow_g9 = 1;
       }
     }
-    // small frames (<= kSkMaxPx pixels): the deep-K wide projections (K >= 1024: the latent project_out)
-    // on the split-K kernel (gemm_sk.hip), whose 64 x 64 tiles x K splits fill the chip where a 256-row
-    // tile gives a handful of blocks (256x256 frame: 36 -> 18 us per launch); at K <= 640 its partial
-    // round trip costs more than it gains (M = 1024, N = 2560: 26 -> 43 us; profiles/r05sk2_*)
+    // small frames (<= sk_max_px pixels): single-source projections on the split-K kernel (gemm_sk.hip),
+    // whose 64 x 64 tiles (x K splits) fill the chip where 256-row or panel tiles give a handful of
+    // blocks - unsplit (epilogue in the kernel) wherever that gives >= 256 tiles, split only for the
+    // K >= 1024 wide projections (the latent project_out of a 256x256 frame: 36 -> 18 us); split at
+    // K <= 640 its partial round trip costs more than it gains (M = 1024, N = 2560 split in two: 26 ->
+    // 43 us, unsplit 20.6 us; profiles/r05sk2_*, r05sk4_*)
     bool use_sk = false;
-    if (ES == 2 && h->gemm_sk && lt && wsk && !g.allow_g8 && a.Ktot >= 1024 && gemm_sk_ok(g)) {
+    const bool sk_one = wsk && gemm_sk_splits(M, g.N, a.Ktot) == 1;
+    if (ES == 2 && h->gemm_sk && wsk && !g.allow_g8 && ((lt && a.Ktot >= 1024) || sk_one) && gemm_sk_ok(g)) {
       use_sk = true;
       use9 = false;
     }
@@ -1631,6 +1632,7 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "gemm_kt") h->gemm_kt = value != 0;
     else if (n == "gemm_f32") h->gemm_f32 = value != 0;
     else if (n == "gemm_sk") h->gemm_sk = value != 0;
+    else if (n == "sk_max_px") h->sk_max_px = value;
     else if (n == "gemm8") h->gemm8 = (int)value;
     else if (n == "gemm8_ps") h->gemm8_ps = value != 0;
     else if (n == "gemm9") h->gemm9 = (int)value;
