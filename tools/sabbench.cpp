@@ -30,7 +30,7 @@ int main(int argc, char** argv) {
   const int waves = argc > 3 ? atoi(argv[3]) : 4;    // ./sabbench reps nsplit(0: default) waves
   const int th = 68, tw = 120, N = th * tw;
   const int ds[] = {128, 256, 512}, Ts[] = {3, 4, 4};
-  const int dbgs[] = {0, 1, 3, 7};
+  const int dbgs[] = {0, 1, 2, 3, 4, 7};
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   srand(1);
