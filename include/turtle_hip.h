@@ -130,6 +130,9 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
  *   "fuse_fp32"    [0] ... also in the fp32 build (the round-1 fused.hip kernel; 0: GEMM + depthwise + GEMM, faster)
  *   "fused2"       [1] the bf16 row-walk fused kernel (fused2.hip); 0: the round-1 fused.hip kernel
  *   "ffn"          [1] FeedForward in one kernel (ffn.hip) at widths 64 / 128 (bf16)
+ *   "gffn"         [1] GatedFeedForward in one kernel at width 256 (gffn.hip: LN -> project_in -> dwconv -> gelu gate ->
+ *                  project_out + residual, the hidden map never in HBM; bf16); 0: pn GEMM + dwgemm
+ *   "gffn_min_blocks" [256] minimum tile count for a gffn launch (one block per CU)
  *   "gemm_pn"      [1] persistent resident-panel GEMM for LN-folded 1x1 convolutions, K <= 512
  *   "gemm_ar"      [1] A-resident per-panel GEMM for the K = 256 residual projections
  *   "gemm_kt"      [1] 2-D tiled deep-ring GEMM (3x3 up/down convolutions, K >= 640, small maps)
@@ -139,7 +142,7 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
  *   "gemm_sk"      [1] split-K GEMM (gemm_sk.hip): single-source projections of GEMMs over <= sk_max_px pixels
  *   "sk_max_px"    [4096] ... its pixel limit (set before the workspace is sized)
  *   "gemm9"        [1] 256-pixel-row GEMM (gemm9.hip): 1 the 'wide' projection class (latent LN projections, project_out
- *                  K = 1280, latent / level-3 W_eff; hipBLASLt until round 4 - the library links no vendor GEMM now),
+ *                  K = 1280, latent / level-3 W_eff),
  *                  2 every eligible projection, 0 never
  *   "gemm8"        [3] 256 x 256 four-phase GEMM (gemm8.hip): 1 the 'wide' class, 2 every eligible projection,
  *                  3 the multi-source projections with K >= 1024 (where it measures fastest), 0 never
@@ -168,6 +171,10 @@ int turtle_profile_filter(TurtleHandle* h, const char* tag);
 int turtle_set_option(TurtleHandle* h, const char* name, int value);
 
 const char* turtle_last_error(void);
+
+/* Hash of the kernel sources (turtlevsr_amd/csrc + build.py, turtlevsr_amd/build.py source_hash) the
+ * library was built from: the Python binding refuses a library whose hash is not the tree's. */
+const char* turtle_source_hash(void);
 
 #ifdef __cplusplus
 }

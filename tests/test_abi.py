@@ -37,6 +37,20 @@ def test_exports_match_header():
         assert hasattr(L, s)
 
 
+def test_library_is_built_from_this_tree(monkeypatch):
+    """the library reports the kernel-source hash it was built from; the binding accepts
+    the tree's hash and refuses any other (a stale prebuilt .so) unless explicitly overridden."""
+    from turtlevsr_amd.build import source_hash
+    L = _lib.lib()
+    assert L.turtle_source_hash().decode() == source_hash()
+    assert _lib.check_source_hash(L) == source_hash()
+    monkeypatch.delenv("TURTLE_ALLOW_STALE_LIB", raising=False)
+    with pytest.raises(RuntimeError, match="built from kernel sources"):
+        _lib.check_source_hash(L, expected="0123456789abcdef")
+    monkeypatch.setenv("TURTLE_ALLOW_STALE_LIB", "1")
+    assert _lib.check_source_hash(L, expected="0123456789abcdef") == source_hash()
+
+
 def test_training_exports_match_header():
     """Every entry point include/turtle_train.h declares is exported by libturtle_hip.so."""
     hdr = open(os.path.join(REPO, "include", "turtle_train.h")).read()

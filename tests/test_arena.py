@@ -103,3 +103,27 @@ def test_submodule_parameter_reassignment_changes_signature():
     assert s1 != s0
     assert any(p is blk.norm1.body.weight for p in m._plist)
     assert m._signature() == s1
+
+
+def test_more_streams_than_default_after_reserve():
+    """with more interleaved streams than arenas kept per slot (the harness at > 64 tiles),
+    every call missed its arena; `reserve_history_streams` (called by the tiled harness with its tile
+    count) keeps one per stream, so the second pass over 70 streams re-uses every arena."""
+    m = _module()
+    n = m._ARENA_STREAMS + 6
+    m.reserve_history_streams(n)
+    caches = [_step(m, None) for _ in range(n)]
+    ptrs = [c[0].untyped_storage().data_ptr() for c in caches]
+    caches = [_step(m, c) for c in caches]
+    assert len(m._arenas[5]) == n
+    assert [c[0].untyped_storage().data_ptr() for c in caches] == ptrs     # no stream re-allocated
+
+
+def test_unrelated_registration_keeps_signature():
+    """ADVICE r5: building another module (a loss, a second model) bumps the global registration epoch;
+    the drop-in module's signature must not change (no repack of unchanged weights)."""
+    import torch.nn as nn
+    m = _module()
+    s0 = m._signature()
+    nn.Linear(3, 3)                                  # registers parameters on an unrelated module
+    assert m._signature() == s0

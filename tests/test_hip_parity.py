@@ -81,6 +81,19 @@ def test_clip_bf16_psnr(name):
     assert vals and min(vals) >= BF16_DB, (name, vals)
 
 
+@pytest.mark.parametrize("name", ["clip_gopro_128x224", "clip_gopro_256"])
+def test_clip_bf16_psnr_gffn_forced(name):
+    """The fused level-3 GatedFeedForward kernel (gffn.hip) on the steady-state GoPro golden clips: at
+    these sizes its tile count is below the default launch threshold, so it is forced on
+    (gffn_min_blocks 0); bf16 >= 58 dB vs the reference's fp32 frames, as every bf16 path."""
+    g, meta = load(name)
+    m = _opts(_model(meta, "bf16"), {"gffn": 1, "gffn_min_blocks": 0})
+    outs, _ = _run(m, clip_input(g, meta))
+    vals = [psnr(o.numpy(), g[f"out{j}"]) for j, o in enumerate(outs) if f"out{j}" in g]
+    print(name, "bf16 (gffn) vs reference fp32 PSNR per frame:", [round(v, 2) for v in vals])
+    assert vals and min(vals) >= BF16_DB, (name, vals)
+
+
 def test_fp32_vs_oracle_256_steady_state():
     """GoPro widths at 256x256 (the bench shape), 5 frames: caches full from frame 3 on (T = 4 at
     dec3 / dec2, 3 at dec1), HIP fp32 vs the CPU oracle on a clip no golden file holds."""
@@ -146,7 +159,7 @@ def test_kernel_variants_agree(dtype):
     base = {"fuse": 0, "fused2": 0, "panel_gemm": 0, "dw_rows": 0, "gemm_lds": 0, "gemm_pn": 0, "sab_mfma": 0,
             "stem_mfma": 0, "gemm_ar": 0, "gemm_kt": 0, "dwgemm": 0, "dwgemm_min_blocks": 0, "ffn": 0, "down_tile": 0,
             "tilepd": 0, "tilepd_min_blocks": 0, "tilepd_gate": 0, "gemm8": 0, "gemm8_ps": 0, "attn_fin": 0, "sab_waves": 4,
-            "gemm9": 0, "gemm_f32": 0, "gemm_sk": 0}
+            "gemm9": 0, "gemm_f32": 0, "gemm_sk": 0, "gffn": 0, "gffn_min_blocks": 0}
     ref = _run(_opts(_model(meta, "fp32"), base), clip)[0]
     variants = [dict(base, fuse=f, panel_gemm=p, dw_rows=d) for f in (0, 1) for p in (0, 1) for d in (0, 1)]
     variants += [dict(base, fuse=1, fuse_fp32=1), dict(base, fuse=1, fuse_fp32=1, panel_gemm=1)]   # fp32 fused block kernel
@@ -157,6 +170,7 @@ def test_kernel_variants_agree(dtype):
                  dict(base, tilepd=1, tilepd_gate=1, tilepd_cb=0), dict(base, gemm8=2), dict(base, gemm8=2, gemm8_ps=1), dict(base, gemm8=3, gemm_kt=1), dict(base, gemm8=2, gemm_kt=1, tilepd=1), dict(base, attn_fin=1), dict(base, sab_waves=8),
                  dict(base, gemm9=2), dict(base, gemm9=1), dict(base, gemm9=2, gemm_pn=1, tilepd=1, dwgemm=1),
                  dict(base, gemm_sk=1), dict(base, gemm_sk=1, gemm9=1, gemm_kt=1),
+                 dict(base, gffn=1), dict(base, gffn=1, tilepd=1, gemm_pn=1, fuse=1, fused2=1, ffn=1),
                  dict(base, gemm_kt=1, gemm_ar=1, gemm_pn=1, gemm_lds=1, fuse=1, fused2=1, dw_rows=1, panel_gemm=1, dwgemm=1, ffn=1),
                  dict(base, gemm_kt=1, gemm_ar=1, gemm_pn=1, fuse=1, fused2=1, dw_rows=1, dwgemm=1, ffn=1, tilepd=1),
                  dict(base, gemm_lds=1, gemm_pn=1, fuse=1, fused2=1, dw_rows=1, panel_gemm=1, sab_mfma=1, stem_mfma=1, gemm9=1)]

@@ -717,3 +717,24 @@ def test_ddp_two_ranks_on_gpu_hip_kernels_match_single_process():
         n += 1
     assert n > 100
     assert 0.5 * (res[0][2] + res[1][2]) == pytest.approx(float(loss.detach()), rel=1e-4)
+
+
+def test_sab_hip_dispatch_respects_key_limit():
+    """the HIP SAB kernels take <= SAB_MAX_KEYS keys; larger token grids must take the ATen
+    top-5 / softmax chain instead of raising from the kernel's argument check."""
+    from turtlevsr_amd.train import SAB_MAX_KEYS, _sab_hip_ok
+
+    class Ops:
+        def sab_attention(self):
+            pass
+
+        def sab_softmax(self):
+            pass
+
+    o = Ops()
+    assert _sab_hip_ok(o, "sab_attention", 144, 128, 1024)
+    assert _sab_hip_ok(o, "sab_softmax", SAB_MAX_KEYS)
+    assert not _sab_hip_ok(o, "sab_attention", SAB_MAX_KEYS + 8, 128, 1024)
+    assert not _sab_hip_ok(o, "sab_softmax", SAB_MAX_KEYS + 1)
+    assert not _sab_hip_ok(o, "sab_attention", 148, 128, 1024)        # n % 8
+    assert not _sab_hip_ok(object(), "sab_softmax", 16)             # op set without the kernel (CPU)

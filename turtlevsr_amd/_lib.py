@@ -57,14 +57,34 @@ def lib():
     L.turtle_profile_filter.argtypes = [vp, C.c_char_p]
     L.turtle_set_option.argtypes = [vp, C.c_char_p, C.c_int]
     L.turtle_last_error.restype = C.c_char_p
+    L.turtle_source_hash.restype = C.c_char_p
+    check_source_hash(L)
     _lib = L
     return L
+
+
+def check_source_hash(L, expected: str | None = None):
+    """The loaded library must be built from this tree's kernel sources (the .so is git-ignored and
+    travels prebuilt): a stale library raises unless TURTLE_ALLOW_STALE_LIB=1."""
+    got = L.turtle_source_hash().decode()
+    if expected is None:
+        from .build import source_hash
+        expected = source_hash()
+    if got != expected and os.environ.get("TURTLE_ALLOW_STALE_LIB") != "1":
+        raise RuntimeError(f"{LIB_PATH} was built from kernel sources {got}, this tree's are {expected}: "
+                           "rebuild with `python -m turtlevsr_amd.build` (or set TURTLE_ALLOW_STALE_LIB=1)")
+    return got
+
+
+def source_hash() -> str:
+    """The kernel-source hash the loaded library reports (turtle_source_hash)."""
+    return lib().turtle_source_hash().decode()
 
 
 EXPORTED = ["turtle_create", "turtle_destroy", "turtle_num_weights", "turtle_weight_info", "turtle_set_weight",
             "turtle_load_weights", "turtle_cache_layout", "turtle_workspace_size", "turtle_forward",
             "turtle_profile_begin", "turtle_profile_end", "turtle_profile_filter", "turtle_set_option",
-            "turtle_last_error"]
+            "turtle_last_error", "turtle_source_hash"]
 K_CLASSES = ["gemm", "dwconv", "chan_attn", "sab_score", "sab_av", "sab_window", "other", "fused"]
 K_ALL = 99
 

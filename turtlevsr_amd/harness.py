@@ -61,6 +61,8 @@ def run_inference_patched(img_lq_prev: torch.Tensor, img_lq_curr: torch.Tensor, 
     E = torch.zeros(b, c, h, w, dtype=torch.float32, device=img_lq_curr.device)
     Wt = torch.zeros_like(E)
     patch_dict_k, patch_dict_v = {}, {}
+    if hasattr(model, "reserve_history_streams"):      # one SAB history stream per tile position
+        model.reserve_history_streams(len(tile_starts(h, tile, stride)) * len(tile_starts(w, tile, stride)))
     for h_idx in tile_starts(h, tile, stride):
         for w_idx in tile_starts(w, tile, stride):
             cur = img_lq_curr[..., h_idx:h_idx + tile, w_idx:w_idx + tile]

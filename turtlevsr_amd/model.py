@@ -115,11 +115,15 @@ class TurtleHIP(TrainGraph, TurtleParams):
         # assigned on a SUBmodule, e.g. blk.attn.temperature = nn.Parameter(...), counts too); the
         # version sum catches in-place updates, the leading data pointers catch device moves and
         # `.data` rebinding
+        # a registration ANYWHERE bumps the epoch: the list is rebuilt then (cheap), but the signature
+        # carries the identities of this module's parameter objects, not the epoch, so a loss or a
+        # second model built next to this one does not trigger a repack
         ps = self.__dict__.get("_plist")
         if ps is None or self.__dict__.get("_plist_epoch") != _REG_EPOCH[0]:
             self.__dict__["_plist_epoch"] = _REG_EPOCH[0]
             ps = self.__dict__["_plist"] = list(self.parameters())
-        return (ps[0].device, self._dtype_name, self.__dict__["_plist_epoch"], sum(map(_VERSION, ps)),
+            self.__dict__["_plist_ids"] = hash(tuple(map(id, ps)))
+        return (ps[0].device, self._dtype_name, self.__dict__["_plist_ids"], sum(map(_VERSION, ps)),
                 tuple(p.data_ptr() for p in ps[:4]))
 
     def refresh_weights(self):
@@ -268,6 +272,11 @@ class TurtleHIP(TrainGraph, TurtleParams):
     _ARENA_BYTES = 6 << 30            # per stream and slot, reached only by doubling
     _ARENA_STREAMS = 64               # arenas remembered per slot (least recently used dropped)
 
+    def reserve_history_streams(self, n: int):
+        """Keep at least n interleaved B = 1 streams' arenas per slot (the tiled harness calls this with
+        its tile count: with more tiles than arenas kept, every call would miss and re-allocate)."""
+        self.__dict__["_ARENA_STREAMS"] = max(type(self)._ARENA_STREAMS, int(n) + 1)
+
     def release_history(self):
         """Drop the SAB history arenas this module keeps for fast cache hand-over (caches the caller
         still holds stay valid: they own their storage)."""
@@ -333,6 +342,9 @@ class TurtleHIP(TrainGraph, TurtleParams):
         if self._handle is None or self._sig is None:
             self.refresh_weights()
         _lib.check(_lib.lib().turtle_set_option(self._handle.h, name.encode(), int(value)))
+        # a switch may change which kernels (and workspace buffers) a forward uses: size the workspace
+        # again at the next forward (raising sk_max_px after a forward left it too small)
+        self._ws = None
         return self
 
     def profile_begin(self, kernel_class: str = "all", tag: Optional[str] = None):

@@ -9,8 +9,10 @@ base_model.py:340-365, dist_util.py:15-30) on the GPU:
   gates and plain GELUs, pointwise 1x1 convolutions (forward, input and weight gradients), the
   channel-attention Gram, the Down / Upsample 3x3 convolutions and the SAB window convolutions run on
   hand-written HIP kernels with hand-written backward (``train_ops.HipOps``, include/turtle_train.h),
-  on channels-last activations; the 3-channel stem / ending convolutions, the FHR / CHM attention with
-  its caches and the SAB dense scores / top-5 / A.v are torch ops, differentiated by autograd.
+  on channels-last activations, and so do (round 5) the stem / ending convolutions, the FHR / CHM
+  attention with its caches (per-channel L2 normalisation, cross-Gram, W_eff over the history) and the
+  SAB core (scores, top-5 + L1-ball clipped softmax, A.v) up to SAB_MAX_KEYS keys per frame; what is
+  left in torch is reshapes, concatenations and the ATen op set that the CPU tests differentiate.
 * caches are NOT detached between frames: the loss of frame j back-propagates into frames < j
   through the history state (video_restoration_model.py:85-95);
 * ``Trainer.train_step``: zero_grad -> autocast forward over the T frames -> L1 per frame summed,
@@ -100,6 +102,19 @@ def _split(x, *sizes, sink=None):
     return _ChanSplit.apply(x, sink, *sizes)
 
 
+# the HIP SAB kernels take at most this many keys per frame (train_ops.hip: one wave per score row);
+# larger token grids (training crops above ~512 x 512) go through the ATen top-5 / softmax chain
+SAB_MAX_KEYS = 1024
+
+
+def _sab_hip_ok(ops, name: str, n: int, g: int = 8, d: int = 8) -> bool:
+    """Whether the StateAlignBlock core runs on the op set's HIP kernel `name` ('sab_attention' or
+    'sab_softmax') for n keys of width g and value width d (n > 1024 used to raise)."""
+    if not hasattr(ops, name) or _ATEN_SAB or n > SAB_MAX_KEYS:
+        return False
+    return name != "sab_attention" or (n % 8 == 0 and g % 8 == 0 and d % 8 == 0)
+
+
 class _ToNCHW(torch.autograd.Function):
     """x.contiguous() for MIOpen's NCHW convolution path whose gradient goes back in x's own
     memory format: otherwise the NCHW input gradient of every dense conv (and the loss's NCHW
@@ -170,9 +185,9 @@ class TrainGraph:
         return self._ops().dwconv3x3(x, m.weight, m.bias)
 
     def _dense(self, x, w, b=None, stride=1, padding=1, groups=1):
-        """Dense / window convolutions (stem, ending, Down/Upsample, SAB window convs) through
-        F.conv2d on a standard-layout copy: MIOpen's channels-last backward faults on some of
-        these shapes (MI355X, ROCm 7.2), its NCHW path does not. Channels-last again afterwards."""
+        """Dense / window convolutions through F.conv2d - reached by the CPU (ATen) op set only: on the GPU
+        the stem / ending, Down / Upsample and SAB window convolutions run on the HIP op set's kernels. A
+        channels-last op set gets a standard-layout copy in and channels-last out."""
         cl = getattr(self._ops(), "channels_last", False)
         y = F.conv2d(_ToNCHW.apply(x) if cl else x.contiguous(), w, b, stride, padding, 1, groups)
         return y.contiguous(memory_format=torch.channels_last) if cl else y
@@ -399,7 +414,7 @@ class TrainGraph:
         q = _l2n(q, -1)
         k = _l2n(k, -1)
         ops = self._ops()
-        if hasattr(ops, "sab_attention") and not _ATEN_SAB and n % 8 == 0 and g % 8 == 0 and (ws * ws * c) % 8 == 0:
+        if _sab_hip_ok(ops, "sab_attention", n, g, ws * ws * c):
             # the values as transposed tokens [b, 1, D, n] (written so by the dilation copy; the cache views
             # handed back are their [b, t, 1, n, D] transposes), scores / top-5 / softmax / A.v on HIP
             vT = self._dilated_t(v, ws)
@@ -419,7 +434,7 @@ class TrainGraph:
         t = k.shape[1]
         s = (q @ k.transpose(-2, -1)) * m.temperature                   # [b, t, 1, n, n]
         ops = self._ops()
-        if hasattr(ops, "sab_softmax") and not _ATEN_SAB:
+        if _sab_hip_ok(ops, "sab_softmax", n):
             a = ops.sab_softmax(s, tw, SAB_RADIUS)
             o = self._undilated(a @ vt, b * t, c, hl, wl, ws, getattr(ops, "channels_last", False))
             o = self._c1(m.project_out, o).reshape(b, t, c, hl, wl)
