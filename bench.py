@@ -34,6 +34,7 @@ from __future__ import annotations
 import argparse
 import shutil
 import json
+import math
 import os
 import sys
 import time
@@ -78,6 +79,13 @@ def source_hash():
     counters to the kernels they were measured on."""
     from turtlevsr_amd.build import source_hash as sh
     return sh()
+
+
+def model_lib_hash():
+    """Kernel-source hash compiled into the loaded libturtle_hip.so (equal to source_hash(): _lib refuses
+    a stale library)."""
+    from turtlevsr_amd import _lib
+    return _lib.source_hash()
 
 
 def cpu_model():
@@ -151,7 +159,15 @@ def cpu_baseline(opt, h, w, threads, sr=False):
     the reference) MEASURED on one steady-state frame at the bench resolution: the history caches
     are full (T = ntc frames at every cached level; their shapes come from 4 priming frames at
     64x64, re-sized to this frame, synthetic contents - the cost does not depend on them).
-    Returns seconds per frame."""
+    Returns (seconds per frame, the oracle's output, and its input frame and caches)."""
+    return oracle_steady_frame(opt, h, w, threads, sr=sr)
+
+
+def oracle_steady_frame(opt, h, w, threads, sr=False, sparse_av=False):
+    """One steady-state frame through the CPU oracle (see cpu_baseline): returns (seconds, out,
+    frame, k caches, v caches) - the same frame and grown caches can then go through the HIP model
+    (the headline size pinned to the oracle directly). sparse_av: the SAB A.v as a
+    sparse product (same sum; the parity test's budget), never for the timed baseline."""
     from oracle import turtle_ref as R
     torch.set_num_threads(threads)
     m = TurtleHIP(opt)
@@ -169,9 +185,26 @@ def cpu_baseline(opt, h, w, threads, sr=False):
         frame = clip_frames(h, w, 12, "cpu", n=2)[1]
         print(f"[bench] cpu baseline: one steady-state {wo}x{ho} oracle frame on {threads} threads ...",
               file=sys.stderr, flush=True)
-        t0 = time.perf_counter()
-        R.turtle_forward(sd, opt, frame, kb, vb, sr=sr)
-        return time.perf_counter() - t0
+        prev, R.SAB_SPARSE_AV = R.SAB_SPARSE_AV, sparse_av
+        try:
+            t0 = time.perf_counter()
+            out, _, _ = R.turtle_forward(sd, opt, frame, kb, vb, sr=sr)
+            dt = time.perf_counter() - t0
+        finally:
+            R.SAB_SPARSE_AV = prev
+        return dt, out, frame, kb, vb
+
+
+def hip_vs_oracle(opt, dev, out_ref, frame, kb, vb, sr=False):
+    """The fp32 HIP build on the oracle frame's input and caches: PSNR (peak 1) and max |diff|."""
+    m = build_model(opt, "fp32", dev, sr)
+    with torch.no_grad():
+        o, _, _ = m(frame.to(dev), kb, vb)
+    o = o.float().cpu()
+    mse = float(((o - out_ref) ** 2).mean())
+    del m
+    torch.cuda.empty_cache()
+    return dict(psnr_db=round(10 * math.log10(1.0 / max(mse, 1e-30)), 2), max_abs=float((o - out_ref).abs().max()))
 
 
 def launch_groups(dump):
@@ -485,16 +518,21 @@ def main():
                                  "caches full, HIP graph replay (the `--gpus N > 1` default workload)")
         del sm
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = cpu_share_threads()
-        dt = cpu_baseline(opt, h // 4 if args.sr else h, w // 4 if args.sr else w, threads, sr=args.sr)
+        dt, out_ref, oframe, okb, ovb = cpu_baseline(opt, h // 4 if args.sr else h, w // 4 if args.sr else w, threads,
+                                                     sr=args.sr)
+        pin = hip_vs_oracle(opt, dev, out_ref, oframe, okb, ovb, sr=args.sr)
         cpu = dict(value=round(1.0 / dt, 6), unit="frames/s", cores=threads, kind="port", measured=True,
                    s_per_frame=round(dt, 2), cpu_model=cpu_model(), nproc=os.cpu_count(),
                    torch_threads=torch.get_num_threads(),
                    sample=f"oracle/turtle_ref.py fp32 (dense SAB, as the reference), ONE steady-state {w}x{h} frame "
                           f"(history caches full: T = ntc at every cached level), B=1, timed on {threads} host threads "
                           f"(the box's CPU share per GPU): {dt:.1f} s/frame; not extrapolated")
+        # the same frame, input and grown caches through the fp32 HIP build
+        parity = dict(psnr_fp32_vs_oracle_db=pin["psnr_db"], max_abs=pin["max_abs"],
+                      frame=f"the cpu_baseline frame: steady-state {oframe.shape[-1]}x{oframe.shape[-2]}, caches full, fp32 HIP vs the oracle")
 
     line = {
         "metric": "restored frames/sec @1080p (1/2/4/8 GPU) + PSNR delta vs ref"
@@ -520,6 +558,8 @@ def main():
         "cpu_baseline": cpu,
         "psnr_bf16_vs_fp32_db": psnr,
         "psnr_delta_vs_fp32_db": dpsnr,
+        "parity_fp32_vs_oracle": parity,
+        "lib_source_hash": model_lib_hash(),
         "alg_tflops": round(f_alg(h, w) * fps / 1e12, 2),
     }
     if scale_pt is not None:

@@ -31,6 +31,12 @@ SAB_TOPK = 5       # turtle_t1_arch.py:588
 SAB_RADIUS = 4     # turtle_t1_arch.py:590 (L1 distance on the token grid)
 PAD_MULT = 32      # turtle_t1_arch.py:1043 padder_size = 2**3 * 4
 
+# A.v of the StateAlignBlock as a sparse product: the clipped-softmax rows have at most top-5 + the
+# 41-key L1 ball non-zeros, so a @ v (turtle_t1_arch.py:600) is the same sum over those keys. Off by
+# default (the CPU baseline times the reference's dense product); the 1080p parity test turns it on
+# so that one steady-state 1920x1088 oracle frame (N = 8160 tokens) fits a test's time budget.
+SAB_SPARSE_AV = False
+
 
 # ----------------------------------------------------------------------------------------------
 # Architecture description (make_model, turtle_t1_arch.py:10-53; Turtle_t1.__init__ 932-1043)
@@ -230,7 +236,12 @@ def state_align(sd: SD, p: str, x: Tensor, ws: int, ntc: int,
     top = torch.zeros_like(s).scatter_(-1, torch.topk(s, SAB_TOPK, dim=-1).indices, 1.0)
     ball = ball_mask(th, tw).to(s.dtype)
     a = clipped_softmax(s * top + s * ball)
-    o = a @ vt                                                        # [b, t, 1, n, ws*ws*c]
+    if SAB_SPARSE_AV:
+        vb = vt.expand(b, t, 1, n, vt.shape[-1])
+        o = torch.stack([torch.sparse.mm(ai.to_sparse(), vi) for ai, vi in
+                         zip(a.reshape(-1, n, n), vb.reshape(-1, n, vt.shape[-1]))]).reshape(b, t, 1, n, -1)
+    else:
+        o = a @ vt                                                    # [b, t, 1, n, ws*ws*c]
     o = o.reshape(b * t, hh, ww_, ws, ws, c).permute(0, 5, 3, 1, 4, 2).reshape(b * t, c, hl, wl)
     o = _conv(sd, p + ".project_out", o).reshape(b, t, c, hl, wl)
     return o, k[:, -ntc:], vt[:, -ntc:]

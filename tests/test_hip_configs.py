@@ -120,6 +120,26 @@ def test_1080p_bf16_psnr_delta_bench_protocol():
     assert worst <= 0.01, worst
 
 
+@pytest.mark.timeout(900)
+def test_1080p_fp32_vs_oracle_steady_state():
+    """the headline size pinned to the oracle directly (not only through the fp32 HIP
+    build): one steady-state 1920x1080 frame (padded 1920x1088: SAB N = 8160 level-1 tokens, every
+    history cache full with the bench's grown synthetic caches) through the oracle and the fp32 HIP
+    build on the same input and caches. The oracle's A.v runs as the equal sparse product
+    (SAB_SPARSE_AV) to fit the test budget; bench.py's cpu_baseline compares against the dense one."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    dev = torch.device("cuda", 0)
+    opt = bench.load_opt()
+    dt, out_ref, frame, kb, vb = bench.oracle_steady_frame(opt, 1080, 1920, bench.cpu_share_threads(), sparse_av=True)
+    pin = bench.hip_vs_oracle(opt, dev, out_ref, frame, kb, vb)
+    print(f"1080p steady state: oracle {dt:.1f} s, fp32 HIP vs oracle {pin['psnr_db']} dB, max |diff| {pin['max_abs']:.3e}")
+    assert out_ref.shape == (1, 3, 1080, 1920)
+    assert pin["psnr_db"] >= 80.0, pin
+    assert pin["max_abs"] <= 2e-4, pin                     # measured 4.8e-6 (profiles/r06b_pytest_pin_1080p.log)
+
+
 def test_sr_1080p_bf16_vs_fp32():
     from turtlevsr_amd.synthetic import synthetic_frames
     _, meta = load("clip_gopro_64")

@@ -141,6 +141,20 @@ def test_clip(name):
                     close(t, g[key], atol=5e-5, rtol=1e-3)
 
 
+def test_sparse_av_matches_golden_steady_state(monkeypatch):
+    """The oracle's sparse A.v switch (SAB_SPARSE_AV, used by the 1080p parity test) computes the same
+    frames as the reference: the steady-state 256x256 GoPro golden clip (N = 256 tokens, top-5 keys
+    outside the L1 ball exercised) at the dense path's tolerance."""
+    monkeypatch.setattr(R, "SAB_SPARSE_AV", True)
+    g, meta = load("clip_gopro_256")
+    opt = meta["opt"]
+    shapes = {k: tuple(v.shape) for k, v in TurtleParams(opt).state_dict().items()}
+    sd = synth_sd(shapes, meta["seed"])
+    outs, _ = R.run_clip(sd, opt, torch.from_numpy(clip_input(g, meta)), sr=meta["sr"])
+    for j, o in enumerate(outs):
+        check_out(g, j, o, atol=5e-5, rtol=1e-3)
+
+
 def test_pad_to_non_square_ragged():
     """check_image_size (turtle_t1_arch.py:1134-1139) pads H and W each to a multiple of 32 with
     zeros at the bottom/right: 540x960 -> 544x960 and 36x70 -> 64x96 (unequal H/W pads)."""

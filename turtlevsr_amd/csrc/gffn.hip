@@ -17,8 +17,8 @@
 //             (prefetched one chunk ahead); H -> LDS as f16, rows permuted at pack time so a lane's 4
 //             accumulators are (x1 c, x1 c+1, x2 c, x2 c+1) of one gate pair: one 8-byte store
 //   P2        depthwise + gate on packed f16 (v_pk_fma_f16; x-neighbours by DPP row shifts inside the
-//             16-lane row = one haloed image row, y-neighbours from the rows the lane walked), GELU in
-//             f32 (tanh form, as every bf16 kernel: common.h), G -> LDS f16 [8 ch-groups][112 px][8]
+//             16-lane row = one haloed image row, y-neighbours from the rows the lane walked), GELU gate
+//             on packed f16 too (tanh form, as every bf16 kernel: common.h), G -> LDS f16 [8 ch-groups][112 px][8]
 //   P3        out_acc[256 x 112] += W2[:, chunk] G on the matrix cores: wave w owns output channels
 //             32 w .. 32 w + 31 (rows permuted: a lane's 8 accumulators are 8 consecutive channels)
 //   epilogue  out = x + acc + b2, 16-byte bf16 stores
@@ -42,7 +42,10 @@ constexpr int GF_NT = 512;
 constexpr int GF_XP = GF_C * 2 + 32;                  // LDS bytes per haloed pixel of X (+32: conflict-free b128)
 constexpr int GF_OFF_G = GF_NXP * GF_XP;              // two G buffers: [8 groups][112 px][8 ch] f16 each
 constexpr int GF_OFF_SINK = GF_OFF_G + 2 * 8 * GF_NGP * 16;   // P2 store target of the x-halo lanes (no branch per row)
-constexpr int GF_LDS = GF_OFF_SINK + 8 * 64 * 4;
+constexpr int GF_MAXNC = 12;                                 // hidden width <= 768 (taps / tb tables in LDS)
+constexpr int GF_OFF_TAP = GF_OFF_SINK + 8 * 64 * 4;          // depthwise taps + bias of every chunk, P2 lane order
+constexpr int GF_OFF_TB = GF_OFF_TAP + GF_MAXNC * 8 * 4 * 80; // P1 epilogue vectors (W1 b_ln + b1) of every chunk
+constexpr int GF_LDS = GF_OFF_TB + GF_MAXNC * 128 * 4;
 static_assert(GF_LDS <= 160 * 1024, "gffn LDS budget");
 static_assert(GF_NGP == 7 * 16, "P3 N tiles");
 
@@ -105,13 +108,14 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
     constexpr int k = decltype(K)::value;
     wf[k & 3] = (DBG & 8) ? make_uint4(lane, k, c, 0) : W1F[((c * 8 + wid) * 8 + k) * 64 + lane];
   };
+  // taps and tb vectors come from LDS tables filled once per block (prologue)
   auto ld_taps = [&](int c) __attribute__((always_inline)) {
-    const uint4* tp = reinterpret_cast<const uint4*>(DWP + ((size_t)(c * 8 + wid) * 4 + g4) * 20);
+    const uint4* tp = reinterpret_cast<const uint4*>(smem + GF_OFF_TAP + (((c * 8 + wid) * 4 + g4) * 20) * 4);
 #pragma unroll
-    for (int q = 0; q < 5; ++q) tq[q] = (DBG & 8) ? make_uint4(0x3c003c00u, lane, q, c) : tp[q];
+    for (int q = 0; q < 5; ++q) tq[q] = tp[q];
   };
   auto ld_tb = [&](int c) __attribute__((always_inline)) {
-    tbv = (DBG & 8) ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(TBP + ((c * 8 + wid) * 16 + 4 * g4));
+    tbv = *reinterpret_cast<const f32x4*>(smem + GF_OFF_TB + ((c * 8 + wid) * 16 + 4 * g4) * 4);
   };
   auto ld_w2 = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
@@ -122,7 +126,6 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
   };
   ld_w1(0, std::integral_constant<int, 0>{});
   ld_w1(0, std::integral_constant<int, 1>{});
-  ld_tb(0);
 
   // ---- haloed x tile -> LayerNorm in registers -> LDS (f16). A pixel's 32 16-byte chunks are held
   // by an aligned group of 8 lanes (chunks cc, cc + 8, cc + 16, cc + 24); statistics by an 8-lane DPP
@@ -152,6 +155,14 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
     }
     for (int e = tid; e < 2 * 8 * GF_NGP; e += GF_NT)
       *reinterpret_cast<uint4*>(smem + GF_OFF_G + e * 16) = make_uint4(0u, 0u, 0u, 0u);
+    {
+      const int ntap = nc * 8 * 4 * 5, ntb = nc * 32;             // 16-byte pieces
+      for (int e = tid; e < ntap; e += GF_NT)
+        *reinterpret_cast<uint4*>(smem + GF_OFF_TAP + e * 16) =
+            (DBG & 8) ? make_uint4(0x3c003c00u, e, 0u, 0u) : reinterpret_cast<const uint4*>(DWP)[e];
+      for (int e = tid; e < ntb; e += GF_NT)
+        *reinterpret_cast<uint4*>(smem + GF_OFF_TB + e * 16) = (DBG & 8) ? make_uint4(0u, 0u, 0u, 0u) : reinterpret_cast<const uint4*>(TBP)[e];
+    }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int p = j * PPJ + pq;
@@ -208,6 +219,7 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
 #pragma unroll
   for (int r = 0; r < GF_RH; ++r) hv[r][0] = hv[r][1] = 0u;
   const char* xb = sX + xl * GF_XP + g4 * 16;
+  f16x8 xa[5];                                              // P1 fragments of haloed rows 0-4, one K step ahead
   const bool wr = xl >= 1 && xl <= GF_TX;
   char* sink = smem + GF_OFF_SINK + tid * 4;
 
@@ -221,22 +233,27 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
     constexpr int k = decltype(K)::value;
     if constexpr (k + 2 < 8) ld_w1(c, std::integral_constant<int, k + 2>{});
     else ld_w1(cn, std::integral_constant<int, k - 6>{});
-    // two batches of 5 rows (20 fragment registers live instead of 40)
+    // rows 0-4 of this step were read at the end of the previous step (their latency behind its P2
+    // row); rows 5-9 are read before rows 0-4 multiply, and rows 0-4 of the NEXT step (the next chunk's
+    // step 0 after step 7: X does not change) after rows 5-9 multiply
+    f16x8 xb5[5];
 #pragma unroll
-    for (int hb = 0; hb < 2; ++hb) {
-      f16x8 xf[5];
+    for (int i = 0; i < 5; ++i) xb5[i] = *reinterpret_cast<const f16x8*>(xb + (5 + i) * 16 * GF_XP + k * 64);
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 5; ++i) xf[i] = *reinterpret_cast<const f16x8*>(xb + (5 * hb + i) * 16 * GF_XP + k * 64);
-      if constexpr ((DBG & 1) == 0) {
-#pragma unroll
-        for (int i = 0; i < 5; ++i)
-          acc[5 * hb + i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(wf[k & 3]), xf[i], acc[5 * hb + i], 0, 0, 0);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) acc[5 * hb + i][0] += (float)xf[i][0] + (float)as_f16x8(wf[k & 3])[1];
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < 5; ++i) {
+      if constexpr ((DBG & 1) == 0) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(wf[k & 3]), xa[i], acc[i], 0, 0, 0);
+      else acc[i][0] += (float)xa[i][0] + (float)as_f16x8(wf[k & 3])[1];
     }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      if constexpr ((DBG & 1) == 0) acc[5 + i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(wf[k & 3]), xb5[i], acc[5 + i], 0, 0, 0);
+      else acc[5 + i][0] += (float)xb5[i][0] + (float)as_f16x8(wf[k & 3])[1];
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) xa[i] = *reinterpret_cast<const f16x8*>(xb + i * 16 * GF_XP + ((k + 1) & 7) * 64);
+    __builtin_amdgcn_sched_barrier(0);
   };
   auto p1_finish = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -265,7 +282,12 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
           s[h] = __builtin_elementwise_fma(h2(tw[2 * (3 * dy + 2) + h]), h2(gf_shl(v)), s[h]);
         }
       }
-      gout = pk_f16(gelu_bf16((float)s[0].x) * (float)s[1].x, gelu_bf16((float)s[0].y) * (float)s[1].y);
+      // gelu(x1) * x2 on packed f16, the tanh form of every bf16 kernel (common.h gelu_tanh: x / (1 + 2^u),
+      // u = -log2(e) 1.5957691 (x + 0.044715 x^3)); f16 rounding of u / 2^u stays below G's own rounding
+      const f16x2 x = s[0];
+      const f16x2 u = x * (x * x * f16x2{(f16)-0.10294324f, (f16)-0.10294324f} + f16x2{(f16)-2.3022082f, (f16)-2.3022082f});
+      const f16x2 e = __builtin_elementwise_exp2(u) + f16x2{(f16)1.f, (f16)1.f};
+      gout = u2(x * (f16x2{(f16)1.f, (f16)1.f} / e) * s[1]);
     } else {
       gout = hv[o][0] ^ hv[o][1] ^ tw[o];
     }
@@ -298,6 +320,9 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
   __syncthreads();
 
   // ---- interval 0: P1(0) ----
+#pragma unroll
+  for (int i = 0; i < 5; ++i) xa[i] = *reinterpret_cast<const f16x8*>(xb + i * 16 * GF_XP);
+  ld_tb(0);
   p1_init();
   gf_for<0, 8>([&](auto K) __attribute__((always_inline)) { p1_step(K, 0, nc > 1 ? 1 : 0); });
   p1_finish();
@@ -366,7 +391,7 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
 
 bool gffn_ok(const GffnArgs& a) {
   if (!a.x || !a.out || !a.w1f || !a.tbp || !a.dwp || !a.w2f || a.x == a.out) return false;
-  if (a.hd <= 0 || a.hd % 64 || a.hd > 2048) return false;
+  if (a.hd <= 0 || a.hd % 64 || a.hd > 64 * GF_MAXNC) return false;
   if (reinterpret_cast<uintptr_t>(a.x) % 16 || reinterpret_cast<uintptr_t>(a.out) % 16 || reinterpret_cast<uintptr_t>(a.w1f) % 16 ||
       reinterpret_cast<uintptr_t>(a.w2f) % 16 || reinterpret_cast<uintptr_t>(a.tbp) % 16 || reinterpret_cast<uintptr_t>(a.dwp) % 16 ||
       (a.b2 && reinterpret_cast<uintptr_t>(a.b2) % 16))

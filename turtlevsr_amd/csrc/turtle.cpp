@@ -662,7 +662,7 @@ static void pack_all(TurtleHandle* h) {
         bw.f_in = pack_gemm(h, pk, dvec(W(h, f + ".project_in.weight")), 2 * b.hidden, c, n2, opt_bias(h, f + ".project_in.bias"));
         bw.f_dw = pack_dw(h, pk, f + ".dwconv", 0, 2 * b.hidden);
         bw.f_out = pack_gemm(h, pk, dvec(W(h, f + ".project_out.weight")), c, b.hidden, "", opt_bias(h, f + ".project_out.bias"));
-        if (pk.bf16 && c == 256 && b.hidden % 64 == 0 && b.hidden <= 2048) {
+        if (pk.bf16 && c == 256 && b.hidden % 64 == 0 && b.hidden <= 768) {
           // the whole block as one kernel (gffn.hip): f16 fragments of W1 diag(g) and W2, tb = W1 b_ln + b1
           const int hd = b.hidden;
           const auto& w1 = W(h, f + ".project_in.weight");
@@ -1020,7 +1020,7 @@ struct Runner {
     return g;
   }
   bool can_gffn(const BlockW& bw, int c, int hd, int H, int Wd) const {
-    if (ES != 2 || !h->gffn || c != 256 || hd % 64 || hd > 2048) return false;
+    if (ES != 2 || !h->gffn || c != 256 || hd % 64 || hd > 768) return false;
     if (!dry() && bw.gf_w1f == NONE) return false;
     GffnArgs g{};
     g.nimg = B; g.H = H; g.W = Wd; g.hd = hd;
