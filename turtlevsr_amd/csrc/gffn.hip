@@ -93,8 +93,8 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
 
   // ---- weight streams of wave `wid` (hidden unit wid of every chunk: no fragment is loaded twice per
   // block). Issue order per interval (vmcnt retires in order; hipcc counts these plain loads exactly
-  // because the loop body is one path): W1 K steps two ahead through a 4-slot ring (the next chunk's
-  // first two during the last two steps), then the taps of the next P2 and the tb vector of the next
+  // because the loop body is one path): W1 K steps three ahead through a 4-slot ring (the next chunk's
+  // first three during the last three steps), then the taps of the next P2 and the tb vector of the next
   // P1, then the W2 fragments of the next P3 ----
   const uint4* W1F = reinterpret_cast<const uint4*>(a.w1f);
   const uint4* W2F = reinterpret_cast<const uint4*>(a.w2f);
@@ -126,6 +126,7 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
   };
   ld_w1(0, std::integral_constant<int, 0>{});
   ld_w1(0, std::integral_constant<int, 1>{});
+  ld_w1(0, std::integral_constant<int, 2>{});
 
   // ---- haloed x tile -> LayerNorm in registers -> LDS (f16). A pixel's 32 16-byte chunks are held
   // by an aligned group of 8 lanes (chunks cc, cc + 8, cc + 16, cc + 24); statistics by an 8-lane DPP
@@ -228,11 +229,11 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
     for (int r = 0; r < GF_RH; ++r) acc[r] = ((rowok >> r) & 1u) ? tbv : f32x4{0.f, 0.f, 0.f, 0.f};
   };
   // one K step of P1 (chunk c): 10 pixel-row fragments from LDS, one W1 fragment, 10 MFMAs; the W1
-  // stream runs two steps ahead (into the next chunk cn during the last two steps)
+  // stream runs three steps ahead (into the next chunk cn during the last three steps)
   auto p1_step = [&](auto K, int c, int cn) __attribute__((always_inline)) {
     constexpr int k = decltype(K)::value;
-    if constexpr (k + 2 < 8) ld_w1(c, std::integral_constant<int, k + 2>{});
-    else ld_w1(cn, std::integral_constant<int, k - 6>{});
+    if constexpr (k + 3 < 8) ld_w1(c, std::integral_constant<int, k + 3>{});
+    else ld_w1(cn, std::integral_constant<int, k - 5>{});
     // rows 0-4 of this step were read at the end of the previous step (their latency behind its P2
     // row); rows 5-9 are read before rows 0-4 multiply, and rows 0-4 of the NEXT step (the next chunk's
     // step 0 after step 7: X does not change) after rows 5-9 multiply
