@@ -9,11 +9,12 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 # 1080p frames only (no 256x256 scaling point: persistent kernels have the same grid at every size)
 BENCH="bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-psnr --no-scaling-point --no-roofline"
-KRE='dwgemm_kernel|ffn_kernel|fused2_kernel|dw_rows_kernel|gemm_pn_kernel|tilepd_kernel'
+KRE='gffn_kernel|dwgemm_kernel|ffn_kernel|fused2_kernel|dw_rows_kernel|gemm_pn_kernel|tilepd_kernel'
 timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/fetch -o run -- python3 $BENCH > $OUT/fetch.log 2>&1 &&
 timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRE" -f csv -d $OUT/write -o run -- python3 $BENCH > $OUT/write.log 2>&1
 rc=$?; echo "pmc rc=$rc"; [ $rc -ne 0 ] && exit $rc
 python3 tools/pmc_traffic.py $OUT \
+  'gffn nimg=1 H=272 W=480 hd=640@@gffn_kernel<0>' \
   'dwgemm gate=1 nimg=1 H=272 W=480 K=640 N=256@@dwgemm_kernel<2>' \
   'tilepd mode=0 nimg=1 H=272 W=480 C=256 N1=768@@tilepd_kernel<0,' \
   'ffn M=522240 C=128@@ffn_kernel<128>' \
