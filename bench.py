@@ -288,7 +288,8 @@ def train_bench(args, world, rank, dev):
     shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
     net.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(shapes, 0).items()})
     net = net.to(dev).train()
-    tr = Trainer(net, amp="bf16")
+    # TURTLE_TRAIN_ACC=0: autograd's per-use parameter gradients instead of the in-place accumulator (A/B)
+    tr = Trainer(net, amp="bf16", accumulate_grads=os.environ.get("TURTLE_TRAIN_ACC", "1") != "0")
     B = args.train_batch
     lq = torch.from_numpy(synthetic_frames((B, 5, 3, 256, 256), clip_seed(rank), name="lq")).to(dev)
     gt = (lq + 0.05 * torch.from_numpy(synthetic_frames((B, 5, 3, 256, 256), clip_seed(rank), name="gt")).to(dev)).clamp(0, 1)

@@ -24,10 +24,12 @@ extern "C" {
  * with bf16 / fp16 y: autocast's cast of the fp32 residual stream folded into the LayerNorm). */
 int turtle_train_ln_fwd(const void* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy, float* mu, float* rstd,
                         int64_t P, int C, int biasfree, int dtype, void* stream);
-/* dx [P][lddx] in x's type, dy in y's type (dtype as ln_fwd); dw, db [C] accumulated (db unused for BiasFree) */
+/* dx [P][lddx] in x's type, dy in y's type (dtype as ln_fwd); dw, db [C] accumulated (db unused for BiasFree).
+ * dres [P][lddres] (x's type) or NULL: the gradient of the block's residual use of x (x + branch(LN(x)),
+ * turtle_t1_arch.py:808-809), added into dx in the same pass (no separate gradient-accumulation add) */
 int turtle_train_ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy,
-                        int64_t lddy, void* dx, int64_t lddx, float* dw, float* db, int64_t P, int C, int biasfree, int dtype,
-                        void* stream);
+                        int64_t lddy, void* dx, int64_t lddx, const void* dres, int64_t lddres, float* dw, float* db, int64_t P,
+                        int C, int biasfree, int dtype, void* stream);
 
 /* depthwise 3x3, stride 1, pad 1, groups = C (nn.Conv2d(C, C, 3, padding=1, groups=C), e.g.
  * turtle_t1_arch.py:167-169, 237, 716-722): x [N][H][W][ldx] -> y [N][H][W][ldy]; w9 tap-major
@@ -106,9 +108,10 @@ int turtle_train_gram_wd(const float* D, const float* aq, const float* ak, void*
  *   y[p][n] = sum_k x[p][k] w[img(p)][n][k] + bias[n]
  * w [N][K] in the activation dtype; wstride = 0: one weight set, else set i at w + i * wstride
  * elements for the i-th run of img_px pixels. bias fp32 [N] or NULL. K % 8 == N % 8 == 0. Runs on
- * the inference GEMM family (gemm*.hip). */
-int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride, int64_t img_px, const float* bias, void* y,
-                      int64_t ldy, int64_t P, int K, int N, int dtype, void* stream);
+ * the inference GEMM family (gemm*.hip). res [P][ldr] in the activation dtype or NULL: added in the
+ * epilogue (the block's residual x + branch, turtle_t1_arch.py:808-809: one rounding, no separate add). */
+int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride, int64_t img_px, const float* bias,
+                      const void* res, int64_t ldr, void* y, int64_t ldy, int64_t P, int K, int N, int dtype, void* stream);
 
 /* reduction GEMM over pixels (a 1x1 convolution's weight gradient dW = dY^T X; the channel
  * attention Gram q^T k over HW, turtle_t1_arch.py:694-697, and its backward):

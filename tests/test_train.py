@@ -200,6 +200,46 @@ def test_ddp_gloo_two_ranks_match_single_process():
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_hip_fused_residual_block_matches_autograd(dtype):
+    """x + conv1x1(LayerNorm(x)) (turtle_t1_arch.py:808-809) with the residual fused: LayerNorm returns
+    x's alias, the GEMM adds it in its epilogue, the LayerNorm backward sums the residual gradient into
+    dx (turtle_train_ln_bwd dres) - against ATen autograd of the written form, values and gradients;
+    and the unfused fallback (an fp32 residual stream under bf16 autocast) still adds."""
+    from turtlevsr_amd.train_ops import HipOps
+    torch.manual_seed(1)
+    dev = "cuda"
+    tol = dict(rtol=1e-4, atol=1e-5) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    C, N = 64, 64
+    x = (torch.randn(2, C, 12, 10, device=dev) * 2 + 0.5).to(dtype).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    w = (1 + 0.1 * torch.randn(C, device=dev)).requires_grad_()
+    b = (0.1 * torch.randn(C, device=dev)).requires_grad_()
+    W = (0.1 * torch.randn(N, C, 1, 1, device=dev)).requires_grad_()
+    cb = (0.1 * torch.randn(N, device=dev)).requires_grad_()
+    gy = torch.randn(2, N, 12, 10, device=dev).to(dtype)
+    y, r = HipOps.layer_norm(x, w, b, False, residual=True)
+    assert r.data_ptr() == x.data_ptr()
+    out = HipOps.conv1x1(y, W, cb, res=r)
+    g = torch.autograd.grad(out, [x, w, b, W, cb], gy)
+    x2, w2, b2, W2, cb2 = (t.detach().float().requires_grad_() for t in (x, w, b, W, cb))
+    out2 = x2 + AtenOps.conv1x1(AtenOps.layer_norm(x2, w2, b2, False), W2, cb2)
+    g2 = torch.autograd.grad(out2, [x2, w2, b2, W2, cb2], gy.float())
+    torch.testing.assert_close(out.float(), out2, **tol)
+    for a, e in zip(g, g2):
+        torch.testing.assert_close(a.float(), e, rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
+    if dtype == torch.bfloat16:
+        xf = x.detach().float().contiguous(memory_format=torch.channels_last).requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y, r = HipOps.layer_norm(xf, w, b, False, residual=True)
+            out = HipOps.conv1x1(y, W, cb, res=r)              # fp32 residual: the add as written
+        assert out.dtype == torch.float32
+        gx, = torch.autograd.grad(out, [xf], gy.float())
+        torch.testing.assert_close(out, out2, **tol)
+        torch.testing.assert_close(gx, g2[0], rtol=tol["rtol"] * 10, atol=tol["atol"] * 100)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_hip_train_ops_match_autograd(dtype):
     from turtlevsr_amd.train_ops import HipOps
     torch.manual_seed(0)
@@ -441,16 +481,23 @@ def test_hip_gelu_window_conv3x3_match_autograd(dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", ["train_tiny", "train_tiny_hetero", "train_gopro"])
-def test_hip_training_graph_matches_reference_gradients(name):
+@pytest.mark.parametrize("name,accumulate", [("train_tiny", False), ("train_tiny", True), ("train_tiny_hetero", True),
+                                             ("train_gopro", True)])
+def test_hip_training_graph_matches_reference_gradients(name, accumulate):
     """fp32 on the GPU with the HIP kernels: loss and every parameter gradient vs the reference
-    (train_gopro: GoPro widths, 59 M parameters, 2 frames of 64x64 with BPTT through the caches)."""
+    (train_gopro: GoPro widths, 59 M parameters, 2 frames of 64x64 with BPTT through the caches).
+    ``accumulate``: Trainer.backward with the in-place parameter-gradient accumulator (one fp32 arena
+    per step, ParamGradAccumulator) - else autograd's per-use gradients and the literal 0 * sum(p)."""
     g, meta = load(name)
     net = _net(meta, None, "cuda")                   # default op set: HipOps
-    tr = Trainer(net, amp=None)
+    tr = Trainer(net, amp=None, accumulate_grads=accumulate)
+    assert (tr.acc is not None) == accumulate
     lq, gt = _data(meta, "cuda")
-    loss = tr.loss(lq, gt)
-    (loss + 0 * sum(p.sum() for p in net.parameters())).backward()
+    if accumulate:
+        loss = tr.backward(lq, gt)
+    else:
+        loss = tr.loss(lq, gt)
+        (loss + 0 * sum(p.sum() for p in net.parameters())).backward()
     torch.cuda.synchronize()
     assert float(loss.detach()) == pytest.approx(float(g["loss"]), rel=1e-4)
     assert _check_grads(net, g, rtol=1e-2, atol=1e-5) == meta["n_params"]
@@ -674,9 +721,7 @@ def _ddp_worker_gpu(rank, world, port, meta, q):
         tr = Trainer(net, amp=None)
         assert isinstance(tr.model, torch.nn.parallel.DistributedDataParallel)
         lq, gt = _data(meta, dev)
-        tr.opt.zero_grad()
-        loss = tr.loss(lq[rank:rank + 1], gt[rank:rank + 1])
-        (loss + 0 * sum(p.sum() for p in net.parameters())).backward()     # bucketed all-reduce (mean)
+        loss = tr.backward(lq[rank:rank + 1], gt[rank:rank + 1])   # bucketed all-reduce (mean), in-place accumulation
         torch.cuda.synchronize()
         grads = {k: p.grad.detach().cpu().numpy().copy() for k, p in net.named_parameters()}
         q.put((rank, grads, float(loss.detach())))
@@ -738,3 +783,67 @@ def test_sab_hip_dispatch_respects_key_limit():
     assert not _sab_hip_ok(o, "sab_softmax", SAB_MAX_KEYS + 1)
     assert not _sab_hip_ok(o, "sab_attention", 148, 128, 1024)        # n % 8
     assert not _sab_hip_ok(object(), "sab_softmax", 16)             # op set without the kernel (CPU)
+
+
+class _ToyLin(torch.autograd.Function):
+    """y = x w^T with the HIP ops' accumulator protocol (train_ops._acc_use / _acc_dst / _acc_done) in
+    plain torch arithmetic, so the bookkeeping runs on the CPU."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        from turtlevsr_amd import train_ops as T
+        ctx.save_for_backward(x, w)
+        ctx.acc = T._acc_use(ctx, 1, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        from turtlevsr_amd import train_ops as T
+        x, w = ctx.saved_tensors
+        g = dy.t() @ x
+        if ctx.acc is None:
+            return dy @ w, g
+        T._acc_dst(ctx.acc, g.numel()).add_(g.reshape(-1))
+        shape = w.shape
+        return dy @ w, T._acc_done(ctx.acc, lambda f: f.view(shape))
+
+
+def test_param_grad_accumulator_matches_autograd_on_cpu():
+    """ParamGradAccumulator: a weight used by three frames (and through a view), one also used by a
+    plain torch op, one never used (zero gradient from the 0 * sum(p) term) - the step's gradients
+    equal autograd's per-use sums; a use whose backward never runs is reported, not dropped."""
+    from turtlevsr_amd.train_ops import ParamGradAccumulator
+    torch.manual_seed(0)
+    w1 = torch.nn.Parameter(torch.randn(6, 4, 1, 1))
+    w2 = torch.nn.Parameter(torch.randn(4, 6))
+    w3 = torch.nn.Parameter(torch.randn(3))               # never used
+    params = [w1, w2, w3]
+    x = torch.randn(5, 4)
+
+    def loss():
+        h, tot = x, 0.0
+        for t in range(3):
+            h = torch.tanh(_ToyLin.apply(h, w1.reshape(6, 4)))
+            h = _ToyLin.apply(h, w2)
+            tot = tot + (h * (t + 1)).sum() + (w2 ** 2).sum() * 0.1
+        return tot
+
+    ref = loss() + 0 * sum(p.sum() for p in params)
+    ref.backward()
+    want = [p.grad.clone() for p in params]
+    for p in params:
+        p.grad = None
+    acc = ParamGradAccumulator(params)
+    with acc.step():
+        l = loss() + acc.zero_term(params)
+        l.backward()
+    for p, r in zip(params, want):
+        torch.testing.assert_close(p.grad, r, rtol=1e-5, atol=1e-6)
+    assert torch.count_nonzero(w3.grad) == 0
+    assert w1.grad.untyped_storage().nbytes() == 4 * acc.total      # w1's sum is the arena slice itself
+    for p in params:
+        p.grad = None
+    with pytest.raises(RuntimeError, match="never ran"):
+        with acc.step():
+            (loss() + acc.zero_term(params)).backward()
+            _ToyLin.apply(x, w1.reshape(6, 4))              # a counted use with no backward

@@ -27,11 +27,25 @@ WATCH = ("copy_", "_to_copy", "clone", "cat", "fill_", "zero_", "zeros", "add", 
 
 
 def _site():
-    for fr in reversed(traceback.extract_stack()[:-3]):
-        f = fr.filename
-        if "turtlevsr_amd" in f or ("tools" in f and "train_sites" not in f):
-            return f"{os.path.basename(f)}:{fr.lineno} {fr.name}"
-    return "<engine>"
+    fr_in = [fr for fr in reversed(traceback.extract_stack()[:-3])
+             if "turtlevsr_amd" in fr.filename or ("tools" in fr.filename and "train_sites" not in fr.filename)]
+    if fr_in:
+        return " < ".join(f"{os.path.basename(fr.filename)}:{fr.lineno} {fr.name}" for fr in fr_in[:2])
+    node = torch._C._current_autograd_node()       # the backward node the engine is running (or None)
+    if node is None:
+        return "<engine>"
+    where = ""
+    try:                                            # anomaly mode keeps the node's forward stack
+        tb = node.metadata.get("traceback_")
+        if tb:
+            lines = [ln for ln in "".join(tb).splitlines() if "turtlevsr_amd" in ln and "File" in ln]
+            if lines:
+                ln = lines[-1].strip()
+                f = ln.split('"')[1]
+                where = f" fwd {os.path.basename(f)}:{ln.split('line ')[1].split(',')[0]}"
+    except Exception:                               # noqa: BLE001 - attribution only
+        pass
+    return f"<engine: {node.name()}{where}>"
 
 
 class Log(TorchDispatchMode):
@@ -57,6 +71,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--res", type=int, default=256)
     ap.add_argument("--frames", type=int, default=5)
+    ap.add_argument("--no-acc", action="store_true", help="autograd's per-use parameter gradients (no accumulator)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     opt = bench.load_opt()
@@ -64,13 +79,13 @@ def main():
     shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
     net.load_state_dict({k: torch.from_numpy(v) for k, v in synthetic_state_dict(shapes, 0).items()})
     net = net.to(dev).train()
-    tr = Trainer(net, amp="bf16")
+    tr = Trainer(net, amp="bf16", accumulate_grads=not a.no_acc)
     lq = torch.from_numpy(synthetic_frames((a.batch, a.frames, 3, a.res, a.res), 1, name="lq")).to(dev)
     gt = torch.from_numpy(synthetic_frames((a.batch, a.frames, 3, a.res, a.res), 1, name="gt")).to(dev)
     tr.train_step(lq, gt)                                       # warm caches (weight casts, workspaces)
     torch.cuda.synchronize()
     log = Log()
-    with log:
+    with torch.autograd.set_detect_anomaly(True, check_nan=False), log:
         tr.train_step(lq, gt)
     torch.cuda.synchronize()
     tot_n, tot_b = sum(log.n.values()), sum(log.b.values())

@@ -143,6 +143,7 @@ template <typename T, typename TY, int G, int NCH>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ w,
                                                      const float* __restrict__ mu, const float* __restrict__ rstd,
                                                      const TY* __restrict__ dy, int64_t lddy, T* __restrict__ dx, int64_t lddx,
+                                                     const T* __restrict__ dres, int64_t lddres,
                                                      float* __restrict__ dw, float* __restrict__ db, int64_t P, int C,
                                                      int biasfree, int ppb) {
   extern __shared__ float sred[];                  // [2][C]
@@ -185,11 +186,16 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ x, in
     for (int j = 0; j < NCH; ++j) {
       const int c = 8 * (l + G * j);
       if (c >= C) continue;
-      float o[8];
+      float o[8], rg[8];
+      if (dres) ld8f(dres + pp * lddres + c, rg);     // the residual branch's gradient, summed in here
+      else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rg[e] = 0.f;
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float g = w[c + e] * gy[j][e];
-        o[e] = biasfree ? r * g - (xv[j][e] - m) * r * r * r * mgx : r * (g - mg - (xv[j][e] - m) * r * mgx);
+        o[e] = rg[e] + (biasfree ? r * g - (xv[j][e] - m) * r * r * r * mgx : r * (g - mg - (xv[j][e] - m) * r * mgx));
         if (live) {
           aw[j][e] = fmaf(gy[j][e], biasfree ? xv[j][e] * r : (xv[j][e] - m) * r, aw[j][e]);
           ab[j][e] += gy[j][e];
@@ -1058,7 +1064,7 @@ int ln_fwd(const void* x, int64_t ldx, const float* w, const float* b, void* y, 
 }
 template <typename T, typename TY = T>
 int ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy, int64_t lddy, void* dx,
-           int64_t lddx, float* dw, float* db, int64_t P, int C, int biasfree, hipStream_t st) {
+           int64_t lddx, const void* dres, int64_t lddres, float* dw, float* db, int64_t P, int C, int biasfree, hipStream_t st) {
   const int G = ln_group(C), nch = (C / 8 + G - 1) / G;
   // ~512 blocks whatever P is (a fixed 256 pixels per block left a 32 x 32 x 8 latent map on 32
   // blocks); pixels per block a multiple of the block's pixel slots
@@ -1069,7 +1075,8 @@ int ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const fl
 #define LNB(GG, NN)                                                                                                       \
   if (G == GG && nch <= NN) {                                                                                             \
     hipLaunchKernelGGL((ln_bwd_kernel<T, TY, GG, NN>), dim3((unsigned)blocks), dim3(256), 2 * C * sizeof(float), st, (const T*)x, \
-                       ldx, w, mu, rstd, (const TY*)dy, lddy, (T*)dx, lddx, dw, db, P, C, biasfree, (int)ppb);                \
+                       ldx, w, mu, rstd, (const TY*)dy, lddy, (T*)dx, lddx, (const T*)dres, lddres, dw, db, P, C, biasfree,  \
+                       (int)ppb);                                                                                         \
     return 0;                                                                                                             \
   }
   LNB(1, 1) LNB(2, 1) LNB(4, 1) LNB(8, 1) LNB(16, 1) LNB(32, 1) LNB(64, 1) LNB(64, 2) LNB(64, 4)
@@ -1321,24 +1328,24 @@ int turtle_train_ln_fwd(const void* x, int64_t ldx, const float* w, const float*
 }
 
 int turtle_train_ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy,
-                        int64_t lddy, void* dx, int64_t lddx, float* dw, float* db, int64_t P, int C, int biasfree, int dtype,
-                        void* stream) {
-  // dtype as turtle_train_ln_fwd: x and dx in x's type, dy in y's type
+                        int64_t lddy, void* dx, int64_t lddx, const void* dres, int64_t lddres, float* dw, float* db, int64_t P,
+                        int C, int biasfree, int dtype, void* stream) {
+  // dtype as turtle_train_ln_fwd: x, dx and dres in x's type, dy in y's type
   const int xdt = dtype & 15, ydt = (dtype >> 4) ? (dtype >> 4) - 1 : xdt;
-  if (!rows_ok(x, ldx, xdt) || !rows_ok(dy, lddy, ydt) || !rows_ok(dx, lddx, xdt) || !w || !mu || !rstd || !dw ||
-      P <= 0 || C <= 0 || C % 8 || C > 2048)
+  if (!rows_ok(x, ldx, xdt) || !rows_ok(dy, lddy, ydt) || !rows_ok(dx, lddx, xdt) || (dres && !rows_ok(dres, lddres, xdt)) ||
+      !w || !mu || !rstd || !dw || P <= 0 || C <= 0 || C % 8 || C > 2048)
     return -1;
   float* dbb = biasfree ? nullptr : db;
   if (xdt != ydt) {
     int rc;
     if (xdt == 0 && ydt == 1)
-      rc = ln_bwd<float, bf16>(x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dw, dbb, P, C, biasfree, (hipStream_t)stream);
+      rc = ln_bwd<float, bf16>(x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dres, lddres, dw, dbb, P, C, biasfree, (hipStream_t)stream);
     else if (xdt == 0 && ydt == 2)
-      rc = ln_bwd<float, f16>(x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dw, dbb, P, C, biasfree, (hipStream_t)stream);
+      rc = ln_bwd<float, f16>(x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dres, lddres, dw, dbb, P, C, biasfree, (hipStream_t)stream);
     else return -1;
     return rc ? rc : (int)hipGetLastError();
   }
-  TT_DISPATCH(xdt, ln_bwd, x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dw, dbb, P, C, biasfree, (hipStream_t)stream);
+  TT_DISPATCH(xdt, ln_bwd, x, ldx, w, mu, rstd, dy, lddy, dx, lddx, dres, lddres, dw, dbb, P, C, biasfree, (hipStream_t)stream);
 }
 
 int turtle_train_dw3x3_fwd(const void* x, int64_t ldx, const float* w9, const float* b, void* y, int64_t ldy, int64_t N, int C,
@@ -1453,9 +1460,10 @@ int turtle_train_gram_wd(const float* D, const float* aq, const float* ak, void*
   TT_DISPATCH(dtype, gram_wd, D, aq, ak, wd, B, c, heads, (hipStream_t)stream);
 }
 
-int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride, int64_t img_px, const float* bias, void* y,
-                      int64_t ldy, int64_t P, int K, int N, int dtype, void* stream) {
+int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride, int64_t img_px, const float* bias,
+                      const void* res, int64_t ldr, void* y, int64_t ldy, int64_t P, int K, int N, int dtype, void* stream) {
   if (dtype != 0 && dtype != 1) return -1;
+  if (res && (!rows_ok(res, ldr, dtype) || ldr < N)) return -1;
   if (!rows_ok(x, ldx, dtype) || !rows_ok(y, ldy, dtype) || !w || P <= 0 || K <= 0 || N <= 0 || K % 8 || N % 8 || ldx < K ||
       ldy < N || (wstride && (img_px <= 0 || P % img_px)) || (img_px > 0 && img_px >= ((int64_t)1 << 31)) || N > TURTLE_CONST_VEC ||
       K > TURTLE_CONST_VEC)
@@ -1467,6 +1475,7 @@ int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride
   g.HW = (int)(img_px > 0 ? img_px : std::min<int64_t>(P, (int64_t)1 << 30)); g.Wimg = g.HW;
   g.w = w; g.ldw = K; g.wstride = wstride; g.wdiv = 1;
   g.bias = bias; g.out = y; g.ldo = ldy; g.offo = 0; g.store_mode = STORE_NHWC;
+  g.res = res; g.ldr = ldr; g.offr = 0;
   g.zeros = train_consts(0); g.ones = train_consts(1);
   if (!g.zeros) return (int)hipErrorOutOfMemory;
   g.allow_panel = g.allow_lds = g.allow_pn = g.allow_ar = g.allow_kt = 1;

@@ -46,6 +46,15 @@ def _l2n(x, dim):
     return x / x.norm(dim=dim, keepdim=True).clamp_min(L2_EPS)
 
 
+def _res(res):
+    """The residual keyword for an op set's conv1x1 (absent when there is none: ATen op sets)."""
+    return {} if res is None else {"res": res}
+
+
+def _plus(res, a):
+    return a if res is None else res + a
+
+
 def _conv1(m, x):
     return F.conv2d(x, m.weight, m.bias)
 
@@ -219,37 +228,39 @@ class TrainGraph:
         y = ops.conv3x3(x, wp, bp)
         return y[:, :n] if n8 != n else y
 
-    def _c1(self, m, x):                            # nn.Conv2d(K, N, 1): the op set's GEMM when it has one
+    def _c1(self, m, x, res=None):                  # nn.Conv2d(K, N, 1): the op set's GEMM when it has one
         ops = self._ops()
         if hasattr(ops, "conv1x1"):
-            return ops.conv1x1(x, m.weight, m.bias)
-        return _conv1(m, x)
+            return ops.conv1x1(x, m.weight, m.bias, **_res(res))
+        return _plus(res, _conv1(m, x))
 
-    def _c1_scaled(self, m, x, scale):
+    def _c1_scaled(self, m, x, scale, res=None):
         """nn.Conv2d(K, N, 1)(x) * scale (scale [1, N, 1, 1]: FeedForward's gamma, ReducedAttn's
         beta) with the scale folded into the weights and bias - W' = diag(scale) W, b' = scale b, tiny
         ops autograd differentiates - so the full-size multiply and its two backward passes (the
         input gradient and gamma's reduction over every pixel) do not run on the op set's GEMM."""
         ops = self._ops()
         if not hasattr(ops, "conv1x1"):
-            return _conv1(m, x) * scale
+            return _plus(res, _conv1(m, x) * scale)
         sv = scale.reshape(-1)
         w = m.weight.reshape(m.weight.shape[0], m.weight.shape[1]) * sv[:, None]
         b = None if m.bias is None else m.bias * sv
-        return ops.conv1x1(x, w, b)
+        return ops.conv1x1(x, w, b, **_res(res))
 
-    def _gffw(self, m, x):                          # GatedFeedForward 159-178
-        return self._c1(m.project_out, self._ops().gelu_gate(self._dw(m.dwconv, self._c1(m.project_in, x))))
+    # ``res`` (every branch): the block's residual stream, returned as res + branch(x) - on op sets
+    # with fused residuals the add is the last GEMM's epilogue (turtle_t1_arch.py:808-809)
+    def _gffw(self, m, x, res=None):                # GatedFeedForward 159-178
+        return self._c1(m.project_out, self._ops().gelu_gate(self._dw(m.dwconv, self._c1(m.project_in, x))), res)
 
     def _gelu(self, x):
         ops = self._ops()
         return ops.gelu(x) if hasattr(ops, "gelu") else F.gelu(x)
 
-    def _ffw(self, m, x):                           # FeedForward 181-210
-        return self._c1_scaled(m.conv5, self._gelu(self._c1(m.conv4, x)), m.gamma)
+    def _ffw(self, m, x, res=None):                 # FeedForward 181-210
+        return self._c1_scaled(m.conv5, self._gelu(self._c1(m.conv4, x)), m.gamma, res)
 
-    def _reduced(self, m, x):                       # ReducedAttn 704-742
-        return self._c1_scaled(m.conv3, self._gelu(self._dw(m.conv2, self._c1(m.conv1, x))), m.beta)
+    def _reduced(self, m, x, res=None):             # ReducedAttn 704-742
+        return self._c1_scaled(m.conv3, self._gelu(self._dw(m.conv2, self._c1(m.conv1, x))), m.beta, res)
 
     def _window(self, x, conv, ws, g):
         """SAB window convolution (k2_dwconv / q2_dwconv: ws x ws, stride ws, padding 1, groups = channels;
@@ -270,7 +281,7 @@ class TrainGraph:
         b, c, h, w = t.shape
         return t.reshape(b, heads, c // heads, h * w)
 
-    def _chan(self, m, x, heads, kc=None, vc=None, ntc=None):
+    def _chan(self, m, x, heads, kc=None, vc=None, ntc=None, res=None):
         """ChannelAttention 666-702; with caches / ntc: FrameHistoryRouter 218-286."""
         b, c, h, w = x.shape
         qkv = self._dw(m.qkv_dwconv, self._c1(m.qkv, x))
@@ -289,7 +300,7 @@ class TrainGraph:
             a = torch.softmax(ops.norm_gram(qk, heads, **kw(0)) * m.temperature, dim=-1)
             wp = m.project_out.weight.reshape(c, heads, ch)
             weff = torch.einsum("ohi,bhij->bohj", wp, a).reshape(b, c, c)
-            return ops.conv1x1(v, weff, m.project_out.bias, **kw(2 * c)), None, None
+            return ops.conv1x1(v, weff, m.project_out.bias, **kw(2 * c), **_res(res)), None, None
         if ntc is None and kc is None and vc is None and hasattr(ops, "gram"):
             # on the op set's kernels: Gram of the raw q, k over HW (per head) divided by the L2
             # norms (== normalising first, 690-693), softmax, then project_out . blockdiag(A) as
@@ -302,16 +313,16 @@ class TrainGraph:
             a = torch.softmax(G / (nq * nk) * m.temperature, dim=-1)
             wp = m.project_out.weight.reshape(c, heads, ch)
             weff = torch.einsum("ohi,bhij->bohj", wp, a).reshape(b, c, c)
-            return ops.conv1x1(v, weff, m.project_out.bias), None, None
+            return ops.conv1x1(v, weff, m.project_out.bias, **_res(res)), None, None
         if hasattr(ops, "cross_gram"):
-            return self._chan_hist(m, qkv, heads, kc, vc, ntc)
+            return self._chan_hist(m, qkv, heads, kc, vc, ntc, res)
         q, k, v = _split(qkv, c, c, c)
         q, k, v = _l2n(self._heads(q, heads), -1), _l2n(self._heads(k, heads), -1), self._heads(v, heads)
         if kc is not None and vc is not None:
             k = torch.cat([kc.to(k.dtype), k], dim=2)
             v = torch.cat([vc.to(v.dtype), v], dim=2)
         a = torch.softmax(q @ k.transpose(-2, -1) * m.temperature, dim=-1)
-        out = self._c1(m.project_out, (a @ v).reshape(b, c, h, w))
+        out = self._c1(m.project_out, (a @ v).reshape(b, c, h, w), res)
         if ntc is None:
             return out, None, None
         keep = int(ntc * c / heads)
@@ -338,7 +349,7 @@ class TrainGraph:
         out = torch.cat([c6.to(cur.dtype), cur6], dim=4)
         return out.reshape(b, h, w, heads * (t + 1) * ch).permute(0, 3, 1, 2), t
 
-    def _chan_hist(self, m, qkv, heads, kc, vc, ntc):
+    def _chan_hist(self, m, qkv, heads, kc, vc, ntc, res=None):
         """FrameHistoryRouter / the CHM's channel attention over the cached frames (turtle_t1_arch.py:218-286,
         649-660) on the op set's kernels: q, k L2-normalised over HW per channel (norm_cols), the scores
         q_hat [k_cache ; k_hat]^T of all head pairs as one reduction GEMM (cross_gram; each head's block
@@ -358,7 +369,7 @@ class TrainGraph:
         a = torch.softmax(Gh * m.temperature, dim=-1)
         wp = m.project_out.weight.reshape(c, heads, ch)
         weff = torch.einsum("ohi,bhik->bohk", wp, a).reshape(b, c, heads * L)
-        out = ops.conv1x1(V, weff, m.project_out.bias)
+        out = ops.conv1x1(V, weff, m.project_out.bias, **_res(res))
         if ntc is None:
             return out, None, None
         keep = int(ntc * c / heads)
@@ -471,7 +482,7 @@ class TrainGraph:
         o = self._c1(m.project_out, self._undilated(vt, b * t, c, hl, wl, ws)).reshape(b, t, c, hl, wl)
         return o, kt[:, -ntc:], vt[:, -ntc:]
 
-    def _chm(self, m, x, heads, ws, ntc, kc, vc):
+    def _chm(self, m, x, heads, ws, ntc, kc, vc, res=None):
         """CausalHistoryModel 612-662."""
         b, c, h, w = x.shape
         sab = self._sab_t0 if self.arch.t0 else self._sab
@@ -483,30 +494,41 @@ class TrainGraph:
         if hasattr(ops, "cross_gram"):
             # the aligned frames' k, v as per-frame channels-last maps: the history concatenation
             # (_hist_cat) reads them in place; k L2-normalised per frame and channel over HW (649-651)
-            out, _, _ = self._chan(m.ChanAttn, x, heads, _Frames(ops.norm_cols(kh), t), _Frames(vh, t), ntc=1)
+            out, _, _ = self._chan(m.ChanAttn, x, heads, _Frames(ops.norm_cols(kh), t), _Frames(vh, t), ntc=1, res=res)
             return out, k_keep, v_keep
         ch = c // heads
         kh = kh.reshape(b, t, heads, ch, h * w).transpose(1, 2).reshape(b, heads, t * ch, h * w)
         vh = vh.reshape(b, t, heads, ch, h * w).transpose(1, 2).reshape(b, heads, t * ch, h * w)
-        out, _, _ = self._chan(m.ChanAttn, x, heads, _l2n(kh, -1), vh, ntc=1)
+        out, _, _ = self._chan(m.ChanAttn, x, heads, _l2n(kh, -1), vh, ntc=1, res=res)
         return out, k_keep, v_keep
 
+    def _ln_res(self, m, x):
+        """(LayerNorm(x), r): r is x for the residual add - on op sets with fused residuals an alias
+        whose gradient the LayerNorm backward sums into its own (no separate gradient add), else None
+        (the branch result is added as written)."""
+        ops = self._ops()
+        if getattr(ops, "fused_residual", False):
+            return ops.layer_norm(x, m.body.weight, getattr(m.body, "bias", None), self.arch.ln_type == "BiasFree",
+                                  residual=True)
+        return self._ln(m, x), None
+
     def _block(self, spec, m, x, kc=None, vc=None):
-        """TurtleAttnBlock 804-811."""
+        """TurtleAttnBlock 804-811: x = x + attn(norm1(x)); x = x + ffn(norm2(x))."""
         k_out = v_out = None
         if spec.attn != "NoAttn":
-            y = self._ln(m.norm1, x)
+            y, r = self._ln_res(m.norm1, x)
             if spec.attn == "ReducedAttn":
-                a = self._reduced(m.attn, y)
+                a = self._reduced(m.attn, y, r)
             elif spec.attn == "Channel":
-                a, _, _ = self._chan(m.attn, y, spec.heads)
+                a, _, _ = self._chan(m.attn, y, spec.heads, res=r)
             elif spec.attn == "FHR":
-                a, k_out, v_out = self._chan(m.attn, y, spec.heads, kc, vc, ntc=spec.ntc)
+                a, k_out, v_out = self._chan(m.attn, y, spec.heads, kc, vc, ntc=spec.ntc, res=r)
             else:
-                a, k_out, v_out = self._chm(m.attn, y, spec.heads, spec.ws, spec.ntc, kc, vc)
-            x = x + a
-        y = self._ln(m.norm2, x)
-        x = x + (self._gffw(m.ffn, y) if spec.ffn == "GFFW" else self._ffw(m.ffn, y))
+                a, k_out, v_out = self._chm(m.attn, y, spec.heads, spec.ws, spec.ntc, kc, vc, res=r)
+            x = a if r is not None else x + a
+        y, r = self._ln_res(m.norm2, x)
+        f = self._gffw(m.ffn, y, r) if spec.ffn == "GFFW" else self._ffw(m.ffn, y, r)
+        x = f if r is not None else x + f
         return x, k_out, v_out
 
     def _level(self, name, x, kc=None, vc=None):    # LevelBlock 856-865
@@ -590,7 +612,7 @@ class Trainer:
     in DistributedDataParallel (RCCL on ROCm) with ``bucket_mb`` gradient buckets."""
 
     def __init__(self, net: TurtleTrain, lr: float = 4e-4, betas=(0.9, 0.99), weight_decay: float = 0.0,
-                 amp: Optional[str] = "bf16", bucket_mb: int = 64):
+                 amp: Optional[str] = "bf16", bucket_mb: int = 64, accumulate_grads: bool = True):
         self.net = net
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         dev = next(net.parameters()).device
@@ -605,6 +627,10 @@ class Trainer:
                                      weight_decay=weight_decay)
         self.amp = amp
         self.scaler = torch.amp.GradScaler("cuda", enabled=(amp == "fp16" and dev.type == "cuda"))
+        # the op set's in-place parameter-gradient accumulation (train_ops.ParamGradAccumulator):
+        # one fp32 arena per step instead of per-use gradients added by autograd
+        make_acc = getattr(net._ops(), "param_grad_accumulator", None) if accumulate_grads else None
+        self.acc = make_acc(list(net.parameters())) if make_acc is not None else None
 
     def _autocast(self):
         if self.amp is None or self.device.type != "cuda":
@@ -624,17 +650,30 @@ class Trainer:
                 total = total + F.l1_loss(out.float(), gt[:, j].float())
         return total / T
 
+    def backward(self, lq: torch.Tensor, gt: torch.Tensor) -> torch.Tensor:
+        """Forward and backward of one iteration (video_restoration_model.py:84-102): the parameter
+        gradients (scaled under fp16) land in ``.grad``; returns the detached pixel loss. With the
+        op set's accumulator every weight gradient is summed in place over the clip's frames."""
+        self.opt.zero_grad(set_to_none=True)
+        if self.acc is not None:
+            with self.acc.step():
+                l_pix = self.loss(lq, gt)
+                l_total = l_pix + self.acc.zero_term(list(self.net.parameters()))
+                self.scaler.scale(l_total).backward()
+        else:
+            l_pix = self.loss(lq, gt)
+            l_total = l_pix + 0 * sum(p.sum() for p in self.net.parameters())
+            self.scaler.scale(l_total).backward()
+        return l_pix.detach()
+
     def train_step(self, lq: torch.Tensor, gt: torch.Tensor) -> float:
         """One iteration; returns the loss averaged over ranks (valid on rank 0, like
         reduce_loss_dict)."""
-        self.opt.zero_grad(set_to_none=True)
-        l_pix = self.loss(lq, gt)
-        l_total = l_pix + 0 * sum(p.sum() for p in self.net.parameters())
-        self.scaler.scale(l_total).backward()
+        l_pix = self.backward(lq, gt)
         self.scaler.unscale_(self.opt)
         self.scaler.step(self.opt)
         self.scaler.update()
-        red = l_pix.detach().clone()
+        red = l_pix.clone()
         if self.world > 1:                           # base_model.py:340-365: reduce to rank 0, / world
             dist.reduce(red, dst=0)
             if dist.get_rank() == 0:

@@ -45,13 +45,13 @@ def lib():
     L = _lib.lib()
     vp, i64, ci, sz = C.c_void_p, C.c_int64, C.c_int, C.c_size_t
     L.turtle_train_ln_fwd.argtypes = [vp, i64, vp, vp, vp, i64, vp, vp, i64, ci, ci, ci, vp]
-    L.turtle_train_ln_bwd.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, vp, i64, ci, ci, ci, vp]
+    L.turtle_train_ln_bwd.argtypes = [vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, vp, vp, i64, ci, ci, ci, vp]
     L.turtle_train_dw3x3_fwd.argtypes = [vp, i64, vp, vp, vp, i64, i64, ci, ci, ci, ci, ci, vp]
     L.turtle_train_dw3x3_wgrad.argtypes = [vp, i64, vp, i64, vp, vp, i64, ci, ci, ci, ci, vp]
     L.turtle_train_gate_fwd.argtypes = [vp, i64, vp, i64, i64, ci, ci, vp]
     L.turtle_train_gate_bwd.argtypes = [vp, i64, vp, i64, vp, i64, i64, ci, ci, vp]
     L.turtle_train_colsum.argtypes = [vp, i64, vp, i64, ci, ci, vp]
-    L.turtle_train_gemm.argtypes = [vp, i64, vp, i64, i64, vp, vp, i64, i64, ci, ci, ci, vp]
+    L.turtle_train_gemm.argtypes = [vp, i64, vp, i64, i64, vp, vp, i64, vp, i64, i64, ci, ci, ci, vp]
     L.turtle_train_rgemm_workspace.argtypes = [i64, ci, ci, i64]
     L.turtle_train_rgemm_workspace.restype = sz
     L.turtle_train_rgemm.argtypes = [vp, i64, vp, i64, vp, i64, ci, ci, i64, ci, ci, vp, sz, vp]
@@ -124,13 +124,145 @@ def _gemm_dt(x: torch.Tensor) -> torch.dtype:
     return torch.float32 if x.dtype == torch.float32 else torch.bfloat16
 
 
+class ParamGradAccumulator:
+    """In-place parameter-gradient accumulation over one training step.
+
+    A clip of T frames uses every weight T times (plus the reference's 0 * sum(p) term,
+    video_restoration_model.py:99), so autograd builds T per-use fp32 gradients of each parameter
+    and adds them pairwise in the AccumulateGrad input buffer - about 4 000 fp32 adds, 1 300 fills
+    and the term's 633 sums / expands / adds per GoPro step (profiles/r06f_train_sites.txt). Inside
+    ``step()`` the HIP ops instead accumulate each use's weight / bias gradient in place into one
+    zero-filled fp32 arena (the reduction GEMM's accumulate mode, the atomics of the LayerNorm /
+    depthwise / window / column-sum reductions), return None for every use but the last backward one
+    of a parameter, and hand autograd the finished sum there: one AccumulateGrad per parameter, as
+    before, with no adds. Uses are counted in the forward; a use whose backward never runs leaves a
+    count behind and ``step()`` raises rather than dropping that parameter's gradient.
+
+    ``zero_term(params)`` is the reference's 0 * sum(p) term with the same (zero) gradient for the
+    parameters no HIP op reported, and none for the others - they receive a real gradient anyway."""
+
+    def __init__(self, params):
+        self.slot, off = {}, 0
+        for p in params:
+            if p.requires_grad and p.dtype == torch.float32 and id(p) not in self.slot:
+                self.slot[id(p)] = (p, off)
+                off += (p.numel() + 15) // 16 * 16             # 64-byte aligned slices
+        self.total = off
+        self.arena, self.count = None, {}
+
+    def use(self, w):
+        """The parameter behind ``w`` (itself or the base of a view of it) when its gradient is
+        accumulated here - one more pending use - else None."""
+        if w is None or not w.requires_grad:
+            return None
+        base = w if w.is_leaf else w._base
+        s = self.slot.get(id(base))
+        if s is None or s[0] is not base:
+            return None
+        self.count[id(base)] = self.count.get(id(base), 0) + 1
+        return base
+
+    def buf(self, p, n: int):
+        """The parameter's first ``n`` fp32 accumulators (flat)."""
+        off = self.slot[id(p)][1]
+        return self.arena[off:off + n]
+
+    def done(self, p, make):
+        """One use's backward finished: None, or ``make(flat slot)`` after the last one."""
+        k = id(p)
+        self.count[k] -= 1
+        if self.count[k]:
+            return None
+        del self.count[k]
+        return make(self.buf(p, p.numel()))
+
+    def zero_term(self, params):
+        return _ZeroTerm.apply(self, *params)
+
+    def step(self):
+        return _AccStep(self)
+
+
+class _AccStep:
+    def __init__(self, acc):
+        self.acc = acc
+
+    def __enter__(self):
+        global _ACC
+        if _ACC is not None:
+            raise RuntimeError("nested ParamGradAccumulator steps")
+        a = self.acc
+        dev = next(iter(a.slot.values()))[0].device if a.slot else None
+        a.arena = torch.zeros(max(a.total, 16), dtype=torch.float32, device=dev)
+        a.count = {}
+        _ACC = a
+        return a
+
+    def __exit__(self, et, ev, tb):
+        global _ACC
+        _ACC = None
+        a = self.acc
+        left, a.count, a.arena = a.count, {}, None
+        if et is None and left:
+            names = sorted(tuple(a.slot[k][0].shape) for k in left)[:4]
+            raise RuntimeError(f"{len(left)} parameters kept gradient uses whose backward never ran (shapes {names})")
+        return False
+
+
+_ACC = None
+
+
+def _acc_use(ctx, i: int, w):
+    """(accumulator, parameter) for input ``i`` (= ``w``) of an autograd Function's forward inside an
+    accumulating step when that input takes a gradient (forward runs in no-grad mode: the
+    Function's needs_input_grad says whether this use will see a backward), else None."""
+    a = _ACC
+    if a is None or not ctx.needs_input_grad[i]:
+        return None
+    p = a.use(w)
+    return None if p is None else (a, p)
+
+
+def _acc_dst(acc, n: int):
+    """A use's gradient destination: the parameter's fp32 arena slice (accumulated into), or None."""
+    return None if acc is None else acc[0].buf(acc[1], n)
+
+
+def _acc_done(acc, make):
+    return acc[0].done(acc[1], make)
+
+
+class _ZeroTerm(torch.autograd.Function):
+    """0 * sum(p.sum()) over ``params`` (video_restoration_model.py:99) as far as the step sees it:
+    a zero added to the loss and a zero gradient for the parameters not accumulated by ``acc``.
+    (The reference's term would also turn the - never used - total loss value into NaN for a
+    non-finite parameter; the loss reported is l_pix in both.)"""
+
+    @staticmethod
+    def forward(ctx, acc, *params):
+        ctx.covered = [id(p) in acc.count for p in params]
+        ctx.shapes = [(p.shape, p.dtype, p.device) for p in params]
+        dev = params[0].device if params else None
+        return torch.zeros((), dtype=torch.float32, device=dev)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None,) + tuple(None if c else torch.zeros(s, dtype=d, device=dv)
+                               for c, (s, d, dv) in zip(ctx.covered, ctx.shapes))
+
+
 class _LayerNorm(torch.autograd.Function):
     """y = LayerNorm(x) in ``out_dtype``: an fp32 x (the residual stream under autocast, promoted by
     the fp32 gamma / beta scales as in the reference) is read as fp32 and y written in the autocast
-    dtype by the kernel itself, and the backward writes dx in fp32 - no cast passes either way."""
+    dtype by the kernel itself, and the backward writes dx in fp32 - no cast passes either way.
+
+    ``residual``: also return x itself (an alias) for the block's residual use, x + branch(LN(x))
+    (turtle_t1_arch.py:808-809). Its gradient then comes back into this backward, which the kernel
+    adds into dx - autograd would otherwise sum x's two gradients with a separate full-size add."""
 
     @staticmethod
-    def forward(ctx, x, w, b, biasfree: bool, out_dtype):
+    def forward(ctx, x, w, b, biasfree: bool, out_dtype, residual: bool = False):
+        x_in = x
         x, ldx = rows(x)
         B, Cc, H, W = x.shape
         P = B * H * W
@@ -144,21 +276,33 @@ class _LayerNorm(torch.autograd.Function):
                                          _stream(x)), "ln_fwd")
         ctx.save_for_backward(x, w32, mu, rs)
         ctx.biasfree, ctx.has_b, ctx.ldx, ctx.ydt = biasfree, b is not None, ldx, y.dtype
-        return y
+        ctx.acc_w, ctx.acc_b, ctx.w_shape = _acc_use(ctx, 1, w), _acc_use(ctx, 2, b), w.shape
+        return (y, x_in.view_as(x_in)) if residual else y
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dy, dres=None):
         x, w32, mu, rs = ctx.saved_tensors
         dy, lddy = rows(dy.to(ctx.ydt))
+        if dres is not None:
+            dres, lddres = rows(dres.to(x.dtype))
         B, Cc, H, W = x.shape
         P = B * H * W
         dx = _empty(B, Cc, H, W, x)
-        z = torch.zeros(2 * Cc if ctx.has_b else Cc, dtype=torch.float32, device=x.device)    # one fill for both
-        dw, db = z[:Cc], (z[Cc:] if ctx.has_b else None)
+        aw, ab = ctx.acc_w, ctx.acc_b
+        dw, db = _acc_dst(aw, Cc), (_acc_dst(ab, Cc) if ctx.has_b else None)
+        nz = (Cc if dw is None else 0) + (Cc if ctx.has_b and db is None else 0)
+        if nz:
+            z = torch.zeros(nz, dtype=torch.float32, device=x.device)                    # one fill for both
+            dw = z[:Cc] if dw is None else dw
+            db = z[nz - Cc:] if ctx.has_b and db is None else db
         dt = _dt(x) | ((_dt(dy) + 1) << 4 if dy.dtype != x.dtype else 0)
-        _check(lib().turtle_train_ln_bwd(_p(x), ctx.ldx, _p(w32), _p(mu), _p(rs), _p(dy), lddy, _p(dx), Cc, _p(dw), _p(db), P, Cc,
-                                         int(ctx.biasfree), dt, _stream(x)), "ln_bwd")
-        return dx, dw, db, None, None
+        _check(lib().turtle_train_ln_bwd(_p(x), ctx.ldx, _p(w32), _p(mu), _p(rs), _p(dy), lddy, _p(dx), Cc, _p(dres),
+                                         lddres if dres is not None else 0, _p(dw), _p(db), P, Cc, int(ctx.biasfree), dt,
+                                         _stream(x)), "ln_bwd")
+        shape = ctx.w_shape
+        dw = _acc_done(aw, lambda f: f.view(shape)) if aw else dw
+        db = _acc_done(ab, lambda f: f.view(shape)) if ab else db
+        return dx, dw, db, None, None, None
 
 
 _DWCACHE = WeakIdKeyDictionary()
@@ -189,6 +333,7 @@ class _DWConv(torch.autograd.Function):
         _check(lib().turtle_train_dw3x3_fwd(_p(x), ldx, _p(w9), _p(b32), _p(y), Cc, B, Cc, H, W, 0, _dt(x), _stream(x)), "dw_fwd")
         ctx.save_for_backward(x, w9)
         ctx.has_b, ctx.ldx = b is not None, ldx
+        ctx.acc_w, ctx.acc_b = _acc_use(ctx, 1, w), _acc_use(ctx, 2, b)
         return y
 
     @staticmethod
@@ -202,10 +347,18 @@ class _DWConv(torch.autograd.Function):
         # passed as a plain forward so the row-sweeping kernel takes it
         w9f = ctx.w9f
         _check(lib().turtle_train_dw3x3_fwd(_p(dy), lddy, _p(w9f), None, _p(dx), Cc, B, Cc, H, W, 0, _dt(x), st), "dw_dgrad")
-        z = torch.zeros(10 * Cc if ctx.has_b else 9 * Cc, dtype=torch.float32, device=x.device)  # one fill for both
-        dw9, db = z[:9 * Cc].view(9, Cc), (z[9 * Cc:] if ctx.has_b else None)
+        aw, ab = ctx.acc_w, ctx.acc_b
+        dw9, db = _acc_dst(aw, 9 * Cc), (_acc_dst(ab, Cc) if ctx.has_b else None)
+        nz = (9 * Cc if dw9 is None else 0) + (Cc if ctx.has_b and db is None else 0)
+        if nz:
+            z = torch.zeros(nz, dtype=torch.float32, device=x.device)                    # one fill for both
+            dw9 = z[:9 * Cc] if dw9 is None else dw9
+            db = z[nz - Cc:] if ctx.has_b and db is None else db
         _check(lib().turtle_train_dw3x3_wgrad(_p(x), ctx.ldx, _p(dy), lddy, _p(dw9), _p(db), B, Cc, H, W, _dt(x), st), "dw_wgrad")
-        return dx, dw9.t().reshape(Cc, 1, 3, 3), db
+        tap_major = lambda f: f.view(9, Cc).t().reshape(Cc, 1, 3, 3)     # the kernel's [9][C] -> [C, 1, 3, 3]
+        dw = _acc_done(aw, tap_major) if aw else tap_major(dw9)
+        db = _acc_done(ab, lambda f: f) if ab else db
+        return dx, dw, db
 
 
 class _Gate(torch.autograd.Function):
@@ -276,6 +429,7 @@ class _WinConv(torch.autograd.Function):
                "window_fwd")
         ctx.save_for_backward(x, wt)
         ctx.ldx, ctx.ws, ctx.has_b, ctx.w_dt = ldx, ws, b is not None, w.dtype
+        ctx.acc_w, ctx.acc_b = _acc_use(ctx, 1, w), _acc_use(ctx, 2, b)
         return y
 
     @staticmethod
@@ -292,13 +446,18 @@ class _WinConv(torch.autograd.Function):
             _check(lib().turtle_train_window_dgrad(_p(dy), lddy, _p(wt), _p(dx), Cc, B, Cc, H, W, ws, th, tw, _dt(x), st),
                    "window_dgrad")
         if ctx.needs_input_grad[1]:
-            dwt = torch.zeros(ws * ws, Cc, dtype=torch.float32, device=x.device)
+            aw = ctx.acc_w
+            dwt = _acc_dst(aw, ws * ws * Cc)
+            dwt = torch.zeros(ws * ws * Cc, dtype=torch.float32, device=x.device) if dwt is None else dwt
             _check(lib().turtle_train_window_wgrad(_p(x), ctx.ldx, _p(dy), lddy, _p(dwt), B, Cc, H, W, ws, th, tw, _dt(x), st),
                    "window_wgrad")
-            dw = dwt.t().reshape(Cc, 1, ws, ws).to(ctx.w_dt)
+            tap_major = lambda f: f.view(ws * ws, Cc).t().reshape(Cc, 1, ws, ws).to(ctx.w_dt)
+            dw = _acc_done(aw, tap_major) if aw else tap_major(dwt)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = torch.zeros(Cc, dtype=torch.float32, device=x.device)
+            db = _acc_dst(ctx.acc_b, Cc)
+            db = torch.zeros(Cc, dtype=torch.float32, device=x.device) if db is None else db
             _check(lib().turtle_train_colsum(_p(dy), lddy, _p(db), B * th * tw, Cc, _dt(dy), st), "colsum")
+            db = _acc_done(ctx.acc_b, lambda f: f) if ctx.acc_b else db
         return dx, dw, db, None
 
 
@@ -395,7 +554,7 @@ def _gemm_rows(x2d, w3d, bias=None):
     P, K = x2d.shape
     nimg, N, _ = w3d.shape
     y = torch.empty(P, N, dtype=x2d.dtype, device=x2d.device)
-    _check(lib().turtle_train_gemm(_p(x2d), K, _p(w3d), N * K, P // nimg, _p(bias), _p(y), N, P, K, N, _dt(x2d), _stream(x2d)),
+    _check(lib().turtle_train_gemm(_p(x2d), K, _p(w3d), N * K, P // nimg, _p(bias), None, 0, _p(y), N, P, K, N, _dt(x2d), _stream(x2d)),
            "gemm")
     return y
 
@@ -523,23 +682,30 @@ class _CrossGram(torch.autograd.Function):
         return dq, dk
 
 
-def _rgemm(a, lda, b, ldb, P, N, K, img_px):
+def _rgemm(a, lda, b, ldb, P, N, K, img_px, acc_into=None):
     """c [nimg, N, K] fp32 = sum over each image's pixels (all pixels when img_px = 0) of
-    a[p][n] b[p][k]; a, b are pixel-row tensors (or head slices of one)."""
+    a[p][n] b[p][k]; a, b are pixel-row tensors (or head slices of one). ``acc_into``: a contiguous
+    fp32 tensor of N K elements (img_px = 0) the sum is added to instead (returned)."""
     L = lib()
     nimg = P // img_px if img_px else 1
-    c = torch.empty(nimg, N, K, dtype=torch.float32, device=a.device)
+    if acc_into is not None:
+        if img_px or acc_into.numel() != N * K or acc_into.dtype != torch.float32 or not acc_into.is_contiguous():
+            raise ValueError("rgemm accumulation target must be a contiguous fp32 [N, K] tensor")
+        c = acc_into
+    else:
+        c = torch.empty(nimg, N, K, dtype=torch.float32, device=a.device)
     nws = L.turtle_train_rgemm_workspace(P, N, K, img_px)
     ws = torch.empty(max(int(nws), 16), dtype=torch.uint8, device=a.device)
-    _check(L.turtle_train_rgemm(_p(a), lda, _p(b), ldb, _p(c), P, N, K, img_px, 0, _dt(a), _p(ws), ws.numel(), _stream(a)),
-           "rgemm")
+    _check(L.turtle_train_rgemm(_p(a), lda, _p(b), ldb, _p(c), P, N, K, img_px, int(acc_into is not None), _dt(a), _p(ws),
+                                ws.numel(), _stream(a)), "rgemm")
     return c
 
 
-def _gemm_into(x, ldx, w, img_px, bias, P, K, N, out=None):
-    """y = x w^T (+ bias): x rows [P][ldx] of a [B, K, H, W] tensor; w [N, K] or [nimg, N, K] in x's
-    dtype; returns a channels_last [B, N, H, W] tensor, or writes ``out`` (NHWC rows with their own
-    pixel stride: a channel slice of a wider tensor) and returns it."""
+def _gemm_into(x, ldx, w, img_px, bias, P, K, N, out=None, res=None):
+    """y = x w^T (+ bias) (+ res): x rows [P][ldx] of a [B, K, H, W] tensor; w [N, K] or [nimg, N, K] in
+    x's dtype; res (x's dtype, [B, N, H, W]) added in the epilogue; returns a channels_last
+    [B, N, H, W] tensor, or writes ``out`` (NHWC rows with their own pixel stride: a channel slice of
+    a wider tensor) and returns it."""
     B, _, H, W = x.shape
     if out is None:
         y, ldy = _empty(B, N, H, W, x), N
@@ -548,8 +714,13 @@ def _gemm_into(x, ldx, w, img_px, bias, P, K, N, out=None):
         if y is not out:
             raise ValueError("gemm output slice is not NHWC rows")
     wstride = (N * K) if w.dim() == 3 else 0
-    _check(lib().turtle_train_gemm(_p(x), ldx, _p(w), wstride, img_px if wstride else 0, _p(bias), _p(y), ldy, P, K, N, _dt(x),
-                                   _stream(x)), "gemm")
+    ldr = 0
+    if res is not None:
+        res, ldr = rows(res)
+        if res.dtype != x.dtype or tuple(res.shape) != (B, N, H, W):
+            raise ValueError("gemm residual must match the output's shape and dtype")
+    _check(lib().turtle_train_gemm(_p(x), ldx, _p(w), wstride, img_px if wstride else 0, _p(bias), _p(res), ldr, _p(y), ldy, P,
+                                   K, N, _dt(x), _stream(x)), "gemm")
     return y
 
 
@@ -641,10 +812,12 @@ def _weight_cast(w, gdt):
 
 
 class _Conv1x1(torch.autograd.Function):
-    """y = x W^T + b on NHWC rows; W [N, K] (shared) or [B, N, K] (one set per image)."""
+    """y = x W^T + b (+ res) on NHWC rows; W [N, K] (shared) or [B, N, K] (one set per image). ``res``
+    (the block's residual stream in the output dtype, turtle_t1_arch.py:808-809) is added in the
+    GEMM epilogue; its gradient is dy itself."""
 
     @staticmethod
-    def forward(ctx, x, w, b, sink=None):
+    def forward(ctx, x, w, b, sink=None, res=None):
         gdt = _gemm_dt(x)
         out_dt = x.dtype
         ctx.sink = sink
@@ -653,9 +826,12 @@ class _Conv1x1(torch.autograd.Function):
         N = w.shape[-2]
         wg, ctx.wcache = _weight_cast(w, gdt)
         b32 = None if b is None else b.float().contiguous()
-        y = _gemm_into(xg, ldx, wg, H * W, b32, B * H * W, K, N)
+        if res is not None and (res.dtype != gdt or out_dt != gdt):
+            raise ValueError("conv1x1 residual fusion needs the residual in the GEMM dtype")
+        y = _gemm_into(xg, ldx, wg, H * W, b32, B * H * W, K, N, res=res)
         ctx.save_for_backward(xg, wg)
         ctx.ldx, ctx.has_b, ctx.in_dt, ctx.w_dt = ldx, b is not None, x.dtype, w.dtype
+        ctx.acc_w, ctx.acc_b, ctx.w_shape = (_acc_use(ctx, 1, w) if w.dim() == 2 else None), _acc_use(ctx, 2, b), w.shape
         return y.to(out_dt)
 
     @staticmethod
@@ -664,6 +840,7 @@ class _Conv1x1(torch.autograd.Function):
         B, K, H, W = xg.shape
         N = wg.shape[-2]
         P, HW = B * H * W, H * W
+        dres = dy if len(ctx.needs_input_grad) > 4 and ctx.needs_input_grad[4] else None
         dy, lddy = rows(dy.to(xg.dtype))
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -671,15 +848,20 @@ class _Conv1x1(torch.autograd.Function):
             dst = _sink_out(ctx.sink, K, ctx.in_dt) if xg.dtype == ctx.in_dt else None
             dx = _gemm_into(dy, lddy, wt, HW, None, P, N, K, out=dst).to(ctx.in_dt)
         if ctx.needs_input_grad[1]:
-            if wg.dim() == 3:
-                dw = _rgemm(dy, lddy, xg, ctx.ldx, P, N, K, HW)  # [B, N, K]
+            if ctx.acc_w is not None:                      # in-place accumulation over the step's uses
+                _rgemm(dy, lddy, xg, ctx.ldx, P, N, K, 0, acc_into=_acc_dst(ctx.acc_w, N * K))
+                shape = ctx.w_shape
+                dw = _acc_done(ctx.acc_w, lambda f: f.view(shape))
+            elif wg.dim() == 3:
+                dw = _rgemm(dy, lddy, xg, ctx.ldx, P, N, K, HW).to(ctx.w_dt)  # [B, N, K]
             else:
-                dw = _rgemm(dy, lddy, xg, ctx.ldx, P, N, K, 0)[0]
-            dw = dw.to(ctx.w_dt)
+                dw = _rgemm(dy, lddy, xg, ctx.ldx, P, N, K, 0)[0].to(ctx.w_dt)
         if ctx.has_b and ctx.needs_input_grad[2]:
-            db = torch.zeros(N, dtype=torch.float32, device=dy.device)
+            db = _acc_dst(ctx.acc_b, N)
+            db = torch.zeros(N, dtype=torch.float32, device=dy.device) if db is None else db
             _check(lib().turtle_train_colsum(_p(dy), lddy, _p(db), P, N, _dt(dy), _stream(dy)), "colsum")
-        return dx, dw, db, None
+            db = _acc_done(ctx.acc_b, lambda f: f) if ctx.acc_b else db
+        return dx, dw, db, None, dres
 
 
 class _Gram(torch.autograd.Function):
@@ -792,11 +974,15 @@ class HipOps:
     """The op set of the training graph, on the HIP kernels (channels-last activations)."""
 
     channels_last = True
+    param_grad_accumulator = ParamGradAccumulator      # Trainer: in-place weight-gradient accumulation
+    fused_residual = True                              # layer_norm(residual=True) + conv1x1(res=): train.py _block
 
     @staticmethod
-    def layer_norm(x, w, b, biasfree: bool):
+    def layer_norm(x, w, b, biasfree: bool, residual: bool = False):
+        """LayerNorm(x); ``residual``: (LayerNorm(x), x) with x's second gradient (its residual use)
+        summed inside the LayerNorm backward."""
         out = _act_dtype(x)                          # an fp32 x under autocast: cast inside the kernel
-        return _LayerNorm.apply(x, w, b, biasfree, out)
+        return _LayerNorm.apply(x, w, b, biasfree, out, residual)
 
     @staticmethod
     def dwconv3x3(x, w, b):
@@ -847,10 +1033,18 @@ class HipOps:
     grad_sink = GradSink
 
     @staticmethod
-    def conv1x1(x, w, b, sink=None):
-        """nn.Conv2d(K, N, 1)(x): w [N, K, 1, 1] (or [B, N, K]: one weight set per image). ``sink``
-        (GradSink, channel offset): write the input gradient into that slice of the sink's buffer."""
-        return _Conv1x1.apply(_act(x), w.reshape(w.shape[0], w.shape[1]) if w.dim() == 4 else w, b, sink)
+    def conv1x1(x, w, b, sink=None, res=None):
+        """nn.Conv2d(K, N, 1)(x) (+ res): w [N, K, 1, 1] (or [B, N, K]: one weight set per image).
+        ``sink`` (GradSink, channel offset): write the input gradient into that slice of the sink's
+        buffer. ``res``: the block's residual stream, res + conv(x) (turtle_t1_arch.py:808-809) - in
+        the GEMM's epilogue when it already has the output dtype, else the add as written."""
+        xa = _act(x)
+        w2 = w.reshape(w.shape[0], w.shape[1]) if w.dim() == 4 else w
+        if res is not None and res.dtype == _gemm_dt(xa) == xa.dtype and res.dim() == 4 and \
+                tuple(res.shape) == (xa.shape[0], w2.shape[-2], xa.shape[2], xa.shape[3]):
+            return _Conv1x1.apply(xa, w2, b, sink, res)
+        y = _Conv1x1.apply(xa, w2, b, sink)
+        return y if res is None else res + y
 
     @staticmethod
     def gram(q, k, heads: int):
