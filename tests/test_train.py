@@ -199,6 +199,32 @@ def test_ddp_gloo_two_ranks_match_single_process():
 # GPU: the HIP training kernels
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.gpu
+@pytest.mark.parametrize("N,K,P,img_px,acc", [(64, 64, 5000, 0, 0), (192, 64, 8192, 0, 1), (256, 128, 4096, 0, 0),
+                                              (128, 384, 3000, 0, 1), (1360, 256, 2048, 0, 0), (136, 264, 2048, 512, 0)])
+def test_hip_reduction_gemm_tiles_match_torch(N, K, P, img_px, acc):
+    """turtle_train_rgemm (the 1x1 weight gradient dW = dy^T x, per image when img_px > 0) on each output
+    tile shape (64 / 128 along N and K, padded edges, ragged pixel splits) and in accumulate mode,
+    against an fp32 matmul of the same bf16 operands."""
+    import ctypes as C
+    from turtlevsr_amd import train_ops as T
+    L = T.lib()
+    torch.manual_seed(N + K)
+    a = torch.randn(P, N, device="cuda").to(torch.bfloat16)
+    b = torch.randn(P, K, device="cuda").to(torch.bfloat16)
+    nimg = P // img_px if img_px else 1
+    c0 = torch.randn(nimg, N, K, device="cuda")
+    c = c0.clone()
+    nws = int(L.turtle_train_rgemm_workspace(P, N, K, img_px))
+    ws = torch.empty(max(nws, 16), dtype=torch.uint8, device="cuda")
+    p = lambda t: C.c_void_p(t.data_ptr())
+    st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert L.turtle_train_rgemm(p(a), N, p(b), K, p(c), P, N, K, img_px, acc, 1, p(ws), ws.numel(), st) == 0
+    torch.cuda.synchronize()
+    ref = torch.einsum("ipn,ipk->ink", a.float().view(nimg, -1, N), b.float().view(nimg, -1, K)) + (c0 if acc else 0)
+    torch.testing.assert_close(c, ref, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_hip_fused_residual_block_matches_autograd(dtype):
     """x + conv1x1(LayerNorm(x)) (turtle_t1_arch.py:808-809) with the residual fused: LayerNorm returns

@@ -75,133 +75,219 @@ template <typename T> TURTLE_DEV void st8f(T* p, const float (&v)[8]) {
   }
 }
 
+// tools/train_kbench.py ablations (TURTLE_TRAIN_ABL, read once; 0 in the product path):
+// bit 0 - skip the end-of-block global atomics of the reduction kernels (ln_bwd, colsum, dw_wgrad)
+static int train_abl() {
+  static const int v = [] { const char* e = getenv("TURTLE_TRAIN_ABL"); return e ? atoi(e) : 0; }();
+  return v;
+}
+// launch-size sweeps of tools/train_kbench.py (TURTLE_TRAIN_TUNE="ln_blocks,cs_blocks,dwg_blocks", read once;
+// 0 or absent = the built-in choice)
+static int train_tune(int i) {
+  static const std::vector<int> v = [] {
+    std::vector<int> r(3, 0);
+    if (const char* e = getenv("TURTLE_TRAIN_TUNE")) sscanf(e, "%d,%d,%d", &r[0], &r[1], &r[2]);
+    return r;
+  }();
+  return v[i];
+}
+
+template <typename T>
+struct Raw8 {                                   // 8 consecutive elements, raw
+  uint4 q[sizeof(T) / 2];
+  TURTLE_DEV void load(const void* p) {
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(T) / 2); ++i) q[i] = reinterpret_cast<const uint4*>(p)[i];
+  }
+  TURTLE_DEV void unpack(float (&v)[8]) const { ld8f(reinterpret_cast<const T*>(q), v); }
+};
+
 // lanes per pixel for a C-channel row: a power of two covering C / 8 chunks (<= 64)
 static int ln_group(int C) {
   int g = 1;
   while (g < C / 8 && g < 64) g <<= 1;
   return g;
 }
+// sum over aligned groups of G lanes, every lane of a group gets the same value: DPP within a row
+// (quad swaps, half-row / row mirrors: VALU ops, no LDS round trip), ds_bpermute across rows
+template <int CTRL>
+TURTLE_DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
 template <int G>
 TURTLE_DEV float group_sum(float v) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if constexpr (G >= 2) v += dpp_f<0xB1>(v);       // quad_perm [1, 0, 3, 2]
+  if constexpr (G >= 4) v += dpp_f<0x4E>(v);       // quad_perm [2, 3, 0, 1]
+  if constexpr (G >= 8) v += dpp_f<0x141>(v);      // row_half_mirror: quad q <-> the other quad of the 8
+  if constexpr (G >= 16) v += dpp_f<0x140>(v);     // row_mirror: 8-lane half <-> the other half of the row
+  if constexpr (G >= 32) v += __shfl_xor(v, 16, 64);
+  if constexpr (G >= 64) v += __shfl_xor(v, 32, 64);
   return v;
 }
 
 // ---------------------------------------------------------------------------------------------
 // channel LayerNorm, NHWC: G lanes per pixel, each lane NCH chunks of 8 channels
 // ---------------------------------------------------------------------------------------------
-template <typename T, typename TY, int G, int NCH>
+template <typename T, typename TY, int G, int NCH, int U, bool BF>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ w,
                                                      const float* __restrict__ b, TY* __restrict__ y, int64_t ldy,
-                                                     float* __restrict__ mu, float* __restrict__ rstd, int64_t P, int C,
-                                                     int biasfree) {
-  const int64_t gid = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t p = gid / G;
-  const int l = (int)(gid % G);
-  const bool live = p < P;
-  const int64_t pp = live ? p : 0;
-  float v[NCH][8];
-  float s = 0.f;
+                                                     float* __restrict__ mu, float* __restrict__ rstd, int64_t P, int C) {
+  // U pixels per lane group, strided by the grid's pixel slots (a wave's 64 / G pixels stay adjacent).
+  // Every load is unconditional (clamped row / channel, out-of-range values zeroed by a select after
+  // the unpack) and issued before the first use: a load inside a per-lane branch makes hipcc wait for
+  // it right there, and a load between two stores waits for the stores (vmcnt counts both)
+  const int64_t nslots = (int64_t)gridDim.x * (256 / G);
+  const int64_t slot = (int64_t)blockIdx.x * (256 / G) + threadIdx.x / G;
+  const int l = threadIdx.x % G;
+  const float invC = 1.f / C;
+  float wv[NCH][8], bv[NCH][8];
+  Raw8<T> raw[U][NCH];
 #pragma unroll
   for (int j = 0; j < NCH; ++j) {
-    const int c = 8 * (l + G * j);
-    if (c < C) {
-      ld8f(x + pp * ldx + c, v[j]);
-    } else {
+    const int c = min(8 * (l + G * j), C - 8);
+    ld8f(w + c, wv[j]);
+    ld8f(BF ? w + c : b + c, bv[j]);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[j][e] = 0.f;
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = slot + u * nslots;
+      raw[u][j].load(x + (p < P ? p : 0) * ldx + c);
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) s += v[j][e];
   }
-  const float m = group_sum<G>(s) / C;
-  float q = 0.f;
 #pragma unroll
-  for (int j = 0; j < NCH; ++j)
-    if (8 * (l + G * j) < C)
+  for (int u = 0; u < U; ++u) {
+    const int64_t p = slot + u * nslots;
+    const bool live = p < P;
+    float v[NCH][8];
+    float s = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) { const float d = v[j][e] - m; q = fmaf(d, d, q); }
-  const float r = rsqrtf(group_sum<G>(q) / C + 1e-5f);
-  if (live && l == 0) { mu[p] = m; rstd[p] = r; }
+    for (int j = 0; j < NCH; ++j) {
+      const bool cin = 8 * (l + G * j) < C;
+      raw[u][j].unpack(v[j]);
 #pragma unroll
-  for (int j = 0; j < NCH; ++j) {
-    const int c = 8 * (l + G * j);
-    if (!live || c >= C) continue;
-    float o[8];
+      for (int e = 0; e < 8; ++e) {
+        v[j][e] = cin ? v[j][e] : 0.f;
+        s += v[j][e];
+      }
+    }
+    const float m = group_sum<G>(s) * invC;
+    float q = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = biasfree ? v[j][e] * r * w[c + e] : fmaf((v[j][e] - m) * r, w[c + e], b[c + e]);
-    st8f(y + p * ldy + c, o);
+    for (int j = 0; j < NCH; ++j) {
+      const bool cin = 8 * (l + G * j) < C;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = cin ? v[j][e] - m : 0.f; q = fmaf(d, d, q); }
+    }
+    const float r = rsqrtf(group_sum<G>(q) * invC + 1e-5f);
+    if (live && l == 0) { mu[p] = m; rstd[p] = r; }
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c = 8 * (l + G * j);
+      if (!live || c >= C) continue;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = BF ? v[j][e] * r * wv[j][e] : fmaf((v[j][e] - m) * r, wv[j][e], bv[j][e]);
+      st8f(y + p * ldy + c, o);
+    }
   }
 }
 
 // backward: g = w dy;  WithBias: xh = (x - mu) r, dx = r (g - mean(g) - xh mean(g xh));
 // BiasFree (y = w x r, r of the centred variance): dx = r g - (x - mu) r^3 mean(g x).
 // dw[c] = sum_p dy xhat (BiasFree xhat = x r), db[c] = sum_p dy: per-lane accumulators over the
-// block's pixels -> LDS -> one atomic per channel per block
-template <typename T, typename TY, int G, int NCH>
+// block's pixels -> LDS -> one atomic per channel per block. dres (or NULL): the residual use's
+// gradient, added into dx.
+template <typename T, typename TY, int G, int NCH, int U, bool BF>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ x, int64_t ldx, const float* __restrict__ w,
                                                      const float* __restrict__ mu, const float* __restrict__ rstd,
                                                      const TY* __restrict__ dy, int64_t lddy, T* __restrict__ dx, int64_t lddx,
                                                      const T* __restrict__ dres, int64_t lddres,
                                                      float* __restrict__ dw, float* __restrict__ db, int64_t P, int C,
-                                                     int biasfree, int ppb) {
+                                                     int ppb, int noatom) {
   extern __shared__ float sred[];                  // [2][C]
   for (int c = threadIdx.x; c < 2 * C; c += 256) sred[c] = 0.f;
   __syncthreads();
   const int l = threadIdx.x % G, slot = threadIdx.x / G, nslot = 256 / G;
-  float aw[NCH][8], ab[NCH][8];
+  const float invC = 1.f / C;
+  float wv[NCH][8], aw[NCH][8], ab[NCH][8];
 #pragma unroll
-  for (int j = 0; j < NCH; ++j)
+  for (int j = 0; j < NCH; ++j) {
+    const int c = 8 * (l + G * j);
+    ld8f(w + min(c, C - 8), wv[j]);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) aw[j][e] = ab[j][e] = 0.f;
+    for (int e = 0; e < 8; ++e) {
+      wv[j][e] = c < C ? wv[j][e] : 0.f;           // lanes past C: gamma 0 -> no contribution
+      aw[j][e] = ab[j][e] = 0.f;
+    }
+  }
   const int64_t p0 = (int64_t)blockIdx.x * ppb;
   const int64_t p1 = min(P, p0 + ppb);
-  for (int64_t pb = p0; pb < p1; pb += nslot) {     // uniform trip count across the block
-    const int64_t p = pb + slot;
-    const bool live = p < p1;
-    const int64_t pp = live ? p : p0;
-    const float m = mu[pp], r = rstd[pp];
-    float xv[NCH][8], gy[NCH][8];
-    float sg = 0.f, sgx = 0.f;
+  // U pixels per lane group per trip (block pixel slots, then U of those strides): every row load of
+  // the trip is unconditional (clamped) and in flight before the first reduction
+  for (int64_t pb = p0; pb < p1; pb += nslot * U) {     // uniform trip count across the block
+    Raw8<T> rx[U][NCH], rr[U][NCH];
+    Raw8<TY> rg[U][NCH];
+    float m[U], r[U];
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
-      const int c = 8 * (l + G * j);
-      if (c < C) {
-        ld8f(x + pp * ldx + c, xv[j]);
-        ld8f(dy + pp * lddy + c, gy[j]);
-      } else {
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = pb + slot + u * nslot;
+      const int64_t pp = p < p1 ? p : p0;
+      m[u] = mu[pp];
+      r[u] = rstd[pp];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) xv[j][e] = gy[j][e] = 0.f;
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float g = (c < C ? w[c + e] : 0.f) * gy[j][e];
-        sg += g;
-        sgx = fmaf(g, biasfree ? xv[j][e] : (xv[j][e] - m) * r, sgx);
+      for (int j = 0; j < NCH; ++j) {
+        const int c = min(8 * (l + G * j), C - 8);
+        rx[u][j].load(x + pp * ldx + c);
+        rg[u][j].load(dy + pp * lddy + c);
       }
     }
-    const float mg = group_sum<G>(sg) / C, mgx = group_sum<G>(sgx) / C;
+    if (dres) {                                    // uniform: the residual gradient rows
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
-      const int c = 8 * (l + G * j);
-      if (c >= C) continue;
-      float o[8], rg[8];
-      if (dres) ld8f(dres + pp * lddres + c, rg);     // the residual branch's gradient, summed in here
-      else {
+      for (int u = 0; u < U; ++u) {
+        const int64_t p = pb + slot + u * nslot;
+        const int64_t pp = p < p1 ? p : p0;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) rg[e] = 0.f;
+        for (int j = 0; j < NCH; ++j) rr[u][j].load(dres + pp * lddres + min(8 * (l + G * j), C - 8));
       }
+    }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float g = w[c + e] * gy[j][e];
-        o[e] = rg[e] + (biasfree ? r * g - (xv[j][e] - m) * r * r * r * mgx : r * (g - mg - (xv[j][e] - m) * r * mgx));
-        if (live) {
-          aw[j][e] = fmaf(gy[j][e], biasfree ? xv[j][e] * r : (xv[j][e] - m) * r, aw[j][e]);
-          ab[j][e] += gy[j][e];
+    for (int u = 0; u < U; ++u) {
+      const int64_t p = pb + slot + u * nslot;
+      const bool live = p < p1;
+      const float mm = m[u], rs = r[u];
+      float xv[NCH][8], gy[NCH][8];
+      float sg = 0.f, sgx = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        rx[u][j].unpack(xv[j]);
+        rg[u][j].unpack(gy[j]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float g = wv[j][e] * gy[j][e];
+          sg += g;
+          sgx = fmaf(g, BF ? xv[j][e] : (xv[j][e] - mm) * rs, sgx);
         }
       }
-      if (live) st8f(dx + p * lddx + c, o);
+      const float mg = group_sum<G>(sg) * invC, mgx = group_sum<G>(sgx) * invC;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        const int c = 8 * (l + G * j);
+        float o[8], res[8];
+        if (dres) rr[u][j].unpack(res);
+        else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) res[e] = 0.f;
+        }
+        const bool ok = live && c < C;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float g = wv[j][e] * gy[j][e];
+          const float xe = xv[j][e];
+          o[e] = res[e] + (BF ? rs * g - (xe - mm) * rs * rs * rs * mgx : rs * (g - mg - (xe - mm) * rs * mgx));
+          aw[j][e] = fmaf(ok ? gy[j][e] : 0.f, BF ? xe * rs : (xe - mm) * rs, aw[j][e]);
+          ab[j][e] += ok ? gy[j][e] : 0.f;
+        }
+        if (ok) st8f(dx + p * lddx + c, o);
+      }
     }
   }
 #pragma unroll
@@ -215,6 +301,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ x, in
     }
   }
   __syncthreads();
+  if (noatom) return;
   for (int c = threadIdx.x; c < C; c += 256) {
     atomicAdd(&dw[c], sred[c]);
     if (db) atomicAdd(&db[c], sred[C + c]);
@@ -317,20 +404,12 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ x, 
 // column as a rolling window of three rows (raw, one new row loaded ahead of the math) and
 // accumulates dw9[t] += dy * x[p + off_t], db += dy. Column sums by cross-lane shuffles, the 4
 // waves meet in LDS, one global atomic per (tap, channel) per block.
-template <typename T>
-struct Raw8 {                                   // 8 consecutive elements, raw
-  uint4 q[sizeof(T) / 2];
-  TURTLE_DEV void load(const void* p) {
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(T) / 2); ++i) q[i] = reinterpret_cast<const uint4*>(p)[i];
-  }
-  TURTLE_DEV void unpack(float (&v)[8]) const { ld8f(reinterpret_cast<const T*>(q), v); }
-};
 constexpr int TW_SX = 32, TW_CV = 8;
 template <typename T>
 __global__ __launch_bounds__(256) void dw_wgrad_rows_kernel(const T* __restrict__ x, int64_t ldx, const T* __restrict__ dy,
                                                             int64_t lddy, float* __restrict__ dw9, float* __restrict__ db,
-                                                            int C, int H, int W, int RB, int nstrip, int nchunk, int nband) {
+                                                            int C, int H, int W, int RB, int nstrip, int nchunk, int nband,
+                                                            int noatom) {
   __shared__ float sred[10][TW_CV * 8];
   const int tid = threadIdx.x, lane = tid & 63;
   for (int i = tid; i < 10 * TW_CV * 8; i += 256) (&sred[0][0])[i] = 0.f;
@@ -362,13 +441,19 @@ __global__ __launch_bounds__(256) void dw_wgrad_rows_kernel(const T* __restrict_
   for (int k = 0; k < 10; ++k)
 #pragma unroll
     for (int e = 0; e < 8; ++e) a[k][e] = 0.f;
-  Raw8<T> w0[3], w1[3], w2[3], nx[3], gr;
+  // dy row y + 1 and x row y + 2 are loaded while row y is consumed; every load unconditional (rows
+  // past the band / image read the zero line): a conditional load makes hipcc wait for it in place
+  auto dy_row = [&](int y) {
+    return live && y < y1 ? reinterpret_cast<const void*>(gin + ((int64_t)y * W + xc) * lddy) : g_zero_tw;
+  };
+  Raw8<T> w0[3], w1[3], w2[3], nx[3], gr, gn;
   load_row(y0 - 1, w0);
   load_row(y0, w1);
   load_row(y0 + 1, w2);
+  gr.load(dy_row(y0));
   for (int y = y0; y < y1; ++y) {
-    if (y + 1 < y1) load_row(y + 2, nx);
-    gr.load(live ? reinterpret_cast<const void*>(gin + ((int64_t)y * W + xc) * lddy) : g_zero_tw);
+    load_row(y + 2, nx);
+    gn.load(dy_row(y + 1));
     float g[8];
     gr.unpack(g);
 #pragma unroll
@@ -383,6 +468,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_rows_kernel(const T* __restrict_
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) { w0[k] = w1[k]; w1[k] = w2[k]; w2[k] = nx[k]; }
+    gr = gn;
   }
   // sum over the 8 columns of a wave (lane bits 3..5), then over the 4 waves in LDS
 #pragma unroll
@@ -403,6 +489,7 @@ __global__ __launch_bounds__(256) void dw_wgrad_rows_kernel(const T* __restrict_
       for (int e = 0; e < 8; ++e) atomicAdd(&sred[k][lane * 8 + e], a[k][e]);
   }
   __syncthreads();
+  if (noatom) return;
   for (int i = tid; i < 10 * TW_CV * 8; i += 256) {
     const int k = i / (TW_CV * 8), j = i - k * TW_CV * 8, c = chunk * TW_CV * 8 + j;
     if (c >= C) continue;
@@ -750,44 +837,52 @@ __global__ __launch_bounds__(256) void sab_softmax_bwd_kernel(const TG* __restri
   }
 }
 
-// column sums db[n] = sum_p dy[p][n] (8 channels per thread, pixel lanes, LDS reduction, atomics)
-template <typename T>
-// square: sums of squares; dy2 != NULL: column dot products sum_p dy[p][n] dy2[p][n]
-__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, int64_t ld, float* __restrict__ db, int64_t P,
-                                                     int N, int64_t ppb, int square, const T* __restrict__ dy2 = nullptr,
-                                                     int64_t ld2 = 0) {
+// column sums db[n] = sum_p dy[p][n] (8 channels per thread, pixel lanes, LDS reduction, atomics);
+// MODE 1: sums of squares; MODE 2: column dot products sum_p dy[p][n] dy2[p][n]
+template <typename T, int MODE, int NT = 256>
+__global__ __launch_bounds__(NT) void colsum_kernel(const T* __restrict__ dy, int64_t ld, float* __restrict__ db, int64_t P,
+                                                    int N, int64_t ppb, const T* __restrict__ dy2, int64_t ld2, int noatom) {
   extern __shared__ float sred[];
   dy += (int64_t)blockIdx.y * P * ld;              // image blockIdx.y of P pixels (one image: y = 0)
-  if (dy2) dy2 += (int64_t)blockIdx.y * P * ld2;
+  if (MODE == 2) dy2 += (int64_t)blockIdx.y * P * ld2;
   db += (int64_t)blockIdx.y * N;
-  for (int i = threadIdx.x; i < N; i += 256) sred[i] = 0.f;
+  for (int i = threadIdx.x; i < N; i += NT) sred[i] = 0.f;
   __syncthreads();
-  const int nch = N / 8, lanes = 256 / nch;
-  const int ch = threadIdx.x % nch, pl = threadIdx.x / nch;
+  const int nch = N / 8, lanes = NT / nch;
+  const int ch = min((int)threadIdx.x % nch, nch - 1), pl = threadIdx.x / nch;
+  const bool lane_live = pl < lanes;
   float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const int64_t p0 = (int64_t)blockIdx.x * ppb, p1 = min(P, p0 + ppb);
-  if (pl < lanes) {
-    for (int64_t p = p0 + pl; p < p1; p += lanes) {
-      float v[8];
-      ld8f(dy + p * ld + 8 * ch, v);
-      if (dy2) {
-        float v2[8];
-        ld8f(dy2 + p * ld2 + 8 * ch, v2);
+  // 4 pixel rows per trip, all loads unconditional (clamped rows, zeroed by a select after the unpack)
+  // and issued before the first add
+  for (int64_t pq = p0 + min(pl, lanes - 1); pq < p1; pq += 4 * lanes) {
+    Raw8<T> r1[4], r2[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) a[e] = fmaf(v[e], v2[e], a[e]);
-      } else if (square) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) a[e] = fmaf(v[e], v[e], a[e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) a[e] += v[e];
-      }
+    for (int u = 0; u < 4; ++u) {
+      const int64_t p = pq + u * lanes;
+      const int64_t pp = p < p1 ? p : p0;
+      r1[u].load(dy + pp * ld + 8 * ch);
+      if constexpr (MODE == 2) r2[u].load(dy2 + pp * ld2 + 8 * ch);
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) atomicAdd(&sred[8 * ch + e], a[e]);
+    for (int u = 0; u < 4; ++u) {
+      const bool live = lane_live && pq + u * lanes < p1;
+      float v[8], v2[8];
+      r1[u].unpack(v);
+      if constexpr (MODE == 2) r2[u].unpack(v2);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float t = MODE == 2 ? v[e] * v2[e] : MODE == 1 ? v[e] * v[e] : v[e];
+        a[e] += live ? t : 0.f;
+      }
+    }
   }
+  if (lane_live)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(&sred[8 * ch + e], a[e]);
   __syncthreads();
-  for (int i = threadIdx.x; i < N; i += 256) atomicAdd(&db[i], sred[i]);
+  if (noatom) return;
+  for (int i = threadIdx.x; i < N; i += NT) atomicAdd(&db[i], sred[i]);
 }
 
 
@@ -840,21 +935,30 @@ TURTLE_DEV uint2 ds_read_tr16(const char* lds_ptr) {
   return r;
 }
 
+// Output tile TN x TK per block (64 or 128 each; 128 x 128 on the wide weights, where the 64 x 64 tile
+// left the matrix cores at ~200 TF/s: 4x fewer transposed LDS reads per MFMA), four waves of
+// (TN / 2) x (TK / 2), RG_BP pixel rows per stage.
 // shW > 0 (3x3 convolution weight gradient, img_px = 0): blockIdx.y = tap t of a 3x3 stencil
 // (dy, dx) = (t / 3 - 1, t % 3 - 1), B's pixel p read at (y + dy, x + dx) of its shH x shW image (zero
 // outside): part[split][t] = sum_p A[p] B[p + shift(t)]^T
+template <int TN, int TK>
 __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict__ A, int64_t lda, const bf16* __restrict__ B,
                                                          int64_t ldb, float* __restrict__ part, int64_t img_px, int nimg_out,
                                                          int N, int K, int64_t P, int64_t ppb, int shH = 0, int shW = 0) {
   typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+  // row pitches: 32 B past the row (40 / 72 dwords): the 8 consecutive rows a 32-lane half of a
+  // transposed read covers land on 8 distinct 8-bank sets
+  constexpr int PA = 2 * TN + 32, PB = 2 * TK + 32;
+  constexpr int CA = TN / 32, CB = TK / 32;        // 16-B chunks per staging thread (4 threads per pixel row)
+  constexpr int FI = TN / 32, FJ = TK / 32;        // 16 x 16 fragments per wave along N / K
   // two stage buffers: the global loads of stage s + 1 are in flight (in registers) while the
   // MFMAs of stage s read the other buffer; one barrier per stage
-  __shared__ __attribute__((aligned(16))) char sA[2][RG_BP * RG_PITCH];
-  __shared__ __attribute__((aligned(16))) char sB[2][RG_BP * RG_PITCH];
+  __shared__ __attribute__((aligned(16))) char sA[2][RG_BP * PA];
+  __shared__ __attribute__((aligned(16))) char sB[2][RG_BP * PB];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int ntn = (N + RG_BN - 1) / RG_BN, ntk = (K + RG_BK - 1) / RG_BK;
+  const int ntn = (N + TN - 1) / TN, ntk = (K + TK - 1) / TK;
   const int tile = blockIdx.x % (ntn * ntk);
-  const int n0 = (tile / ntk) * RG_BN, k0 = (tile % ntk) * RG_BK;
+  const int n0 = (tile / ntk) * TN, k0 = (tile % ntk) * TK;
   const int split = blockIdx.x / (ntn * ntk);
   const int img = blockIdx.y;
   const int64_t pbase = img_px > 0 ? (int64_t)img * img_px : 0;
@@ -862,24 +966,23 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
   const int64_t p0 = (int64_t)split * ppb, p1 = min(plen, p0 + ppb);
   const int wn = wid >> 1, wk = wid & 1;
   const int sdy = img / 3 - 1, sdx = img % 3 - 1;   // (tap mode only)
-  f32x4 acc[2][2];
+  f32x4 acc[FI][FJ];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // staging: thread -> pixel row tid >> 2, 16-B chunks 2 (tid & 3) and + 1 of each operand.
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // staging: thread -> pixel row tid >> 2, 16-B chunks CA (tid & 3) .. + CA - 1 of A (CB of B).
   // Loads are unconditional: a column chunk past N / K is clamped to the last one (it only feeds
   // output rows / columns that are not stored), a pixel row past the split's end is clamped to its
   // last row and zeroed by a mask when it is written to LDS (both operands: no inf * 0).
-  const int srow = tid >> 2, sch = 2 * (tid & 3);
-  const bf16* pa[2];
-  const bf16* pb_[2];
+  const int srow = tid >> 2, sca = CA * (tid & 3), scb = CB * (tid & 3);
+  const bf16* pa[CA];
+  const bf16* pb_[CB];
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    pa[u] = A + pbase * lda + min(n0 + 8 * (sch + u), N - 8);
-    pb_[u] = B + pbase * ldb + min(k0 + 8 * (sch + u), K - 8);
-  }
-  uint4 ra[2], rb[2];
+  for (int u = 0; u < CA; ++u) pa[u] = A + pbase * lda + min(n0 + 8 * (sca + u), N - 8);
+#pragma unroll
+  for (int u = 0; u < CB; ++u) pb_[u] = B + pbase * ldb + min(k0 + 8 * (scb + u), K - 8);
+  uint4 ra[CA], rb[CB];
   uint32_t live_mask = 0, b_mask = 0;
   auto gload = [&](int64_t pbk) {
     const int64_t p = pbk + srow;
@@ -894,18 +997,20 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
       b_mask = ok ? live_mask : 0u;
     }
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      ra[u] = *reinterpret_cast<const uint4*>(pa[u] + pc * lda);
-      rb[u] = *reinterpret_cast<const uint4*>(pb_[u] + pcb * ldb);
-    }
+    for (int u = 0; u < CA; ++u) ra[u] = *reinterpret_cast<const uint4*>(pa[u] + pc * lda);
+#pragma unroll
+    for (int u = 0; u < CB; ++u) rb[u] = *reinterpret_cast<const uint4*>(pb_[u] + pcb * ldb);
   };
   auto lstore = [&](int buf) {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < CA; ++u) {
       const uint4 va = make_uint4(ra[u].x & live_mask, ra[u].y & live_mask, ra[u].z & live_mask, ra[u].w & live_mask);
+      *reinterpret_cast<uint4*>(sA[buf] + srow * PA + 16 * (sca + u)) = va;
+    }
+#pragma unroll
+    for (int u = 0; u < CB; ++u) {
       const uint4 vb = make_uint4(rb[u].x & b_mask, rb[u].y & b_mask, rb[u].z & b_mask, rb[u].w & b_mask);
-      *reinterpret_cast<uint4*>(sA[buf] + srow * RG_PITCH + 16 * (sch + u)) = va;
-      *reinterpret_cast<uint4*>(sB[buf] + srow * RG_PITCH + 16 * (sch + u)) = vb;
+      *reinterpret_cast<uint4*>(sB[buf] + srow * PB + 16 * (scb + u)) = vb;
     }
   };
   // transposed reads: lane group g = lane >> 4, row q = (lane >> 2) & 3, column quad pq = lane & 3
@@ -922,46 +1027,51 @@ __global__ __launch_bounds__(256) void rgemm_bf16_kernel(const bf16* __restrict_
     const char* cA = sA[buf];
     const char* cB = sB[buf];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {               // 32 pixels per MFMA K step
-      uint2 ra0[2], ra1[2], rb0[2], rb1[2];
+    for (int ks = 0; ks < RG_BP / 32; ++ks) {      // 32 pixels per MFMA K step
+      uint2 ra0[FI], ra1[FI], rb0[FJ], rb1[FJ];
+      const int r0 = 32 * ks + 4 * g + q;
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int cn = 32 * wn + 16 * t + 4 * pq, ck = 32 * wk + 16 * t + 4 * pq;
-        const int r0 = 32 * ks + 4 * g + q;
-        ra0[t] = ds_read_tr16(cA + r0 * RG_PITCH + 2 * cn);
-        ra1[t] = ds_read_tr16(cA + (r0 + 16) * RG_PITCH + 2 * cn);
-        rb0[t] = ds_read_tr16(cB + r0 * RG_PITCH + 2 * ck);
-        rb1[t] = ds_read_tr16(cB + (r0 + 16) * RG_PITCH + 2 * ck);
-      }
-      // the wait names the read results as operands: the compiler does not see the asm reads as
-      // LDS loads, so without the dependence it may schedule an MFMA before the wait
-      asm volatile("s_waitcnt lgkmcnt(0)"
-                   : "+v"(ra0[0]), "+v"(ra0[1]), "+v"(ra1[0]), "+v"(ra1[1]), "+v"(rb0[0]), "+v"(rb0[1]), "+v"(rb1[0]),
-                     "+v"(rb1[1])::"memory");
-      bf16x8v af[2], bfr[2];
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        af[t] = __builtin_bit_cast(bf16x8v, make_uint4(ra0[t].x, ra0[t].y, ra1[t].x, ra1[t].y));
-        bfr[t] = __builtin_bit_cast(bf16x8v, make_uint4(rb0[t].x, rb0[t].y, rb1[t].x, rb1[t].y));
+      for (int t = 0; t < FI; ++t) {
+        const int cn = (TN / 2) * wn + 16 * t + 4 * pq;
+        ra0[t] = ds_read_tr16(cA + r0 * PA + 2 * cn);
+        ra1[t] = ds_read_tr16(cA + (r0 + 16) * PA + 2 * cn);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int t = 0; t < FJ; ++t) {
+        const int ck = (TK / 2) * wk + 16 * t + 4 * pq;
+        rb0[t] = ds_read_tr16(cB + r0 * PB + 2 * ck);
+        rb1[t] = ds_read_tr16(cB + (r0 + 16) * PB + 2 * ck);
+      }
+      // the compiler does not see the asm reads as LDS loads: the wait is an ordered volatile asm and
+      // every read result passes through an (ordered) empty asm after it before an MFMA may use it
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int t = 0; t < FI; ++t) asm volatile("" : "+v"(ra0[t]), "+v"(ra1[t]));
+#pragma unroll
+      for (int t = 0; t < FJ; ++t) asm volatile("" : "+v"(rb0[t]), "+v"(rb1[t]));
+      bf16x8v af[FI], bfr[FJ];
+#pragma unroll
+      for (int t = 0; t < FI; ++t) af[t] = __builtin_bit_cast(bf16x8v, make_uint4(ra0[t].x, ra0[t].y, ra1[t].x, ra1[t].y));
+#pragma unroll
+      for (int t = 0; t < FJ; ++t) bfr[t] = __builtin_bit_cast(bf16x8v, make_uint4(rb0[t].x, rb0[t].y, rb1[t].x, rb1[t].y));
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (more) lstore(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
-  // lane holds C[n0 + 32 wn + 16 i + 4 g + e][k0 + 32 wk + 16 j + (lane & 15)]
+  // lane holds C[n0 + (TN / 2) wn + 16 i + 4 g + e][k0 + (TK / 2) wk + 16 j + (lane & 15)]
   float* out = part + ((int64_t)split * nimg_out + img) * N * K;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FJ; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int n = n0 + 32 * wn + 16 * i + 4 * g + e, k = k0 + 32 * wk + 16 * j + (lane & 15);
+        const int n = n0 + (TN / 2) * wn + 16 * i + 4 * g + e, k = k0 + (TK / 2) * wk + 16 * j + (lane & 15);
         if (n < N && k < K) out[(int64_t)n * K + k] = acc[i][j][e];
       }
 }
@@ -1051,11 +1161,17 @@ template <typename T, typename TY = T>
 int ln_fwd(const void* x, int64_t ldx, const float* w, const float* b, void* y, int64_t ldy, float* mu, float* rstd, int64_t P,
            int C, int biasfree, hipStream_t st) {
   const int G = ln_group(C), nch = (C / 8 + G - 1) / G;
-  const int64_t blocks = (P * G + 255) / 256;
+  // U = 4 / NCH pixels per lane group (4 row loads in flight per lane)
 #define LNF(GG, NN)                                                                                                  \
   if (G == GG && nch <= NN) {                                                                                        \
-    hipLaunchKernelGGL((ln_fwd_kernel<T, TY, GG, NN>), dim3((unsigned)blocks), dim3(256), 0, st, (const T*)x, ldx, w, b, \
-                       (TY*)y, ldy, mu, rstd, P, C, biasfree);                                                        \
+    constexpr int U = NN >= 4 ? 1 : 4 / NN;                                                                          \
+    const int64_t blocks = std::max<int64_t>(1, (P * G + 256 * U - 1) / (256 * U));                                  \
+    if (biasfree)                                                                                                    \
+      hipLaunchKernelGGL((ln_fwd_kernel<T, TY, GG, NN, U, true>), dim3((unsigned)blocks), dim3(256), 0, st, (const T*)x, \
+                         ldx, w, b, (TY*)y, ldy, mu, rstd, P, C);                                                     \
+    else                                                                                                             \
+      hipLaunchKernelGGL((ln_fwd_kernel<T, TY, GG, NN, U, false>), dim3((unsigned)blocks), dim3(256), 0, st, (const T*)x, \
+                         ldx, w, b, (TY*)y, ldy, mu, rstd, P, C);                                                     \
     return 0;                                                                                                        \
   }
   LNF(1, 1) LNF(2, 1) LNF(4, 1) LNF(8, 1) LNF(16, 1) LNF(32, 1) LNF(64, 1) LNF(64, 2) LNF(64, 4)
@@ -1066,17 +1182,25 @@ template <typename T, typename TY = T>
 int ln_bwd(const void* x, int64_t ldx, const float* w, const float* mu, const float* rstd, const void* dy, int64_t lddy, void* dx,
            int64_t lddx, const void* dres, int64_t lddres, float* dw, float* db, int64_t P, int C, int biasfree, hipStream_t st) {
   const int G = ln_group(C), nch = (C / 8 + G - 1) / G;
-  // ~512 blocks whatever P is (a fixed 256 pixels per block left a 32 x 32 x 8 latent map on 32
-  // blocks); pixels per block a multiple of the block's pixel slots
+  // ~256 blocks whatever P is (a fixed 256 pixels per block left a 32 x 32 x 8 latent map on 32
+  // blocks; 512 - 1024 blocks measured slower: more end-of-block atomics, tools/train_kbench.py);
+  // pixels per block a multiple of the block's pixel slots x U
   const int64_t nslot = 256 / G;
-  int64_t ppb = std::max<int64_t>(nslot, (P + 511) / 512);
-  ppb = (ppb + nslot - 1) / nslot * nslot;
-  const int64_t blocks = (P + ppb - 1) / ppb;
 #define LNB(GG, NN)                                                                                                       \
   if (G == GG && nch <= NN) {                                                                                             \
-    hipLaunchKernelGGL((ln_bwd_kernel<T, TY, GG, NN>), dim3((unsigned)blocks), dim3(256), 2 * C * sizeof(float), st, (const T*)x, \
-                       ldx, w, mu, rstd, (const TY*)dy, lddy, (T*)dx, lddx, (const T*)dres, lddres, dw, db, P, C, biasfree,  \
-                       (int)ppb);                                                                                         \
+    constexpr int U = NN >= 4 ? 1 : 4 / NN;                                                                               \
+    const int64_t nbt = train_tune(0) > 0 ? train_tune(0) : 256;                                                           \
+    int64_t ppb = std::max<int64_t>(nslot * U, (P + nbt - 1) / nbt);                                                      \
+    ppb = (ppb + nslot * U - 1) / (nslot * U) * (nslot * U);                                                              \
+    const int64_t blocks = (P + ppb - 1) / ppb;                                                                           \
+    if (biasfree)                                                                                                         \
+      hipLaunchKernelGGL((ln_bwd_kernel<T, TY, GG, NN, U, true>), dim3((unsigned)blocks), dim3(256), 2 * C * sizeof(float), st, \
+                         (const T*)x, ldx, w, mu, rstd, (const TY*)dy, lddy, (T*)dx, lddx, (const T*)dres, lddres, dw, db, P, C, \
+                         (int)ppb, train_abl() & 1);                                                                     \
+    else                                                                                                                  \
+      hipLaunchKernelGGL((ln_bwd_kernel<T, TY, GG, NN, U, false>), dim3((unsigned)blocks), dim3(256), 2 * C * sizeof(float), st, \
+                         (const T*)x, ldx, w, mu, rstd, (const TY*)dy, lddy, (T*)dx, lddx, (const T*)dres, lddres, dw, db, P, C, \
+                         (int)ppb, train_abl() & 1);                                                                     \
     return 0;                                                                                                             \
   }
   LNB(1, 1) LNB(2, 1) LNB(4, 1) LNB(8, 1) LNB(16, 1) LNB(32, 1) LNB(64, 1) LNB(64, 2) LNB(64, 4)
@@ -1109,10 +1233,13 @@ int dw_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* dw
     const int nstrip = (W + TW_SX - 1) / TW_SX, nchunk = (C / 8 + TW_CV - 1) / TW_CV;
     int RB = 32;
     auto nblk = [&](int rb) { return N * nchunk * nstrip * ((H + rb - 1) / rb); };
-    while (RB > 4 && nblk(RB) < 2048) RB /= 2;
+    // ~512 blocks: longer row bands amortise the block's column / tap reduction (2048 blocks of 8-row
+    // bands: 80 us at level 1 against 42 us, tools/train_kbench.py)
+    const int64_t target = train_tune(2) > 0 ? train_tune(2) : 512;
+    while (RB > 4 && nblk(RB) < target) RB /= 2;
     const int nband = (H + RB - 1) / RB;
     hipLaunchKernelGGL(dw_wgrad_rows_kernel<T>, dim3((unsigned)nblk(RB)), dim3(256), 0, st, (const T*)x, ldx, (const T*)dy, lddy,
-                       dw9, db, C, H, W, RB, nstrip, nchunk, nband);
+                       dw9, db, C, H, W, RB, nstrip, nchunk, nband, train_abl() & 1);
     return 0;
   }
   const int64_t P = N * H * W;
@@ -1181,9 +1308,13 @@ int win_wgrad(const void* x, int64_t ldx, const void* dy, int64_t lddy, float* d
 }
 template <typename T>
 int colsum(const void* dy, int64_t ld, float* db, int64_t P, int N, hipStream_t st) {
-  const int64_t blocks = std::min<int64_t>(1024, std::max<int64_t>(1, P / 256));
+  // 1024-thread blocks, at most 256 of them: the end-of-block global atomics (N per block) cost more
+  // than the column reads once there are ~1000 blocks (L1: 38 vs 21 us without them)
+  const int cap = train_tune(1) > 0 ? train_tune(1) : 256;
+  const int64_t blocks = std::min<int64_t>(cap, std::max<int64_t>(1, P * (N / 8) / 4096));   // >= 4 rows per thread
   const int64_t ppb = (P + blocks - 1) / blocks;
-  hipLaunchKernelGGL(colsum_kernel<T>, dim3((unsigned)blocks), dim3(256), N * sizeof(float), st, (const T*)dy, ld, db, P, N, ppb, 0);
+  hipLaunchKernelGGL((colsum_kernel<T, 0, 1024>), dim3((unsigned)blocks), dim3(1024), N * sizeof(float), st, (const T*)dy, ld, db, P,
+                     N, ppb, nullptr, 0, train_abl() & 1);
   return 0;
 }
 // per-image column sums of squares: out[img][n] += sum over the image's img_px pixels of x^2
@@ -1192,8 +1323,8 @@ int colsumsq(const void* x, int64_t ld, float* out, int64_t P, int N, int64_t im
   const int64_t nimg = P / img_px;
   const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 512 / nimg), std::max<int64_t>(1, img_px / 256));
   const int64_t ppb = (img_px + blocks - 1) / blocks;
-  hipLaunchKernelGGL(colsum_kernel<T>, dim3((unsigned)blocks, (unsigned)nimg), dim3(256), N * sizeof(float), st, (const T*)x, ld, out,
-                     img_px, N, ppb, 1);
+  hipLaunchKernelGGL((colsum_kernel<T, 1>), dim3((unsigned)blocks, (unsigned)nimg), dim3(256), N * sizeof(float), st, (const T*)x, ld,
+                     out, img_px, N, ppb, nullptr, 0, 0);
   return 0;
 }
 
@@ -1203,8 +1334,8 @@ int coldot(const void* a, int64_t lda, const void* b, int64_t ldb, float* out, i
   const int64_t nimg = P / img_px;
   const int64_t blocks = std::min<int64_t>(std::max<int64_t>(1, 512 / nimg), std::max<int64_t>(1, img_px / 256));
   const int64_t ppb = (img_px + blocks - 1) / blocks;
-  hipLaunchKernelGGL(colsum_kernel<T>, dim3((unsigned)blocks, (unsigned)nimg), dim3(256), N * sizeof(float), st, (const T*)a, lda, out,
-                     img_px, N, ppb, 0, (const T*)b, ldb);
+  hipLaunchKernelGGL((colsum_kernel<T, 2>), dim3((unsigned)blocks, (unsigned)nimg), dim3(256), N * sizeof(float), st, (const T*)a, lda,
+                     out, img_px, N, ppb, (const T*)b, ldb, 0);
   return 0;
 }
 template <typename T>
@@ -1277,11 +1408,25 @@ static const float* train_consts(int which) {
   return which ? it->second + TURTLE_CONST_VEC : it->second;
 }
 
-static int64_t rgemm_splits(int64_t P, int N, int K, int64_t img_px, int ntap = 1) {
+// the bf16 reduction GEMM's output tile: 128 along N (K) when N (K) is a multiple of 128 or >= 256 (little
+// padding), else 64; fp32 runs 64 x 64
+static int rgemm_tn(int N, int dtype) { return dtype == 1 && (N % 128 == 0 || N >= 256) ? 128 : 64; }
+static int64_t rgemm_splits(int64_t P, int N, int K, int64_t img_px, int ntap = 1, int dtype = 0) {
   const int64_t plen = img_px > 0 ? img_px : P;
   const int64_t nimg = (img_px > 0 ? P / img_px : 1) * ntap;
-  const int64_t tiles = ((N + RG_BN - 1) / RG_BN) * ((K + RG_BK - 1) / RG_BK) * nimg;
-  return std::max<int64_t>(1, std::min<int64_t>((1024 + tiles - 1) / tiles, (plen + 511) / 512));
+  const int tn = rgemm_tn(N, dtype), tk = rgemm_tn(K, dtype);
+  const int64_t tiles = ((N + tn - 1) / tn) * ((K + tk - 1) / tk) * nimg;
+  // ~1024 blocks of the 64 x 64 tile (41 KB of LDS: 3 per CU), ~512 of a wider one (57-74 KB: 2 per
+  // CU) - every split adds N K fp32 partials written here and read back by rgemm_reduce
+  const int64_t target = (tn == 128 || tk == 128) ? 512 : 1024;
+  return std::max<int64_t>(1, std::min<int64_t>((target + tiles - 1) / tiles, (plen + 511) / 512));
+}
+template <typename... Args>
+static void launch_rgemm_bf16(int tn, int tk, dim3 grid, hipStream_t st, Args... args) {
+  if (tn == 128 && tk == 128) hipLaunchKernelGGL((rgemm_bf16_kernel<128, 128>), grid, dim3(256), 0, st, args...);
+  else if (tn == 128) hipLaunchKernelGGL((rgemm_bf16_kernel<128, 64>), grid, dim3(256), 0, st, args...);
+  else if (tk == 128) hipLaunchKernelGGL((rgemm_bf16_kernel<64, 128>), grid, dim3(256), 0, st, args...);
+  else hipLaunchKernelGGL((rgemm_bf16_kernel<64, 64>), grid, dim3(256), 0, st, args...);
 }
 
 }  // namespace turtle
@@ -1542,8 +1687,8 @@ int turtle_train_conv3x3_wgrad(const void* dy, int64_t lddy, const void* x, int6
   float* part = reinterpret_cast<float*>(ws);
   if (dtype == 1) {
     const dim3 grid((unsigned)(((N + RG_BN - 1) / RG_BN) * ((Cin + RG_BK - 1) / RG_BK) * nsplit), 9u);
-    hipLaunchKernelGGL(rgemm_bf16_kernel, grid, dim3(256), 0, st, (const bf16*)dy, lddy, (const bf16*)x, ldx, part, (int64_t)0, 9,
-                       N, Cin, P, ppb, H, W);
+    hipLaunchKernelGGL((rgemm_bf16_kernel<64, 64>), grid, dim3(256), 0, st, (const bf16*)dy, lddy, (const bf16*)x, ldx, part,
+                       (int64_t)0, 9, N, Cin, P, ppb, H, W);
   } else {
     const dim3 grid((unsigned)(((N + 63) / 64) * ((Cin + 63) / 64) * nsplit), 9u);
     hipLaunchKernelGGL(rgemm_f32_kernel, grid, dim3(256), 0, st, (const float*)dy, lddy, (const float*)x, ldx, part, (int64_t)0, 9,
@@ -1558,8 +1703,10 @@ int turtle_train_conv3x3_wgrad(const void* dy, int64_t lddy, const void* x, int6
 }
 
 size_t turtle_train_rgemm_workspace(int64_t P, int N, int K, int64_t img_px) {
+  // sized for the larger of the two dtype plans (the bf16 plan splits less for its wider tiles)
   const int64_t nimg = img_px > 0 ? P / img_px : 1;
-  return (size_t)rgemm_splits(P, N, K, img_px) * nimg * N * K * sizeof(float);
+  const int64_t ns = std::max(rgemm_splits(P, N, K, img_px, 1, 0), rgemm_splits(P, N, K, img_px, 1, 1));
+  return (size_t)ns * nimg * N * K * sizeof(float);
 }
 
 int turtle_train_rgemm(const void* a, int64_t lda, const void* b, int64_t ldb, float* c, int64_t P, int N, int K, int64_t img_px,
@@ -1570,17 +1717,17 @@ int turtle_train_rgemm(const void* a, int64_t lda, const void* b, int64_t ldb, f
     return -1;
   const int64_t plen = img_px > 0 ? img_px : P;
   const int64_t nimg = img_px > 0 ? P / img_px : 1;
-  int64_t nsplit = rgemm_splits(P, N, K, img_px);
+  int64_t nsplit = rgemm_splits(P, N, K, img_px, 1, dtype);
   if (!ws || ws_bytes < (size_t)nsplit * nimg * N * K * sizeof(float) || nimg > 65535) return -1;
   int64_t ppb = (plen + nsplit - 1) / nsplit;
   ppb = (ppb + RG_BP - 1) / RG_BP * RG_BP;
   nsplit = (plen + ppb - 1) / ppb;
-  const dim3 grid((unsigned)(((N + RG_BN - 1) / RG_BN) * ((K + RG_BK - 1) / RG_BK) * nsplit), (unsigned)nimg);
+  const int tn = rgemm_tn(N, dtype), tk = rgemm_tn(K, dtype);
+  const dim3 grid((unsigned)(((N + tn - 1) / tn) * ((K + tk - 1) / tk) * nsplit), (unsigned)nimg);
   hipStream_t st = (hipStream_t)stream;
   float* part = reinterpret_cast<float*>(ws);
   if (dtype == 1)
-    hipLaunchKernelGGL(rgemm_bf16_kernel, grid, dim3(256), 0, st, (const bf16*)a, lda, (const bf16*)b, ldb, part, img_px,
-                       (int)nimg, N, K, P, ppb);
+    launch_rgemm_bf16(tn, tk, grid, st, (const bf16*)a, lda, (const bf16*)b, ldb, part, img_px, (int)nimg, N, K, P, ppb, 0, 0);
   else
     hipLaunchKernelGGL(rgemm_f32_kernel, grid, dim3(256), 0, st, (const float*)a, lda, (const float*)b, ldb, part, img_px,
                        (int)nimg, N, K, P, ppb);
