@@ -68,7 +68,15 @@ for name, P, Cc in SHAPES:
     f_dw = lambda: L.turtle_train_dw3x3_wgrad(p(x), Cc, p(dy), Cc, p(dw9), p(db), 8, Cc, H, H, 1, st)
     w9 = torch.ones(9, Cc, device=dev)
     f_df = lambda: L.turtle_train_dw3x3_fwd(p(x), Cc, p(w9), None, p(y), Cc, 8, Cc, H, H, 0, 1, st)
-    for tag, fn, gb in (("ln_fwd", f_ln, 2 * mb), ("ln_bwd+res", f_lb, 4 * mb), ("ln_bwd", f_lb0, 3 * mb), ("colsum", f_cs, mb),
+    h = 3 * Cc                                       # a GatedFFN-like hidden width (2h gate input)
+    xg = torch.randn(P, 2 * h, device=dev).to(torch.bfloat16)
+    gg = torch.randn(P, h, device=dev).to(torch.bfloat16)
+    yg = torch.empty(P, h, device=dev, dtype=torch.bfloat16)
+    dxg = torch.empty(P, 2 * h, device=dev, dtype=torch.bfloat16)
+    f_gf = lambda: L.turtle_train_gate_fwd(p(xg), 2 * h, p(yg), h, P, h, 1, st)
+    f_gb = lambda: L.turtle_train_gate_bwd(p(xg), 2 * h, p(gg), h, p(dxg), 2 * h, P, h, 1, st)
+    mbh = P * h * 2 / 1e6
+    for tag, fn, gb in (("gate_fwd", f_gf, 3 * mbh), ("gate_bwd", f_gb, 5 * mbh), ("ln_fwd", f_ln, 2 * mb), ("ln_bwd+res", f_lb, 4 * mb), ("ln_bwd", f_lb0, 3 * mb), ("colsum", f_cs, mb),
                         ("dw_wgrad", f_dw, 2 * mb), ("dw_fwd", f_df, 2 * mb)):
         us = timeit(fn)
         print(f"{name:4s} P={P:7d} C={Cc:4d} {tag:11s} {us:8.1f} us  {gb / us:6.2f} TB/s")

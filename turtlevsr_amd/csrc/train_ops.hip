@@ -1416,9 +1416,9 @@ static int64_t rgemm_splits(int64_t P, int N, int K, int64_t img_px, int ntap = 
   const int64_t nimg = (img_px > 0 ? P / img_px : 1) * ntap;
   const int tn = rgemm_tn(N, dtype), tk = rgemm_tn(K, dtype);
   const int64_t tiles = ((N + tn - 1) / tn) * ((K + tk - 1) / tk) * nimg;
-  // ~1024 blocks of the 64 x 64 tile (41 KB of LDS: 3 per CU), ~512 of a wider one (57-74 KB: 2 per
+  // ~1024 blocks (64-wide tiles), ~512 of the 128 x 128 tile (74 KB of LDS: 2 per
   // CU) - every split adds N K fp32 partials written here and read back by rgemm_reduce
-  const int64_t target = (tn == 128 || tk == 128) ? 512 : 1024;
+  const int64_t target = (tn == 128 && tk == 128) ? 512 : 1024;
   return std::max<int64_t>(1, std::min<int64_t>((target + tiles - 1) / tiles, (plen + 511) / 512));
 }
 template <typename... Args>
