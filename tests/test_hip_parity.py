@@ -171,6 +171,7 @@ def test_kernel_variants_agree(dtype):
                  dict(base, gemm9=2), dict(base, gemm9=1), dict(base, gemm9=2, gemm_pn=1, tilepd=1, dwgemm=1),
                  dict(base, gemm_sk=1), dict(base, gemm_sk=1, gemm9=1, gemm_kt=1),
                  dict(base, gffn=1), dict(base, gffn=1, tilepd=1, gemm_pn=1, fuse=1, fused2=1, ffn=1),
+                 dict(base, split_out=0), dict(base, gemm_kt=1, kt_max_px=4096), dict(base, gemm_sk=1, sk_max_px=65536),
                  dict(base, gemm_kt=1, gemm_ar=1, gemm_pn=1, gemm_lds=1, fuse=1, fused2=1, dw_rows=1, panel_gemm=1, dwgemm=1, ffn=1),
                  dict(base, gemm_kt=1, gemm_ar=1, gemm_pn=1, fuse=1, fused2=1, dw_rows=1, dwgemm=1, ffn=1, tilepd=1),
                  dict(base, gemm_lds=1, gemm_pn=1, fuse=1, fused2=1, dw_rows=1, panel_gemm=1, sab_mfma=1, stem_mfma=1, gemm9=1)]

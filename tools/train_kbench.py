@@ -35,8 +35,21 @@ SHAPES = [("L1", 8 * 256 * 256, 64), ("L2", 8 * 128 * 128, 128), ("L3", 8 * 64 *
 print(f"TURTLE_TRAIN_ABL={os.environ.get('TURTLE_TRAIN_ABL', '0')} TURTLE_TRAIN_TUNE={os.environ.get('TURTLE_TRAIN_TUNE', '')}")
 # weight-gradient reduction GEMMs dW[N][K] = dy^T x over P pixels (config-5 shapes: GatedFFN project_in /
 # project_out, qkv, 64 x 64) - algorithmic bytes = dy + x once (the partials are overhead)
-for P, N, K in ((524288, 344, 64), (524288, 64, 176), (524288, 192, 64), (524288, 64, 64), (131072, 680, 128),
-                (131072, 128, 344), (32768, 1360, 256), (8192, 2720, 512)):
+# forward / input-gradient GEMMs y[P][N] = x[P][K] W^T (the inference GEMM family; the dgrad shapes have
+# the wide K): algorithmic bytes = x + W + y once
+for P, K, N in ((524288, 64, 320), (524288, 320, 64), (524288, 160, 64), (524288, 64, 160), (131072, 128, 640),
+                (131072, 640, 128), (131072, 320, 128), (32768, 256, 1280), (32768, 1280, 256), (8192, 512, 2560),
+                (8192, 2560, 512)):
+    x = torch.randn(P, K, device=dev).to(torch.bfloat16)
+    w = (0.05 * torch.randn(N, K, device=dev)).to(torch.bfloat16)
+    y = torch.empty(P, N, device=dev, dtype=torch.bfloat16)
+    fn = lambda: L.turtle_train_gemm(p(x), K, p(w), 0, 0, None, None, 0, p(y), N, P, K, N, 1, st)
+    assert fn() == 0
+    us = timeit(fn)
+    mb = (P * (K + N) + N * K) * 2 / 1e6
+    print(f"gemm  P={P:7d} K={K:5d} N={N:4d} {us:8.1f} us  {mb / us:6.2f} TB/s  {2 * P * K * N / us / 1e6:7.1f} TF/s")
+for P, N, K in ((524288, 320, 64), (524288, 64, 160), (524288, 192, 64), (524288, 64, 64), (131072, 640, 128),
+                (131072, 128, 320), (32768, 1280, 256), (8192, 2560, 512)):
     a = torch.randn(P, N, device=dev).to(torch.bfloat16)
     b_ = torch.randn(P, K, device=dev).to(torch.bfloat16)
     c = torch.zeros(N, K, device=dev)
@@ -68,7 +81,7 @@ for name, P, Cc in SHAPES:
     f_dw = lambda: L.turtle_train_dw3x3_wgrad(p(x), Cc, p(dy), Cc, p(dw9), p(db), 8, Cc, H, H, 1, st)
     w9 = torch.ones(9, Cc, device=dev)
     f_df = lambda: L.turtle_train_dw3x3_fwd(p(x), Cc, p(w9), None, p(y), Cc, 8, Cc, H, H, 0, 1, st)
-    h = 3 * Cc                                       # a GatedFFN-like hidden width (2h gate input)
+    h = 5 * Cc // 2                                  # the GatedFFN hidden width (ffn_expansion_factor 2.5)
     xg = torch.randn(P, 2 * h, device=dev).to(torch.bfloat16)
     gg = torch.randn(P, h, device=dev).to(torch.bfloat16)
     yg = torch.empty(P, h, device=dev, dtype=torch.bfloat16)

@@ -81,12 +81,12 @@ static int train_abl() {
   static const int v = [] { const char* e = getenv("TURTLE_TRAIN_ABL"); return e ? atoi(e) : 0; }();
   return v;
 }
-// launch-size sweeps of tools/train_kbench.py (TURTLE_TRAIN_TUNE="ln_blocks,cs_blocks,dwg_blocks", read once;
+// launch-size sweeps of tools/train_kbench.py (TURTLE_TRAIN_TUNE="ln_blocks,cs_blocks,dwg_blocks,kt_max_px", read once;
 // 0 or absent = the built-in choice)
 static int train_tune(int i) {
   static const std::vector<int> v = [] {
-    std::vector<int> r(3, 0);
-    if (const char* e = getenv("TURTLE_TRAIN_TUNE")) sscanf(e, "%d,%d,%d", &r[0], &r[1], &r[2]);
+    std::vector<int> r(4, 0);
+    if (const char* e = getenv("TURTLE_TRAIN_TUNE")) sscanf(e, "%d,%d,%d,%d", &r[0], &r[1], &r[2], &r[3]);
     return r;
   }();
   return v[i];
@@ -1624,6 +1624,7 @@ int turtle_train_gemm(const void* x, int64_t ldx, const void* w, int64_t wstride
   g.zeros = train_consts(0); g.ones = train_consts(1);
   if (!g.zeros) return (int)hipErrorOutOfMemory;
   g.allow_panel = g.allow_lds = g.allow_pn = g.allow_ar = g.allow_kt = 1;
+  if (train_tune(3) > 0) g.kt_max_px = train_tune(3);   // tools/train_kbench.py routing sweep
   try {
     if (dtype == 1) launch_gemm<bf16>(g, (hipStream_t)stream);
     else launch_gemm<float>(g, (hipStream_t)stream);

@@ -18,7 +18,11 @@ base_model.py:340-365, dist_util.py:15-30) on the GPU:
 * ``Trainer.train_step``: zero_grad -> autocast forward over the T frames -> L1 per frame summed,
   / T -> ``+ 0 * sum(p.sum())`` (every parameter in the graph, so DDP needs no unused-parameter
   search, :99) -> (GradScaler for fp16) backward -> AdamW step -> loss reduced to rank 0 (dist.reduce
-  + / world_size, base_model.py:340-365);
+  + / world_size, base_model.py:340-365). On the HIP op set (round 6) the weight gradients of the T
+  frames accumulate in place into one fp32 arena (``train_ops.ParamGradAccumulator``; the 0 * sum(p)
+  term then adds its zero gradient only to parameters no HIP op reported) and every block's
+  residual add is the last GEMM's epilogue, its gradient summed inside the LayerNorm backward
+  (``_ln_res``);
 * multi-GPU: one process per GPU, ``torch.nn.parallel.DistributedDataParallel`` over the
   ``nccl`` backend (RCCL over xGMI on MI355X): the gradient all-reduce is bucketed and overlaps the
   backward; buckets are sized for xGMI (fewer, larger all-reduces of the 236 MB fp32 gradient).
@@ -125,10 +129,10 @@ def _sab_hip_ok(ops, name: str, n: int, g: int = 8, d: int = 8) -> bool:
 
 
 class _ToNCHW(torch.autograd.Function):
-    """x.contiguous() for MIOpen's NCHW convolution path whose gradient goes back in x's own
-    memory format: otherwise the NCHW input gradient of every dense conv (and the loss's NCHW
-    gradient through the ending conv) makes the whole channels-last residual-stream backward NCHW,
-    and each HIP op re-lays it out."""
+    """x.contiguous() for F.conv2d's NCHW path (a channels-last op set without a dense-conv kernel
+    for that shape) whose gradient goes back in x's own memory format: otherwise the NCHW input
+    gradient of the dense conv makes the channels-last residual-stream backward NCHW, and each
+    following op re-lays it out."""
 
     @staticmethod
     def forward(ctx, x):
