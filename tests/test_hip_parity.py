@@ -159,7 +159,7 @@ def test_kernel_variants_agree(dtype):
     base = {"fuse": 0, "fused2": 0, "panel_gemm": 0, "dw_rows": 0, "gemm_lds": 0, "gemm_pn": 0, "sab_mfma": 0,
             "stem_mfma": 0, "gemm_ar": 0, "gemm_kt": 0, "dwgemm": 0, "dwgemm_min_blocks": 0, "ffn": 0, "down_tile": 0,
             "tilepd": 0, "tilepd_min_blocks": 0, "tilepd_gate": 0, "gemm8": 0, "gemm8_ps": 0, "attn_fin": 0, "sab_waves": 4,
-            "gemm9": 0, "gemm_f32": 0, "gemm_sk": 0, "gffn": 0, "gffn_min_blocks": 0}
+            "gemm9": 0, "gemm_f32": 0, "gemm_sk": 0, "gffn": 0, "gffn_min_blocks": 0, "gffn_c128": 0, "gffn_c64": 0}
     ref = _run(_opts(_model(meta, "fp32"), base), clip)[0]
     variants = [dict(base, fuse=f, panel_gemm=p, dw_rows=d) for f in (0, 1) for p in (0, 1) for d in (0, 1)]
     variants += [dict(base, fuse=1, fuse_fp32=1), dict(base, fuse=1, fuse_fp32=1, panel_gemm=1)]   # fp32 fused block kernel
@@ -170,7 +170,7 @@ def test_kernel_variants_agree(dtype):
                  dict(base, tilepd=1, tilepd_gate=1, tilepd_cb=0), dict(base, gemm8=2), dict(base, gemm8=2, gemm8_ps=1), dict(base, gemm8=3, gemm_kt=1), dict(base, gemm8=2, gemm_kt=1, tilepd=1), dict(base, attn_fin=1), dict(base, sab_waves=8),
                  dict(base, gemm9=2), dict(base, gemm9=1), dict(base, gemm9=2, gemm_pn=1, tilepd=1, dwgemm=1),
                  dict(base, gemm_sk=1), dict(base, gemm_sk=1, gemm9=1, gemm_kt=1),
-                 dict(base, gffn=1), dict(base, gffn=1, tilepd=1, gemm_pn=1, fuse=1, fused2=1, ffn=1),
+                 dict(base, gffn=1), dict(base, gffn=1, gffn_c128=1), dict(base, gffn=1, gffn_c64=1), dict(base, gffn=1, tilepd=1, gemm_pn=1, fuse=1, fused2=1, ffn=1),
                  dict(base, split_out=0), dict(base, gemm_kt=1, kt_max_px=4096), dict(base, gemm_sk=1, sk_max_px=65536),
                  dict(base, gemm_kt=1, gemm_ar=1, gemm_pn=1, gemm_lds=1, fuse=1, fused2=1, dw_rows=1, panel_gemm=1, dwgemm=1, ffn=1),
                  dict(base, gemm_kt=1, gemm_ar=1, gemm_pn=1, fuse=1, fused2=1, dw_rows=1, dwgemm=1, ffn=1, tilepd=1),

@@ -60,7 +60,7 @@ struct Model {
       for (int k = 0; k < C; ++k) { w1f[(size_t)n * C + k] = w1[(size_t)n * C + k] * g[k]; t += w1[(size_t)n * C + k] * bln[k]; }
       tb[n] = t;
     }
-    gffn_pack(hd, w1f, tb, dw9, dwb, w2, hp);
+    gffn_pack(256, hd, w1f, tb, dw9, dwb, w2, hp);
     CK(hipMalloc(&dw1f, hp.w1f.size() * 2)); CK(hipMalloc(&dw2f, hp.w2f.size() * 2));
     CK(hipMalloc(&dtbp, hp.tbp.size() * 4)); CK(hipMalloc(&ddwp, hp.dwp.size() * 4)); CK(hipMalloc(&db2, C * 4));
     CK(hipMemcpy(dw1f, hp.w1f.data(), hp.w1f.size() * 2, hipMemcpyHostToDevice));
@@ -72,7 +72,7 @@ struct Model {
   }
   GffnArgs args(void* x, void* out, int nimg, int H, int W) const {
     GffnArgs a{};
-    a.x = x; a.out = out; a.nimg = nimg; a.H = H; a.W = W; a.hd = hd; a.centred = 1;
+    a.x = x; a.out = out; a.nimg = nimg; a.H = H; a.W = W; a.hd = hd; a.C = 256; a.centred = 1;
     a.w1f = dw1f; a.tbp = (const float*)dtbp; a.dwp = (const uint32_t*)ddwp; a.w2f = dw2f; a.b2 = (const float*)db2;
     return a;
   }

@@ -4,8 +4,11 @@
 //                                                                               the block's x + ffn(norm2(x)))
 //
 // LN = the block's LayerNorm (turtle_t1_arch.py:83-112; W1' = W1 diag(g), tb = W1 b_ln + b1 folded at pack
-// time), dw = depthwise 3x3 with zero padding of H at the image border. Input width C = 256, hidden
-// width hd = 64 k (GoPro level 3: hd = 640, H = 2 hd = 1280 channels). Against project_in GEMM ->
+// time), dw = depthwise 3x3 with zero padding of H at the image border. Input width C = 256 (level 3),
+// 128 or 64 (levels 2 / 1, round 6: instead of the fused2 row walk), hidden width hd = 64 k (GoPro level 3:
+// hd = 640, H = 2 hd = 1280 channels; level 2: 320; level 1: 160, run as 192 with zero weights for the
+// padding channels - exact: their H, G and W2 columns are 0). At width 64 P3's 64 output channels are
+// 4 groups of 16 and each group's 7 pixel tiles are split 4 / 3 over two waves. Against project_in GEMM ->
 // depthwise + gate -> project_out GEMM with the hidden map in HBM (1080p level 3: 334 MB written and
 // read back per block, 20 blocks per frame) only x is read and the output written.
 //
@@ -37,16 +40,28 @@ typedef _Float16 f16;
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
-constexpr int GF_C = 256, GF_TX = 14, GF_TR = 8, GF_RH = GF_TR + 2, GF_NXP = 16 * GF_RH, GF_NGP = GF_TX * GF_TR;
+constexpr int GF_TX = 14, GF_TR = 8, GF_RH = GF_TR + 2, GF_NXP = 16 * GF_RH, GF_NGP = GF_TX * GF_TR;
 constexpr int GF_NT = 512;
-constexpr int GF_XP = GF_C * 2 + 32;                  // LDS bytes per haloed pixel of X (+32: conflict-free b128)
-constexpr int GF_OFF_G = GF_NXP * GF_XP;              // two G buffers: [8 groups][112 px][8 ch] f16 each
-constexpr int GF_OFF_SINK = GF_OFF_G + 2 * 8 * GF_NGP * 16;   // P2 store target of the x-halo lanes (no branch per row)
 constexpr int GF_MAXNC = 12;                                 // hidden width <= 768 (taps / tb tables in LDS)
-constexpr int GF_OFF_TAP = GF_OFF_SINK + 8 * 64 * 4;          // depthwise taps + bias of every chunk, P2 lane order
-constexpr int GF_OFF_TB = GF_OFF_TAP + GF_MAXNC * 8 * 4 * 80; // P1 epilogue vectors (W1 b_ln + b1) of every chunk
-constexpr int GF_LDS = GF_OFF_TB + GF_MAXNC * 128 * 4;
-static_assert(GF_LDS <= 160 * 1024, "gffn LDS budget");
+// geometry per input width C: X rows, K steps per chunk, output channels per wave
+template <int C>
+struct GfGeom {
+  static constexpr int XP = C * 2 + 32;                      // LDS bytes per haloed pixel of X (+32: conflict-free b128)
+  static constexpr int OFF_G = GF_NXP * XP;                  // two G buffers: [8 groups][112 px][8 ch] f16 each
+  static constexpr int OFF_SINK = OFF_G + 2 * 8 * GF_NGP * 16;   // P2 store target of the x-halo lanes (no branch per row)
+  static constexpr int OFF_TAP = OFF_SINK + 8 * 64 * 4;      // depthwise taps + bias of every chunk, P2 lane order
+  static constexpr int OFF_TB = OFF_TAP + GF_MAXNC * 8 * 4 * 80;   // P1 epilogue vectors (W1 b_ln + b1) of every chunk
+  static constexpr int LDS = OFF_TB + GF_MAXNC * 128 * 4;
+  static constexpr int KS = C / 32;                          // P1 K steps per chunk (32 input channels each)
+  static constexpr bool SN = C == 64;                        // P3 at width 64: 4 channel groups x 2 pixel halves of waves
+  static constexpr int MW = SN ? 1 : C / 128;                // P3: 16 MW output channels per wave (MW MFMA row tiles)
+  static constexpr int CW = SN ? 4 : 8;                      // P3 output-channel groups
+  static constexpr int NTW = SN ? 4 : 7;                     // P3 pixel N tiles per wave (7 = 112 px / 16)
+  static constexpr int CPL = C / 64;                         // prologue: 16-byte chunks per lane of a pixel's 8 lanes
+  static constexpr int RPS = GF_TR / KS;                     // P2 output rows per P1 K step
+  static_assert(LDS <= 160 * 1024, "gffn LDS budget");
+  static_assert(KS * RPS == GF_TR, "P2 rows per K step");
+};
 static_assert(GF_NGP == 7 * 16, "P3 N tiles");
 
 __device__ __attribute__((aligned(64))) uint4 g_zero_gf[4];
@@ -72,14 +87,20 @@ TURTLE_DEV void gf_for(F&& f) {
   }
 }
 
-template <int DBG>
+template <int C, int DBG>
 __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
+  using G = GfGeom<C>;
+  constexpr int KS = G::KS, MW = G::MW, XP = G::XP, NTW = G::NTW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* sX = smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int xl = lane & 15, g4 = lane >> 4;
   const int nc = a.hd / 64;
+  // P3 / epilogue ownership: output-channel group cw, pixel N tiles n0 .. n0 + NTW - 1 (ntl of them live)
+  const int cw = G::SN ? (wid & 3) : wid;
+  const int n0 = G::SN ? (wid >> 2) * 4 : 0;
+  const int ntl = G::SN ? ((wid >> 2) ? 3 : 4) : 7;
 
   // ---- tile (row-major over the image; consecutive tiles on one XCD share halo rows) ----
   const int tx_n = (a.W + GF_TX - 1) / GF_TX, ty_n = (a.H + GF_TR - 1) / GF_TR;
@@ -100,41 +121,41 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
   const uint4* W2F = reinterpret_cast<const uint4*>(a.w2f);
   const uint32_t* DWP = a.dwp;                              // (no lambda below refers to `a`: a by-reference capture of the
   const float* TBP = a.tbp;                                 // kernel argument would copy it to scratch)
-  uint4 wf[4];                                              // 4 slots: 8 steps per chunk keep the slot of step k = k & 3
+  uint4 wf[4];                                              // 4 slots: 8 (4) steps per chunk keep the slot of step k = k & 3
   uint4 tq[5];
-  uint4 w2[2][2];
+  uint4 w2[MW][2];
   f32x4 tbv;
   auto ld_w1 = [&](int c, auto K) __attribute__((always_inline)) {
     constexpr int k = decltype(K)::value;
-    wf[k & 3] = (DBG & 8) ? make_uint4(lane, k, c, 0) : W1F[((c * 8 + wid) * 8 + k) * 64 + lane];
+    wf[k & 3] = (DBG & 8) ? make_uint4(lane, k, c, 0) : W1F[((c * 8 + wid) * KS + k) * 64 + lane];
   };
   // taps and tb vectors come from LDS tables filled once per block (prologue)
   auto ld_taps = [&](int c) __attribute__((always_inline)) {
-    const uint4* tp = reinterpret_cast<const uint4*>(smem + GF_OFF_TAP + (((c * 8 + wid) * 4 + g4) * 20) * 4);
+    const uint4* tp = reinterpret_cast<const uint4*>(smem + G::OFF_TAP + (((c * 8 + wid) * 4 + g4) * 20) * 4);
 #pragma unroll
     for (int q = 0; q < 5; ++q) tq[q] = tp[q];
   };
   auto ld_tb = [&](int c) __attribute__((always_inline)) {
-    tbv = *reinterpret_cast<const f32x4*>(smem + GF_OFF_TB + ((c * 8 + wid) * 16 + 4 * g4) * 4);
+    tbv = *reinterpret_cast<const f32x4*>(smem + G::OFF_TB + ((c * 8 + wid) * 16 + 4 * g4) * 4);
   };
   auto ld_w2 = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < MW; ++m)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        w2[m][ks] = (DBG & 8) ? make_uint4(lane, m, ks, c) : W2F[(((c * 8 + wid) * 2 + m) * 2 + ks) * 64 + lane];
+        w2[m][ks] = (DBG & 8) ? make_uint4(lane, m, ks, c) : W2F[(((c * G::CW + cw) * MW + m) * 2 + ks) * 64 + lane];
   };
   ld_w1(0, std::integral_constant<int, 0>{});
   ld_w1(0, std::integral_constant<int, 1>{});
-  ld_w1(0, std::integral_constant<int, 2>{});
+  if constexpr (KS > 2) ld_w1(0, std::integral_constant<int, 2>{});
 
-  // ---- haloed x tile -> LayerNorm in registers -> LDS (f16). A pixel's 32 16-byte chunks are held
-  // by an aligned group of 8 lanes (chunks cc, cc + 8, cc + 16, cc + 24); statistics by an 8-lane DPP
+  // ---- haloed x tile -> LayerNorm in registers -> LDS (f16). A pixel's C / 8 16-byte chunks are held
+  // by an aligned group of 8 lanes (chunks cc, cc + 8, ...); statistics by an 8-lane DPP
   // reduction, two passes (biased variance, eps 1e-5 inside the sqrt: turtle_t1_arch.py:78-80, 96-99);
   // pixels outside the image are 0 and stay 0 (and P1 keeps their H at 0: the depthwise zero padding).
   // The two G buffers start zeroed (P3 of the first loop interval multiplies one of them) ----
   {
-    constexpr int LPP = 8, CPL = 4, PPJ = GF_NT / LPP, NJ = (GF_NXP + PPJ - 1) / PPJ;
+    constexpr int LPP = 8, CPL = G::CPL, PPJ = GF_NT / LPP, NJ = (GF_NXP + PPJ - 1) / PPJ;
     const bf16* X = reinterpret_cast<const bf16*>(a.x);
     const int cc = tid % LPP, pq = tid / LPP;
     auto sum8 = [](float v) __attribute__((always_inline)) {
@@ -149,20 +170,20 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
       const int p = j * PPJ + pq, hr = p >> 4, hp = p & 15;
       const int y = y0 - 1 + hr, x = x0 - 1 + hp;
       const bool ok = p < GF_NXP && y >= 0 && y < a.H && x >= 0 && x < a.W;
-      const bf16* src = X + (((int64_t)img * a.H + (ok ? y : 0)) * a.W + (ok ? x : 0)) * GF_C + cc * 8;
+      const bf16* src = X + (((int64_t)img * a.H + (ok ? y : 0)) * a.W + (ok ? x : 0)) * C + cc * 8;
 #pragma unroll
       for (int q = 0; q < CPL; ++q)
         vx[j][q] = (DBG & 16) ? make_uint4(p, q, cc, 0x3f803f80u) : ld16(ok ? reinterpret_cast<const void*>(src + q * LPP * 8) : g_zero_gf);
     }
     for (int e = tid; e < 2 * 8 * GF_NGP; e += GF_NT)
-      *reinterpret_cast<uint4*>(smem + GF_OFF_G + e * 16) = make_uint4(0u, 0u, 0u, 0u);
+      *reinterpret_cast<uint4*>(smem + G::OFF_G + e * 16) = make_uint4(0u, 0u, 0u, 0u);
     {
       const int ntap = nc * 8 * 4 * 5, ntb = nc * 32;             // 16-byte pieces
       for (int e = tid; e < ntap; e += GF_NT)
-        *reinterpret_cast<uint4*>(smem + GF_OFF_TAP + e * 16) =
+        *reinterpret_cast<uint4*>(smem + G::OFF_TAP + e * 16) =
             (DBG & 8) ? make_uint4(0x3c003c00u, e, 0u, 0u) : reinterpret_cast<const uint4*>(DWP)[e];
       for (int e = tid; e < ntb; e += GF_NT)
-        *reinterpret_cast<uint4*>(smem + GF_OFF_TB + e * 16) = (DBG & 8) ? make_uint4(0u, 0u, 0u, 0u) : reinterpret_cast<const uint4*>(TBP)[e];
+        *reinterpret_cast<uint4*>(smem + G::OFF_TB + e * 16) = (DBG & 8) ? make_uint4(0u, 0u, 0u, 0u) : reinterpret_cast<const uint4*>(TBP)[e];
     }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -174,7 +195,7 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) sm += vv.v[e];
       }
-      const float mu = sum8(sm) * (1.f / GF_C);
+      const float mu = sum8(sm) * (1.f / C);
       float sq = 0.f;
 #pragma unroll
       for (int q = 0; q < CPL; ++q) {
@@ -182,7 +203,7 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) { const float d = vv.v[e] - mu; sq = fmaf(d, d, sq); }
       }
-      const float rs = rsqrtf(sum8(sq) * (1.f / GF_C) + 1e-5f);
+      const float rs = rsqrtf(sum8(sq) * (1.f / C) + 1e-5f);
       const float c0 = a.centred ? -mu * rs : 0.f;
       if (p < GF_NXP) {
 #pragma unroll
@@ -191,7 +212,7 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
           uint32_t w[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) w[e] = pk_f16(fmaf(vv.v[2 * e], rs, c0), fmaf(vv.v[2 * e + 1], rs, c0));
-          *reinterpret_cast<uint4*>(sX + p * GF_XP + (cc + q * LPP) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
+          *reinterpret_cast<uint4*>(sX + p * XP + (cc + q * LPP) * 16) = make_uint4(w[0], w[1], w[2], w[3]);
         }
       }
     }
@@ -207,11 +228,11 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
     rowok |= (colok && yg >= 0 && yg < a.H) ? (1u << r) : 0u;
   }
 
-  f32x4 oacc[2][7];
+  f32x4 oacc[MW][NTW];
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
+  for (int m = 0; m < MW; ++m)
 #pragma unroll
-    for (int n = 0; n < 7; ++n) oacc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NTW; ++n) oacc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // P1 state: acc[r] = the lane's 4 slots (x1 c, x1 c+1, x2 c, x2 c+1 of gate pair 4 wid + g4) of
   // haloed pixel (r, xl); hv = the previous chunk's H as f16 pairs (P2's input)
@@ -219,10 +240,10 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
   uint32_t hv[GF_RH][2];
 #pragma unroll
   for (int r = 0; r < GF_RH; ++r) hv[r][0] = hv[r][1] = 0u;
-  const char* xb = sX + xl * GF_XP + g4 * 16;
+  const char* xb = sX + xl * XP + g4 * 16;
   f16x8 xa[5];                                              // P1 fragments of haloed rows 0-4, one K step ahead
   const bool wr = xl >= 1 && xl <= GF_TX;
-  char* sink = smem + GF_OFF_SINK + tid * 4;
+  char* sink = smem + G::OFF_SINK + tid * 4;
 
   auto p1_init = [&]() __attribute__((always_inline)) {
 #pragma unroll
@@ -232,14 +253,19 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
   // stream runs three steps ahead (into the next chunk cn during the last three steps)
   auto p1_step = [&](auto K, int c, int cn) __attribute__((always_inline)) {
     constexpr int k = decltype(K)::value;
-    if constexpr (k + 3 < 8) ld_w1(c, std::integral_constant<int, k + 3>{});
-    else ld_w1(cn, std::integral_constant<int, k - 5>{});
+    // KS >= 4: three steps ahead through the 4-slot ring (slot = step & 3). KS = 2 (width 64): the next
+    // chunk's step k replaces this step's slot after its MFMAs (two steps ahead; 3 would overwrite step
+    // k + 1 of this chunk)
+    if constexpr (KS >= 4) {
+      if constexpr (k + 3 < KS) ld_w1(c, std::integral_constant<int, k + 3>{});
+      else ld_w1(cn, std::integral_constant<int, k + 3 - KS>{});
+    }
     // rows 0-4 of this step were read at the end of the previous step (their latency behind its P2
     // row); rows 5-9 are read before rows 0-4 multiply, and rows 0-4 of the NEXT step (the next chunk's
     // step 0 after step 7: X does not change) after rows 5-9 multiply
     f16x8 xb5[5];
 #pragma unroll
-    for (int i = 0; i < 5; ++i) xb5[i] = *reinterpret_cast<const f16x8*>(xb + (5 + i) * 16 * GF_XP + k * 64);
+    for (int i = 0; i < 5; ++i) xb5[i] = *reinterpret_cast<const f16x8*>(xb + (5 + i) * 16 * XP + k * 64);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < 5; ++i) {
@@ -252,8 +278,9 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
       if constexpr ((DBG & 1) == 0) acc[5 + i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(wf[k & 3]), xb5[i], acc[5 + i], 0, 0, 0);
       else acc[5 + i][0] += (float)xb5[i][0] + (float)as_f16x8(wf[k & 3])[1];
     }
+    if constexpr (KS < 4) ld_w1(cn, K);
 #pragma unroll
-    for (int i = 0; i < 5; ++i) xa[i] = *reinterpret_cast<const f16x8*>(xb + i * 16 * GF_XP + ((k + 1) & 7) * 64);
+    for (int i = 0; i < 5; ++i) xa[i] = *reinterpret_cast<const f16x8*>(xb + i * 16 * XP + ((k + 1) % KS) * 64);
     __builtin_amdgcn_sched_barrier(0);
   };
   auto p1_finish = [&]() __attribute__((always_inline)) {
@@ -299,48 +326,53 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
     const char* gb = gbuf + xl * 16;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      f16x8 bfr[7];
+      f16x8 bfr[NTW];
 #pragma unroll
-      for (int n = 0; n < 7; ++n) bfr[n] = *reinterpret_cast<const f16x8*>(gb + ((ks * 4 + g4) * GF_NGP + n * 16) * 16);
+      for (int j = 0; j < NTW; ++j) {                        // (a dead 4th tile of the second wave half re-reads tile 6)
+        const int n = min(n0 + j, 6);
+        bfr[j] = *reinterpret_cast<const f16x8*>(gb + ((ks * 4 + g4) * GF_NGP + n * 16) * 16);
+      }
       if constexpr ((DBG & 4) == 0) {
 #pragma unroll
-        for (int n = 0; n < 7; ++n) {
-          oacc[0][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(w2[0][ks]), bfr[n], oacc[0][n], 0, 0, 0);
-          oacc[1][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(w2[1][ks]), bfr[n], oacc[1][n], 0, 0, 0);
-        }
+        for (int j = 0; j < NTW; ++j)
+#pragma unroll
+          for (int m = 0; m < MW; ++m)
+            oacc[m][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(as_f16x8(w2[m][ks]), bfr[j], oacc[m][j], 0, 0, 0);
       } else {
 #pragma unroll
-        for (int n = 0; n < 7; ++n) { oacc[0][n][0] += (float)bfr[n][0]; oacc[1][n][0] += (float)as_f16x8(w2[1][ks])[0]; }
+        for (int j = 0; j < NTW; ++j) { oacc[0][j][0] += (float)bfr[j][0]; oacc[MW - 1][j][1] += (float)as_f16x8(w2[MW - 1][ks])[0]; }
       }
     }
   };
-  char* const G0 = smem + GF_OFF_G;
-  char* const G1 = smem + GF_OFF_G + 8 * GF_NGP * 16;
+  char* const G0 = smem + G::OFF_G;
+  char* const G1 = smem + G::OFF_G + 8 * GF_NGP * 16;
   auto gbuf = [&](int c) __attribute__((always_inline)) { return (c & 1) ? G1 : G0; };
 
   __syncthreads();
 
   // ---- interval 0: P1(0) ----
 #pragma unroll
-  for (int i = 0; i < 5; ++i) xa[i] = *reinterpret_cast<const f16x8*>(xb + i * 16 * GF_XP);
+  for (int i = 0; i < 5; ++i) xa[i] = *reinterpret_cast<const f16x8*>(xb + i * 16 * XP);
   ld_tb(0);
   p1_init();
-  gf_for<0, 8>([&](auto K) __attribute__((always_inline)) { p1_step(K, 0, nc > 1 ? 1 : 0); });
+  gf_for<0, KS>([&](auto K) __attribute__((always_inline)) { p1_step(K, 0, nc > 1 ? 1 : 0); });
   p1_finish();
   ld_taps(0);
   ld_tb(nc > 1 ? 1 : 0);
   ld_w2(0);
   __syncthreads();
 
-  // ---- intervals 1 .. nc - 1: P1(c) with P2(c - 1) interleaved row by row (one output row per K step),
+  // ---- intervals 1 .. nc - 1: P1(c) with P2(c - 1) interleaved row by row (RPS output rows per K step),
   // then P3(c - 2) (at c = 1 over the zeroed G buffer: adds 0) ----
   for (int c = 1; c < nc; ++c) {
     const int cn = c + 1 < nc ? c + 1 : c;
     char* gw = gbuf(c - 1);
     p1_init();
-    gf_for<0, 8>([&](auto K) __attribute__((always_inline)) {
+    gf_for<0, KS>([&](auto K) __attribute__((always_inline)) {
       p1_step(K, c, cn);
-      p2_row(std::integral_constant<int, decltype(K)::value + 1>{}, gw);
+      gf_for<0, G::RPS>([&](auto J) __attribute__((always_inline)) {
+        p2_row(std::integral_constant<int, decltype(K)::value * G::RPS + decltype(J)::value + 1>{}, gw);
+      });
     });
     p1_finish();
     ld_taps(c);
@@ -356,62 +388,74 @@ __global__ __launch_bounds__(GF_NT, 1) void gffn_kernel(GffnArgs a) {
   __syncthreads();
   p3(gbuf(nc - 1));
 
-  // ---------------- epilogue: out = x + acc + b2 (8 consecutive channels per lane and N tile) ----------------
+  // ---------------- epilogue: out = x + acc + b2 (4 MW consecutive channels per lane and N tile) ----------------
   {
-    const int chb = 32 * wid + 8 * g4;
-    f32x4 bb0 = f32x4{0.f, 0.f, 0.f, 0.f}, bb1 = bb0;
-    if (a.b2) {
-      bb0 = *reinterpret_cast<const f32x4*>(a.b2 + chb);
-      bb1 = *reinterpret_cast<const f32x4*>(a.b2 + chb + 4);
-    }
+    constexpr int NCH = 4 * MW;
+    const int chb = 16 * MW * cw + NCH * g4;
+    f32x4 bb[MW];
+#pragma unroll
+    for (int m = 0; m < MW; ++m)
+      bb[m] = a.b2 ? *reinterpret_cast<const f32x4*>(a.b2 + chb + 4 * m) : f32x4{0.f, 0.f, 0.f, 0.f};
     const bf16* X = reinterpret_cast<const bf16*>(a.x);
     bf16* O = reinterpret_cast<bf16*>(a.out);
-    uint4 rv[7];                                            // every residual load in flight before the first store
-    int64_t offs[7];
-    bool st[7];
+    typedef uint32_t rawv __attribute__((ext_vector_type(NCH / 2)));   // the lane's NCH bf16 channels, raw
+    rawv rv[NTW];                                           // every residual load in flight before the first store
+    int64_t offs[NTW];
+    bool st[NTW];
 #pragma unroll
-    for (int n = 0; n < 7; ++n) {
-      const int gp = n * 16 + xl, o = gp / GF_TX, xo = gp - o * GF_TX;
+    for (int n = 0; n < NTW; ++n) {
+      const int gp = min(n0 + n, 6) * 16 + xl, o = gp / GF_TX, xo = gp - o * GF_TX;
       const int y = y0 + o, x = x0 + xo;
-      st[n] = y < a.H && x < a.W;
-      offs[n] = (((int64_t)img * a.H + (st[n] ? y : 0)) * a.W + (st[n] ? x : 0)) * GF_C + chb;
-      rv[n] = ld16(X + offs[n]);
+      st[n] = n < ntl && y < a.H && x < a.W;
+      offs[n] = (((int64_t)img * a.H + (st[n] ? y : 0)) * a.W + (st[n] ? x : 0)) * C + chb;
+      rv[n] = *reinterpret_cast<const rawv*>(X + offs[n]);
     }
+    typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int n = 0; n < 7; ++n) {
-      Vec<bf16> r; r.from_raw(rv[n]);
+    for (int n = 0; n < NTW; ++n) {
+      rawv ov;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        r.v[e] += oacc[0][n][e] + bb0[e];
-        r.v[4 + e] += oacc[1][n][e] + bb1[e];
+      for (int q = 0; q < NCH / 2; ++q) {
+        const uint32_t wv = rv[n][q];
+        const int m = (2 * q) / 4, e = (2 * q) % 4;
+        const f32x2 sum2 = {__uint_as_float(wv << 16) + (oacc[m][n][e] + bb[m][e]),
+                            __uint_as_float(wv & 0xffff0000u) + (oacc[m][n][e + 1] + bb[m][e + 1])};
+        ov[q] = __builtin_bit_cast(uint32_t, __builtin_convertvector(sum2, bf16x2v));
       }
-      if (st[n]) r.store(O + offs[n]);
+      if (st[n]) *reinterpret_cast<rawv*>(O + offs[n]) = ov;
     }
   }
 }
 
 bool gffn_ok(const GffnArgs& a) {
   if (!a.x || !a.out || !a.w1f || !a.tbp || !a.dwp || !a.w2f || a.x == a.out) return false;
-  if (a.hd <= 0 || a.hd % 64 || a.hd > 64 * GF_MAXNC) return false;
+  if ((a.C != 256 && a.C != 128 && a.C != 64) || a.hd <= 0 || a.hd % 64 || a.hd > 64 * GF_MAXNC) return false;
   if (reinterpret_cast<uintptr_t>(a.x) % 16 || reinterpret_cast<uintptr_t>(a.out) % 16 || reinterpret_cast<uintptr_t>(a.w1f) % 16 ||
       reinterpret_cast<uintptr_t>(a.w2f) % 16 || reinterpret_cast<uintptr_t>(a.tbp) % 16 || reinterpret_cast<uintptr_t>(a.dwp) % 16 ||
       (a.b2 && reinterpret_cast<uintptr_t>(a.b2) % 16))
     return false;
-  return a.H > 0 && a.W > 0 && a.nimg > 0 && (int64_t)a.nimg * a.H * a.W * GF_C < ((int64_t)1 << 40);
+  return a.H > 0 && a.W > 0 && a.nimg > 0 && (int64_t)a.nimg * a.H * a.W * a.C < ((int64_t)1 << 40);
 }
 
 int64_t gffn_blocks(const GffnArgs& a) {
   return (int64_t)a.nimg * ((a.H + GF_TR - 1) / GF_TR) * ((a.W + GF_TX - 1) / GF_TX);
 }
 
-template <int DBG>
-static void gf_launch(const GffnArgs& a, hipStream_t st) {
+template <int C, int DBG>
+static void gf_launch_c(const GffnArgs& a, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gffn_kernel<DBG>), hipFuncAttributeMaxDynamicSharedMemorySize, GF_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(gffn_kernel<C, DBG>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              GfGeom<C>::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL(gffn_kernel<DBG>, dim3((unsigned)gffn_blocks(a)), dim3(GF_NT), GF_LDS, st, a);
+  hipLaunchKernelGGL((gffn_kernel<C, DBG>), dim3((unsigned)gffn_blocks(a)), dim3(GF_NT), GfGeom<C>::LDS, st, a);
+}
+template <int DBG>
+static void gf_launch(const GffnArgs& a, hipStream_t st) {
+  if (a.C == 64) gf_launch_c<64, DBG>(a, st);
+  else if (a.C == 128) gf_launch_c<128, DBG>(a, st);
+  else gf_launch_c<256, DBG>(a, st);
 }
 
 void launch_gffn(const GffnArgs& a, hipStream_t st) {
@@ -445,9 +489,9 @@ static uint16_t f16_bits(double x) {
   return u;
 }
 
-void gffn_pack(int hd, const std::vector<double>& w1, const std::vector<double>& tb, const std::vector<double>& dw9,
+void gffn_pack(int C, int hd, const std::vector<double>& w1, const std::vector<double>& tb, const std::vector<double>& dw9,
                const std::vector<double>& dwb, const std::vector<double>& w2, GffnHost& o) {
-  const int C = GF_C, nc = hd / 64, H2 = 2 * hd;
+  const int nc = hd / 64, H2 = 2 * hd, KS = C / 32, MW = C >= 128 ? C / 128 : 1, CW = C == 64 ? 4 : 8;
   // hidden row of slot s of unit u in chunk c: gate pair p = 4 u + s / 4 (chunk-local), e = s % 4:
   // (x1 2p, x1 2p + 1, x2 2p, x2 2p + 1)
   auto hrow = [&](int c, int u, int s) {
@@ -460,10 +504,10 @@ void gffn_pack(int hd, const std::vector<double>& w1, const std::vector<double>&
   for (int c = 0; c < nc; ++c)
     for (int u = 0; u < 8; ++u) {
       for (int s = 0; s < 16; ++s) o.tbp[(size_t)(c * 8 + u) * 16 + s] = tb.empty() ? 0.f : (float)tb[hrow(c, u, s)];
-      for (int k = 0; k < 8; ++k)
+      for (int k = 0; k < KS; ++k)
         for (int l = 0; l < 64; ++l)
           for (int j = 0; j < 8; ++j)
-            o.w1f[((((size_t)(c * 8 + u) * 8 + k) * 64 + l) * 8) + j] = f16_bits(w1[(size_t)hrow(c, u, l & 15) * C + 32 * k + 8 * (l >> 4) + j]);
+            o.w1f[((((size_t)(c * 8 + u) * KS + k) * 64 + l) * 8) + j] = f16_bits(w1[(size_t)hrow(c, u, l & 15) * C + 32 * k + 8 * (l >> 4) + j]);
     }
   // depthwise taps for P2 lane (wave w, group g): channels x1 a, a + 1 and x2 a, a + 1 with a = 64 c + 8 w + 2 g
   o.dwp.assign((size_t)nc * 8 * 4 * 20, 0u);
@@ -480,17 +524,17 @@ void gffn_pack(int hd, const std::vector<double>& w1, const std::vector<double>&
         d[18] = f16_bits(b(ca)) | ((uint32_t)f16_bits(b(ca + 1)) << 16);
         d[19] = f16_bits(b(hd + ca)) | ((uint32_t)f16_bits(b(hd + ca + 1)) << 16);
       }
-  // W2 fragment (c, w, m, ks): row i = l & 15 -> output channel 32 w + 8 (i >> 2) + 4 m + (i & 3),
-  // k = 64 c + 32 ks + 8 (l >> 4) + j
+  // W2 fragment (c, w, m, ks): row i = l & 15 -> output channel 16 MW w + 4 MW (i >> 2) + 4 m + (i & 3)
+  // (a lane's MW x 4 accumulators are 4 MW consecutive channels), k = 64 c + 32 ks + 8 (l >> 4) + j
   o.w2f.assign((size_t)C * hd, 0);
   for (int c = 0; c < nc; ++c)
-    for (int w = 0; w < 8; ++w)
-      for (int m = 0; m < 2; ++m)
+    for (int w = 0; w < CW; ++w)
+      for (int m = 0; m < MW; ++m)
         for (int ks = 0; ks < 2; ++ks)
           for (int l = 0; l < 64; ++l)
             for (int j = 0; j < 8; ++j) {
-              const int i = l & 15, oc = 32 * w + 8 * (i >> 2) + 4 * m + (i & 3), k = 64 * c + 32 * ks + 8 * (l >> 4) + j;
-              o.w2f[(((((size_t)(c * 8 + w) * 2 + m) * 2 + ks) * 64 + l) * 8) + j] = f16_bits(w2[(size_t)oc * hd + k]);
+              const int i = l & 15, oc = 16 * MW * w + 4 * MW * (i >> 2) + 4 * m + (i & 3), k = 64 * c + 32 * ks + 8 * (l >> 4) + j;
+              o.w2f[(((((size_t)(c * CW + w) * MW + m) * 2 + ks) * 64 + l) * 8) + j] = f16_bits(w2[(size_t)oc * hd + k]);
             }
 }
 

@@ -297,14 +297,15 @@ void launch_tilepd(const TilePdArgs& a, hipStream_t st);
 // gffn.hip: the whole GatedFeedForward block at input width 256, out = x + W2 (gelu(dw H1) * dw H2) + b2
 // with [H1 ; H2] = W1' LN(x) + tb; bf16 in / out, f16 operands on chip, fp32 accumulation
 struct GffnArgs {
-  const void* x; void* out;        // [nimg][H][W][256] bf16, out != x (neighbouring tiles read x's halo)
+  const void* x; void* out;        // [nimg][H][W][C] bf16, out != x (neighbouring tiles read x's halo)
   int nimg, H, W, hd;              // hd = hidden width (multiple of 64)
+  int C;                           // input / output width: 256 (level 3) or 128 (level 2)
   int centred;                     // WithBias LayerNorm (BiasFree: x * rstd)
   const void* w1f;                 // W1' as f16 MFMA A fragments (gffn_pack)
   const float* tbp;                // [2 hd] W1 b_ln + b1 in the fragments' row order
   const uint32_t* dwp;             // depthwise taps + bias as f16 pairs in P2 lane order
   const void* w2f;                 // W2 as f16 MFMA A fragments
-  const float* b2;                 // [256] project_out bias or null
+  const float* b2;                 // [C] project_out bias or null
   int dbg;                         // tools/gfbench ablations (0 in the product path)
 };
 struct GffnHost {                  // gffn_pack output (host), uploaded as four segments
@@ -317,7 +318,7 @@ int64_t gffn_blocks(const GffnArgs& a);
 void launch_gffn(const GffnArgs& a, hipStream_t st);
 // w1 [2 hd][256] (LayerNorm weight folded), tb [2 hd] (or empty), dw9 [9][2 hd] tap-major, dwb [2 hd] (or
 // empty), w2 [256][hd]
-void gffn_pack(int hd, const std::vector<double>& w1, const std::vector<double>& tb, const std::vector<double>& dw9,
+void gffn_pack(int C, int hd, const std::vector<double>& w1, const std::vector<double>& tb, const std::vector<double>& dw9,
                const std::vector<double>& dwb, const std::vector<double>& w2, GffnHost& o);
 
 struct FfnArgs {                   // ffn.hip: out = x + g2 * (W2 gelu(LN-folded W1 x) + b2), bf16, C in {64, 128}

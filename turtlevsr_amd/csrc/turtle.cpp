@@ -215,7 +215,8 @@ struct BlockW {
   DwW a_dw, sab_qk_dw, sab_v_dw, fhr_dw, kv_dw, f_dw, chm_dw6;
   DwW a_dw_qk, a_dw_v;
   size_t ffn_w1f = NONE, ffn_w2f = NONE;                // FeedForward conv4' / conv5 in MFMA fragment order (ffn.hip)
-  size_t gf_w1f = NONE, gf_tbp = NONE, gf_dwp = NONE, gf_w2f = NONE;   // GatedFeedForward at width 256 as one kernel (gffn.hip)                                  // channel attention: qkv_dwconv split (q,k | v) for the dwgemm v path
+  size_t gf_w1f = NONE, gf_tbp = NONE, gf_dwp = NONE, gf_w2f = NONE;
+  int gf_hd = 0;                                  // gffn's hidden width (level 1: 160 padded to 192 with zero weights)   // GatedFeedForward at width 256 as one kernel (gffn.hip)                                  // channel attention: qkv_dwconv split (q,k | v) for the dwgemm v path
   size_t q2_win = NONE, q2_winb = NONE, k2_win = NONE, k2_winb = NONE, sab_tau = NONE;
   size_t wp = NONE, po_bias = NONE, tau = NONE;   // channel-attention projection (fp32) + temperature
 };
@@ -358,6 +359,10 @@ struct TurtleHandle {
   bool gffn = true;                                   // GatedFeedForward at width 256 as one kernel (gffn.hip): the hidden
                                                       // map never in HBM (instead of the pn GEMM + dwgemm pair)
   int gffn_min_blocks = 256;                          // one block per CU: below one full round the GEMM path stays
+  bool gffn_c128 = true;                              // ... also at width 128 (level 2) instead of the fused2 row walk
+                                                      // (1080p: 364 vs 421 us per launch)
+  bool gffn_c64 = false;                              // ... and at width 64 (level 1, hidden padded to a multiple of 64):
+                                                      // measured slower than the fused2 walk (812 vs 607 us), off
   bool dwgemm_cb = true;                              // GatedFeedForward hidden map channel-blocked for dwgemm (STORE_CB16)
   bool down_tile = true;                              // level-1 Downsample as the LDS-tiled conv kernel (spatial.hip down_tile_kernel)
   bool split_out = true;                              // split-bf16 weights for reduce_chan_level1 (bf16 builds)
@@ -662,28 +667,38 @@ static void pack_all(TurtleHandle* h) {
         bw.f_in = pack_gemm(h, pk, dvec(W(h, f + ".project_in.weight")), 2 * b.hidden, c, n2, opt_bias(h, f + ".project_in.bias"));
         bw.f_dw = pack_dw(h, pk, f + ".dwconv", 0, 2 * b.hidden);
         bw.f_out = pack_gemm(h, pk, dvec(W(h, f + ".project_out.weight")), c, b.hidden, "", opt_bias(h, f + ".project_out.bias"));
-        if (pk.bf16 && c == 256 && b.hidden % 64 == 0 && b.hidden <= 768) {
-          // the whole block as one kernel (gffn.hip): f16 fragments of W1 diag(g) and W2, tb = W1 b_ln + b1
+        const int hp = (b.hidden + 63) / 64 * 64;     // gffn hidden width: padded with zero channels (exact)
+        if (pk.bf16 && (c == 256 || c == 128 || c == 64) && (b.hidden % 64 == 0 || c == 64) && hp <= 768) {
+          // the whole block as one kernel (gffn.hip): f16 fragments of W1 diag(g) and W2, tb = W1 b_ln + b1;
+          // hidden channel j of each gate half maps to kernel channel j (j < hd), the rest are zero
           const int hd = b.hidden;
           const auto& w1 = W(h, f + ".project_in.weight");
           const auto& gw = W(h, n2 + ".body.weight");
-          std::vector<double> w1f((size_t)2 * hd * c), tb((size_t)2 * hd, 0.0), dw9((size_t)9 * 2 * hd), dwb;
+          const auto& w2r = W(h, f + ".project_out.weight");
+          std::vector<double> w1f((size_t)2 * hp * c, 0.0), tb((size_t)2 * hp, 0.0), dw9((size_t)9 * 2 * hp, 0.0), dwb,
+              w2p((size_t)c * hp, 0.0);
           const bool lnb = !A.cfg.layernorm_biasfree;
-          for (int n = 0; n < 2 * hd; ++n) {
-            double t = has(h, f + ".project_in.bias") ? W(h, f + ".project_in.bias")[n] : 0.0;
-            for (int k = 0; k < c; ++k) {
-              w1f[(size_t)n * c + k] = (double)w1[(size_t)n * c + k] * gw[k];
-              if (lnb) t += (double)w1[(size_t)n * c + k] * W(h, n2 + ".body.bias")[k];
-            }
-            tb[n] = t;
-          }
+          const bool hasdb = has(h, f + ".dwconv.bias");
+          if (hasdb) dwb.assign((size_t)2 * hp, 0.0);
           const auto& dww = W(h, f + ".dwconv.weight");
-          for (int ch = 0; ch < 2 * hd; ++ch)
-            for (int t = 0; t < 9; ++t) dw9[(size_t)t * 2 * hd + ch] = dww[(size_t)ch * 9 + t];
-          if (has(h, f + ".dwconv.bias")) dwb = dvec(W(h, f + ".dwconv.bias"));
+          for (int half = 0; half < 2; ++half)
+            for (int j = 0; j < hd; ++j) {
+              const int n = half * hd + j, np = half * hp + j;   // reference channel, kernel channel
+              double t = has(h, f + ".project_in.bias") ? W(h, f + ".project_in.bias")[n] : 0.0;
+              for (int k = 0; k < c; ++k) {
+                w1f[(size_t)np * c + k] = (double)w1[(size_t)n * c + k] * gw[k];
+                if (lnb) t += (double)w1[(size_t)n * c + k] * W(h, n2 + ".body.bias")[k];
+              }
+              tb[np] = t;
+              for (int t9 = 0; t9 < 9; ++t9) dw9[(size_t)t9 * 2 * hp + np] = dww[(size_t)n * 9 + t9];
+              if (hasdb) dwb[np] = W(h, f + ".dwconv.bias")[n];
+            }
+          for (int o = 0; o < c; ++o)
+            for (int j = 0; j < hd; ++j) w2p[(size_t)o * hp + j] = w2r[(size_t)o * hd + j];
           GffnHost gh;
-          gffn_pack(hd, w1f, tb, dw9, dwb, dvec(W(h, f + ".project_out.weight")), gh);
+          gffn_pack(c, hp, w1f, tb, dw9, dwb, w2p, gh);
           bw.gf_w1f = pk.raw(gh.w1f); bw.gf_tbp = pk.raw(gh.tbp); bw.gf_dwp = pk.raw(gh.dwp); bw.gf_w2f = pk.raw(gh.w2f);
+          bw.gf_hd = hp;
         }
       } else {
         bw.f_in = pack_gemm(h, pk, dvec(W(h, f + ".conv4.weight")), 2 * c, c, n2, dvec(W(h, f + ".conv4.bias")));
@@ -1009,10 +1024,10 @@ struct Runner {
   }
   // FeedForward in one kernel (ffn.hip): bf16, widths 64 / 128 (shape-only, same in the dry run)
   bool can_ffn(int c) const { return ES == 2 && h->ffn && (c == 64 || c == 128); }
-  // the whole GatedFeedForward at width 256 in one kernel (gffn.hip); out = xin + ffn(norm2(xin))
-  GffnArgs gffn_args(const BlockW& bw, const T* xin, T* out, int hd, int H, int Wd) const {
+  // the whole GatedFeedForward at width 256 (128) in one kernel (gffn.hip); out = xin + ffn(norm2(xin))
+  GffnArgs gffn_args(const BlockW& bw, const T* xin, T* out, int c, int hd, int H, int Wd) const {
     GffnArgs g{};
-    g.x = xin; g.out = out; g.nimg = B; g.H = H; g.W = Wd; g.hd = hd;
+    g.x = xin; g.out = out; g.nimg = B; g.H = H; g.W = Wd; g.hd = (hd + 63) / 64 * 64; g.C = c;   // (= bw.gf_hd)
     g.centred = h->arch.cfg.layernorm_biasfree ? 0 : 1;
     g.w1f = h->ptr(bw.gf_w1f); g.tbp = h->fptr(bw.gf_tbp);
     g.dwp = reinterpret_cast<const uint32_t*>(h->ptr(bw.gf_dwp)); g.w2f = h->ptr(bw.gf_w2f);
@@ -1020,19 +1035,21 @@ struct Runner {
     return g;
   }
   bool can_gffn(const BlockW& bw, int c, int hd, int H, int Wd) const {
-    if (ES != 2 || !h->gffn || c != 256 || hd % 64 || hd > 768) return false;
+    if (ES != 2 || !h->gffn || !(c == 256 || (c == 128 && h->gffn_c128) || (c == 64 && h->gffn_c64))) return false;
+    if ((hd % 64 && c != 64) || (hd + 63) / 64 * 64 > 768) return false;
     if (!dry() && bw.gf_w1f == NONE) return false;
     GffnArgs g{};
     g.nimg = B; g.H = H; g.W = Wd; g.hd = hd;
     return gffn_blocks(g) >= h->gffn_min_blocks;
   }
-  void gffn(const BlockW& bw, const T* xin, T* out, int hd, int H, int Wd) {
+  void gffn(const BlockW& bw, const T* xin, T* out, int c, int hd, int H, int Wd) {
     if (dry()) return;
-    GffnArgs g = gffn_args(bw, xin, out, hd, H, Wd);
+    GffnArgs g = gffn_args(bw, xin, out, c, hd, H, Wd);
     if (!gffn_ok(g)) TFAIL(TURTLE_EINVAL, "gffn: arguments outside the kernel's contract");
     const double px = (double)B * H * Wd;
-    tag("gffn nimg=%d H=%d W=%d hd=%d", B, H, Wd, hd);
-    launch(TURTLE_K_FUSED, ES * px * 2.0 * 256, px * (2.0 * 256 * 2 * hd + 2.0 * hd * 256 + 18.0 * 2 * hd), [&] { launch_gffn(g, st); });
+    if (c == 256) tag("gffn nimg=%d H=%d W=%d hd=%d", B, H, Wd, hd);
+    else tag("gffn nimg=%d H=%d W=%d C=%d hd=%d", B, H, Wd, c, hd);
+    launch(TURTLE_K_FUSED, ES * px * 2.0 * c, px * (2.0 * c * 2 * hd + 2.0 * hd * c + 18.0 * 2 * hd), [&] { launch_gffn(g, st); });
   }
   void ffn(const BlockW& bw, T* x, int64_t P, int c) {
     if (dry()) return;
@@ -1152,11 +1169,11 @@ struct Runner {
     // feed-forward
     if (b.ffn == TURTLE_FFN_GFFW) {
       const int hd = b.hidden;
-      if (can_fuse(c, F_GATE, 2 * hd, hd)) {
-        fused(F_GATE, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, &bw.f_out, x, xalt, {});
+      if (can_gffn(bw, c, hd, H, Wd)) {                // width 256 / 128: the block as one kernel
+        gffn(bw, x, xalt, c, hd, H, Wd);
         std::swap(x, xalt);
-      } else if (can_gffn(bw, c, hd, H, Wd)) {
-        gffn(bw, x, xalt, hd, H, Wd);
+      } else if (can_fuse(c, F_GATE, 2 * hd, hd)) {
+        fused(F_GATE, bw.f_in, bw.f_dw, x, c, 0, c, B, H, Wd, hd, &bw.f_out, x, xalt, {});
         std::swap(x, xalt);
       } else if (h->tilepd_gate && can_tilepd(c, 2 * hd, B, H, Wd)) {
         // LN -> project_in -> dwconv -> gelu gate in one kernel (the 2h-channel hidden map stays on
@@ -1686,6 +1703,8 @@ int turtle_set_option(TurtleHandle* h, const char* name, int value) {
     else if (n == "tilepd_gate") h->tilepd_gate = value != 0;
     else if (n == "gffn") h->gffn = value != 0;
     else if (n == "gffn_min_blocks") h->gffn_min_blocks = (int)value;
+    else if (n == "gffn_c128") h->gffn_c128 = value != 0;
+    else if (n == "gffn_c64") h->gffn_c64 = value != 0;
     else if (n == "tilepd_min_blocks") h->tilepd_min_blocks = (int)value;
     else if (n == "down_tile") h->down_tile = value != 0;
     else if (n == "sab_db") h->sab_db = (int)value;
