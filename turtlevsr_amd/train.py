@@ -50,6 +50,15 @@ def _l2n(x, dim):
     return x / x.norm(dim=dim, keepdim=True).clamp_min(L2_EPS)
 
 
+def _act_dt(t: torch.Tensor) -> torch.dtype:
+    """The dtype of a per-image weight set the HIP conv1x1 applies to ``t``: its GEMM dtype - fp32 for an
+    fp32 graph, bf16 under autocast (the 1x1 GEMMs run bf16 for fp16 autocast too, train_ops._gemm_dt) -
+    so the weights are rounded once."""
+    if (torch.is_autocast_enabled() and t.is_cuda) or t.dtype != torch.float32:
+        return torch.bfloat16
+    return torch.float32
+
+
 def _res(res):
     """The residual keyword for an op set's conv1x1 (absent when there is none: ATen op sets)."""
     return {} if res is None else {"res": res}
@@ -301,9 +310,13 @@ class TrainGraph:
             qk, v = _split(qkv, 2 * c, c, sink=sink)
             ch = c // heads
             kw = lambda off: {} if sink is None else {"sink": (sink, off)}
-            a = torch.softmax(ops.norm_gram(qk, heads, **kw(0)) * m.temperature, dim=-1)
+            Gn = ops.norm_gram(qk, heads, **kw(0))
             wp = m.project_out.weight.reshape(c, heads, ch)
-            weff = torch.einsum("ohi,bhij->bohj", wp, a).reshape(b, c, c)
+            if hasattr(ops, "attn_weff"):           # softmax + W_eff as one op with its own backward
+                weff = ops.attn_weff(Gn, m.temperature, wp, _act_dt(v))
+            else:
+                a = torch.softmax(Gn * m.temperature, dim=-1)
+                weff = torch.einsum("ohi,bhij->bohj", wp, a).reshape(b, c, c)
             return ops.conv1x1(v, weff, m.project_out.bias, **kw(2 * c), **_res(res)), None, None
         if ntc is None and kc is None and vc is None and hasattr(ops, "gram"):
             # on the op set's kernels: Gram of the raw q, k over HW (per head) divided by the L2
@@ -370,9 +383,12 @@ class TrainGraph:
         L = (t + 1) * ch
         G = ops.cross_gram(qn, K)                                           # [b, c, heads * L]
         Gh = G.view(b, heads, ch, heads, L).diagonal(dim1=1, dim2=3).permute(0, 3, 1, 2)   # [b, heads, ch, L]
-        a = torch.softmax(Gh * m.temperature, dim=-1)
         wp = m.project_out.weight.reshape(c, heads, ch)
-        weff = torch.einsum("ohi,bhik->bohk", wp, a).reshape(b, c, heads * L)
+        if hasattr(ops, "attn_weff"):
+            weff = ops.attn_weff(Gh, m.temperature, wp, _act_dt(V))
+        else:
+            a = torch.softmax(Gh * m.temperature, dim=-1)
+            weff = torch.einsum("ohi,bhik->bohk", wp, a).reshape(b, c, heads * L)
         out = ops.conv1x1(V, weff, m.project_out.bias, **_res(res))
         if ntc is None:
             return out, None, None

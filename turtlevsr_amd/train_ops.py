@@ -957,6 +957,43 @@ class _NormGram(torch.autograd.Function):
         return dqk.to(ctx.in_dt), None, None
 
 
+class _AttnWeff(torch.autograd.Function):
+    """The channel-attention / FHR finalize (turtle_t1_arch.py:697-702, 240-244): A = softmax(G * t) per
+    head (G [b, heads, ch, L] fp32, t = the temperature [heads, 1, 1]) and the per-image weight set
+    W_eff[b, o, (h, k)] = sum_i wp[o, h, i] A[b, h, i, k] (wp = project_out's weight as [c, heads, ch]) that
+    the conv1x1 applies to v (A v followed by project_out as one GEMM), in fp32 with a hand-written
+    backward: one op chain instead of autograd's softmax / einsum / cast / view nodes (~20 small
+    launches per site and step)."""
+
+    @staticmethod
+    def forward(ctx, G, temp, wp, out_dtype):
+        Gf = G.float()
+        t = temp.float()
+        a = torch.softmax(Gf * t, dim=-1)
+        weff = torch.einsum("ohi,bhik->bohk", wp.float(), a)
+        ctx.save_for_backward(Gf, t, wp, a)
+        ctx.g_dt, ctx.t_dt, ctx.w_dt = G.dtype, temp.dtype, wp.dtype
+        b, h, ch, L = G.shape
+        return weff.reshape(b, wp.shape[0], h * L).to(out_dtype)
+
+    @staticmethod
+    def backward(ctx, dweff):
+        Gf, t, wp, a = ctx.saved_tensors
+        b, h, ch, L = Gf.shape
+        dW = dweff.float().view(b, wp.shape[0], h, L)
+        dG = dt = dwp = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            da = torch.einsum("ohi,bohk->bhik", wp.float(), dW)
+            ds = a * (da - (da * a).sum(-1, keepdim=True))                     # softmax backward
+            if ctx.needs_input_grad[0]:
+                dG = (ds * t).to(ctx.g_dt)
+            if ctx.needs_input_grad[1]:
+                dt = (ds * Gf).sum(dim=(0, 2, 3)).view(t.shape).to(ctx.t_dt)
+        if ctx.needs_input_grad[2]:
+            dwp = torch.einsum("bohk,bhik->ohi", dW, a).to(ctx.w_dt)
+        return dG, dt, dwp, None
+
+
 def _act_dtype(x: torch.Tensor) -> torch.dtype:
     if torch.is_autocast_enabled("cuda") and x.dtype == torch.float32:
         return torch.get_autocast_dtype("cuda")
@@ -1049,6 +1086,11 @@ class HipOps:
     @staticmethod
     def gram(q, k, heads: int):
         return _Gram.apply(_act(q), _act(k), heads)
+
+    @staticmethod
+    def attn_weff(G, temp, wp, out_dtype):
+        """softmax(G * temp) per head and W_eff = project_out . blockdiag(A) as one op (_AttnWeff)."""
+        return _AttnWeff.apply(G, temp, wp, out_dtype)
 
     @staticmethod
     def norm_gram(qk, heads: int, sink=None):
