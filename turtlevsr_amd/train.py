@@ -51,11 +51,9 @@ def _l2n(x, dim):
 
 
 def _act_dt(t: torch.Tensor) -> torch.dtype:
-    """The dtype of a per-image weight set the HIP conv1x1 applies to ``t``: its GEMM dtype - fp32 for an
-    fp32 graph, bf16 under autocast (the 1x1 GEMMs run bf16 for fp16 autocast too, train_ops._gemm_dt) -
-    so the weights are rounded once."""
-    if (torch.is_autocast_enabled() and t.is_cuda) or t.dtype != torch.float32:
-        return torch.bfloat16
+    """The dtype the attention finalize hands its per-image weight set to the HIP conv1x1 in: fp32 - the
+    conv casts it to its GEMM dtype once (train_ops._weight_cast), its weight gradient comes back in
+    fp32 (the reduction GEMM's output) and the finalize's backward needs no cast either way."""
     return torch.float32
 
 
